@@ -1,0 +1,122 @@
+/*
+ * hbam_oracle.h -- CPU restatement of Hadoop-BAM's BAM read path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load this library, and only as the checker
+ * (or the timed CPU baseline).  The product (libhbam.so) never links it.
+ *
+ * Reference: /root/reference (huangzhibo/Hadoop-BAM 7.9.2-SNAPSHOT, Java) plus
+ * htsjdk 2.13.2 (pom.xml:43), which is NOT vendored in the reference.  Every
+ * function cites the reference file:line it follows; htsjdk behaviour is
+ * marked [htsjdk] and restated from its published semantics.
+ *
+ * Parity pins (see DESIGN.md "Oracle"):
+ *   - inflate: zlib 1.2.x raw inflate (the library java.util.zip.Inflater
+ *     wraps), checked against the fixtures' plain-text twins;
+ *   - first-record voff of test.bam == 0x196a (TestBAMSplitGuesser.java:21);
+ *   - BGZF block boundaries of the VCF fixtures (TestBGZFSplitGuesser.java:36);
+ *   - keys / .splitting-bai: cross-checked against an independent Python
+ *     restatement (oracle/py_oracle.py); no reference golden exists.
+ */
+#ifndef HBAM_ORACLE_H
+#define HBAM_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes: identical numbering to include/hbam.h */
+#define ORC_OK 0
+#define ORC_E_FORMAT 1 /* SAMFormatException */
+#define ORC_E_TRUNC 2  /* FileTruncatedException / RuntimeEOFException */
+#define ORC_E_ARG 3    /* IllegalArgumentException */
+#define ORC_E_IO 4     /* IOException / RuntimeIOException */
+#define ORC_E_NOMEM 7
+
+typedef struct {
+  uint64_t coff;   /* compressed offset of the block in the file */
+  uint32_t csize;  /* BSIZE + 1 */
+  uint32_t isize;  /* ISIZE footer */
+  uint32_t crc;    /* CRC32 footer */
+  uint32_t pad;
+  uint64_t ustart; /* offset of the block's first byte in the inflated stream */
+} orc_block;
+
+typedef struct orc_stream orc_stream;
+
+/* Walk + inflate every BGZF block of a whole file (htsjdk
+ * BlockCompressedInputStream.readBlock / BlockGunzipper.unzipBlock) and parse
+ * the BAM header (htsjdk BAMFileReader.readHeader; SplittingBAMIndexer.java:292-328).
+ * parse_header=0 treats the input as plain BGZF (VCF/BCF fixtures). */
+int orc_open(const uint8_t *file, uint64_t len, int check_crc, int parse_header,
+             orc_stream **out);
+void orc_close(orc_stream *s);
+const char *orc_error(const orc_stream *s);
+
+uint64_t orc_nblocks(const orc_stream *s);
+const orc_block *orc_blocks(const orc_stream *s);
+const uint8_t *orc_data(const orc_stream *s);
+uint64_t orc_data_len(const orc_stream *s);
+int32_t orc_n_ref(const orc_stream *s);
+int32_t orc_l_text(const orc_stream *s);
+uint64_t orc_header_end(const orc_stream *s);      /* inflated-stream position */
+uint64_t orc_first_record_voff(const orc_stream *s);
+uint64_t orc_voff_of(const orc_stream *s, uint64_t pos); /* normalized voff */
+
+/* Decoded records of one span, SoA (LazyBAMRecordFactory.java:37-50 field set). */
+typedef struct {
+  uint64_t n;
+  int32_t *ref_id, *pos, *l_seq, *next_ref_id, *next_pos, *tlen;
+  uint8_t *l_read_name, *mapq;
+  uint16_t *bin, *n_cigar, *flag;
+  int64_t *key;
+  uint64_t *voff, *offset; /* offset = inflated-stream position of block_size */
+  uint32_t *rest_len;
+} orc_records;
+
+/* BAMRecordReader.initialize/nextKeyValue over FileVirtualSplit [vstart,vend)
+ * (BAMRecordReader.java:123-232 + [htsjdk] BAMFileReader span iterator). */
+int orc_decode_span(orc_stream *s, uint64_t vstart, uint64_t vend, orc_records *out);
+void orc_records_free(orc_records *r);
+
+/* SplittingBAMIndexer.index (SplittingBAMIndexer.java:248-368). */
+int orc_splitting_index(orc_stream *s, uint64_t file_size, int32_t granularity,
+                        uint8_t **out, uint64_t *out_len);
+void orc_free(void *p);
+
+/* MurmurHash3.murmurhash3(byte[],int) (util/MurmurHash3.java:32-102). */
+int64_t orc_murmurhash3(const uint8_t *key, uint64_t len, int32_t seed);
+/* BAMRecordReader.getKey(SAMRecord) (BAMRecordReader.java:81-111) for an
+ * undecoded BAM record. */
+int64_t orc_get_key(int32_t ref_id, int32_t pos0, uint16_t flag,
+                    const uint8_t *var, uint32_t var_len);
+
+/* BaseSplitGuesser.guessNextBGZFPos (BaseSplitGuesser.java:31-108) over a byte
+ * array; returns 1 and fills pos/size if found. */
+int orc_guess_bgzf_pos(const uint8_t *arr, uint64_t alen, int32_t p, int32_t end,
+                       int32_t *pos, int32_t *size);
+/* BAMSplitGuesser.guessNextBAMRecordStart (BAMSplitGuesser.java:108-235). */
+int orc_guess_record_start(orc_stream *s, const uint8_t *file, uint64_t flen,
+                           uint64_t beg, uint64_t end, uint64_t *out);
+
+/* BGZFSplitGuesser.guessNextBGZFBlockStart (util/BGZFSplitGuesser.java:64-112)
+ * restated for the TestBGZFSplitGuesser pins. */
+int64_t orc_guess_next_bgzf_block_start(const uint8_t *file, uint64_t flen,
+                                        uint64_t beg, uint64_t end);
+
+/* BAMInputFormat split planning for one file (BAMInputFormat.java:264-318,
+ * 469-530).  sbi may be NULL (-> probabilistic splits). */
+int orc_get_splits(orc_stream *s, const uint8_t *file, uint64_t flen,
+                   const uint64_t *starts, const uint64_t *lengths, uint64_t n,
+                   const uint8_t *sbi, uint64_t sbi_len, uint64_t *vstarts,
+                   uint64_t *vends, uint64_t *nout);
+
+/* zlib crc32, for tests */
+uint32_t orc_crc32(const uint8_t *p, uint64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,204 @@
+"""ctypes binding of the C oracle (oracle/liborc.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, always as the checker / CPU baseline, never as the
+thing measured or shipped.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liborc.so")
+        if not os.path.exists(path):
+            raise RuntimeError("oracle/liborc.so not built: run `make -C oracle`")
+        L = C.CDLL(path)
+        u64, i32, i64, u32 = C.c_uint64, C.c_int32, C.c_int64, C.c_uint32
+        P = C.c_void_p
+        L.orc_open.argtypes = [P, u64, C.c_int, C.c_int, C.POINTER(P)]
+        L.orc_close.argtypes = [P]
+        L.orc_error.argtypes = [P]
+        L.orc_error.restype = C.c_char_p
+        for n in ("orc_nblocks", "orc_data_len", "orc_header_end", "orc_first_record_voff"):
+            getattr(L, n).argtypes = [P]
+            getattr(L, n).restype = u64
+        L.orc_voff_of.argtypes = [P, u64]
+        L.orc_voff_of.restype = u64
+        L.orc_blocks.argtypes = [P]
+        L.orc_blocks.restype = P
+        L.orc_data.argtypes = [P]
+        L.orc_data.restype = P
+        L.orc_n_ref.argtypes = [P]
+        L.orc_n_ref.restype = i32
+        L.orc_l_text.argtypes = [P]
+        L.orc_l_text.restype = i32
+        L.orc_decode_span.argtypes = [P, u64, u64, P]
+        L.orc_records_free.argtypes = [P]
+        L.orc_splitting_index.argtypes = [P, u64, i32, C.POINTER(P), C.POINTER(u64)]
+        L.orc_free.argtypes = [P]
+        L.orc_murmurhash3.argtypes = [P, u64, i32]
+        L.orc_murmurhash3.restype = i64
+        L.orc_get_key.argtypes = [i32, i32, C.c_uint16, P, u32]
+        L.orc_get_key.restype = i64
+        L.orc_guess_record_start.argtypes = [P, P, u64, u64, u64, C.POINTER(u64)]
+        L.orc_guess_next_bgzf_block_start.argtypes = [P, u64, u64, u64]
+        L.orc_guess_next_bgzf_block_start.restype = i64
+        L.orc_get_splits.argtypes = [P, P, u64, P, P, u64, P, u64, P, P, C.POINTER(u64)]
+        L.orc_crc32.argtypes = [P, u64]
+        L.orc_crc32.restype = u32
+        _LIB = L
+    return _LIB
+
+
+BLOCK_DTYPE = np.dtype([("coff", "<u8"), ("csize", "<u4"), ("isize", "<u4"),
+                        ("crc", "<u4"), ("pad", "<u4"), ("ustart", "<u8")])
+
+RECORD_FIELDS = [
+    ("ref_id", np.int32), ("pos", np.int32), ("l_seq", np.int32), ("next_ref_id", np.int32),
+    ("next_pos", np.int32), ("tlen", np.int32), ("l_read_name", np.uint8), ("mapq", np.uint8),
+    ("bin", np.uint16), ("n_cigar", np.uint16), ("flag", np.uint16), ("key", np.int64),
+    ("voff", np.uint64), ("offset", np.uint64), ("rest_len", np.uint32),
+]
+
+
+class _Records(C.Structure):
+    _fields_ = [("n", C.c_uint64)] + [(name, C.c_void_p) for name, _ in RECORD_FIELDS]
+
+
+class OracleError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"oracle error {code}: {msg}")
+        self.code = code
+
+
+class Stream:
+    """A whole BGZF file inflated by zlib + BAM header parse (the oracle)."""
+
+    def __init__(self, data: bytes, check_crc=False, parse_header=True):
+        L = lib()
+        self._buf = C.create_string_buffer(bytes(data), len(data))
+        self.file = bytes(data)
+        self._h = C.c_void_p()
+        rc = L.orc_open(self._buf, len(data), int(check_crc), int(parse_header), C.byref(self._h))
+        if rc != 0:
+            msg = L.orc_error(self._h).decode()
+            L.orc_close(self._h)
+            self._h = None
+            raise OracleError(rc, msg)
+
+    def close(self):
+        if self._h:
+            lib().orc_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def blocks(self):
+        L = lib()
+        n = L.orc_nblocks(self._h)
+        if n == 0:
+            return np.zeros(0, BLOCK_DTYPE)
+        raw = C.string_at(L.orc_blocks(self._h), n * BLOCK_DTYPE.itemsize)
+        return np.frombuffer(raw, BLOCK_DTYPE).copy()
+
+    @property
+    def data(self) -> bytes:
+        L = lib()
+        n = L.orc_data_len(self._h)
+        return C.string_at(L.orc_data(self._h), n) if n else b""
+
+    @property
+    def n_ref(self):
+        return lib().orc_n_ref(self._h)
+
+    @property
+    def header_end(self):
+        return lib().orc_header_end(self._h)
+
+    @property
+    def first_record_voff(self):
+        return lib().orc_first_record_voff(self._h)
+
+    def voff_of(self, pos):
+        return lib().orc_voff_of(self._h, pos)
+
+    def decode_span(self, vstart, vend):
+        """Returns (status, dict of numpy columns)."""
+        L = lib()
+        r = _Records()
+        rc = L.orc_decode_span(self._h, vstart, vend, C.byref(r))
+        out = {}
+        for name, dt in RECORD_FIELDS:
+            p = getattr(r, name)
+            if r.n and p:
+                out[name] = np.frombuffer(C.string_at(p, r.n * np.dtype(dt).itemsize), dt).copy()
+            else:
+                out[name] = np.zeros(0, dt)
+        L.orc_records_free(C.byref(r))
+        return rc, out
+
+    def decode_all(self):
+        return self.decode_span(self.first_record_voff, (1 << 64) - 1)
+
+    def splitting_index(self, granularity):
+        L = lib()
+        p = C.c_void_p()
+        n = C.c_uint64()
+        rc = L.orc_splitting_index(self._h, len(self.file), granularity, C.byref(p), C.byref(n))
+        if rc != 0:
+            raise OracleError(rc, L.orc_error(self._h).decode())
+        b = C.string_at(p, n.value)
+        L.orc_free(p)
+        return b
+
+    def guess_record_start(self, beg, end):
+        L = lib()
+        out = C.c_uint64()
+        rc = L.orc_guess_record_start(self._h, self._buf, len(self.file), beg, end, C.byref(out))
+        if rc != 0:
+            raise OracleError(rc, L.orc_error(self._h).decode())
+        return out.value
+
+    def get_splits(self, starts, lengths, sbi=None):
+        L = lib()
+        n = len(starts)
+        s = (C.c_uint64 * n)(*starts)
+        ln = (C.c_uint64 * n)(*lengths)
+        vs = (C.c_uint64 * max(n, 1))()
+        ve = (C.c_uint64 * max(n, 1))()
+        nout = C.c_uint64()
+        sbuf = C.create_string_buffer(sbi, len(sbi)) if sbi is not None else None
+        rc = L.orc_get_splits(self._h, self._buf, len(self.file), s, ln, n, sbuf,
+                              len(sbi) if sbi is not None else 0, vs, ve, C.byref(nout))
+        if rc != 0:
+            raise OracleError(rc, L.orc_error(self._h).decode())
+        return [(vs[i], ve[i]) for i in range(nout.value)]
+
+
+def murmurhash3(data: bytes, seed=0):
+    return lib().orc_murmurhash3(C.c_char_p(bytes(data)), len(data), seed)
+
+
+def get_key(ref_id, pos0, flag, var: bytes):
+    return lib().orc_get_key(ref_id, pos0, flag, C.c_char_p(bytes(var)), len(var))
+
+
+def guess_next_bgzf_block_start(file: bytes, beg, end):
+    buf = C.create_string_buffer(file, len(file))
+    return lib().orc_guess_next_bgzf_block_start(buf, len(file), beg, end)
+
+
+def crc32(b: bytes):
+    return lib().orc_crc32(C.c_char_p(bytes(b)), len(b))

@@ -1,0 +1,175 @@
+"""Independent pure-Python restatement of the key path (TEST INFRASTRUCTURE ONLY).
+
+Written separately from oracle/hbam_oracle.c so that the two restatements can
+cross-check each other on test.bam (no reference golden exists
+for keys).  Pure-Python loops: small inputs only.
+
+  murmurhash3  <- util/MurmurHash3.java:32-102 (quirk at :59), fmix :173-180
+  get_key      <- BAMRecordReader.java:81-121
+  records      <- [htsjdk] BAMRecordCodec.decode chain from the header end
+  splitting_index <- SplittingBAMIndexer.java:248-290
+"""
+import struct
+import zlib
+
+M64 = (1 << 64) - 1
+
+
+def _rotl(x, r):
+    return ((x << r) | (x >> (64 - r))) & M64
+
+
+def _fmix(k):
+    k ^= k >> 33
+    k = (k * 0xFF51AFD7ED558CCD) & M64
+    k ^= k >> 33
+    k = (k * 0xC4CEB9FE1A85EC53) & M64
+    k ^= k >> 33
+    return k
+
+
+def _signed64(x):
+    return x - (1 << 64) if x >> 63 else x
+
+
+def _signed32(x):
+    x &= 0xFFFFFFFF
+    return x - (1 << 32) if x >> 31 else x
+
+
+def murmurhash3(key: bytes, seed: int = 0) -> int:
+    """Java long returned by MurmurHash3.murmurhash3(byte[], int)."""
+    c1, c2 = 0x87C37B91114253D5, 0x4CF5AD432745937F
+    h1 = h2 = seed & M64
+    n = len(key)
+    nb = n // 16
+    for i in range(nb):
+        k1, k2 = struct.unpack_from("<QQ", key, 16 * i)
+        k1 = (k1 * c1) & M64
+        k1 = _rotl(k1, 31)
+        k1 = (k1 * c2) & M64
+        h1 ^= k1
+        h1 = _rotl(h1, 27)
+        h1 = (h1 + h2) & M64
+        h1 = (h1 * 5 + 0x52DCE729) & M64
+        k2 = (k2 * c2) & M64
+        k2 = _rotl(k2, 33)
+        k2 = (k2 * c1) & M64
+        h2 ^= k2
+        h2 = ((h2 << 31) | (h1 >> 33)) & M64  # the :59 quirk
+        h2 = (h2 + h1) & M64
+        h2 = (h2 * 5 + 0x38495AB5) & M64
+    tail = key[16 * nb:]
+    r = n & 15
+    k1 = k2 = 0
+    if r > 8:
+        for j in range(8, r):
+            k2 ^= tail[j] << (8 * (j - 8))
+        k2 = (k2 * c2) & M64
+        k2 = _rotl(k2, 33)
+        k2 = (k2 * c1) & M64
+        h2 ^= k2
+    if r > 0:
+        for j in range(0, min(r, 8)):
+            k1 ^= tail[j] << (8 * j)
+        k1 = (k1 * c1) & M64
+        k1 = _rotl(k1, 31)
+        k1 = (k1 * c2) & M64
+        h1 ^= k1
+    h1 ^= n
+    h2 ^= n
+    h1 = (h1 + h2) & M64
+    h2 = (h2 + h1) & M64
+    h1 = _fmix(h1)
+    h2 = _fmix(h2)
+    h1 = (h1 + h2) & M64
+    return _signed64(h1)
+
+
+def get_key(ref_id, pos0, flag, var: bytes) -> int:
+    start = _signed32(pos0 + 1)
+    if not ((flag & 4) or ref_id < 0 or start < 0):
+        return _signed64(((ref_id << 32) & M64) | (_signed32(start - 1) & M64))
+    h = _signed32(murmurhash3(var, 0))
+    return _signed64(((0x7FFFFFFF << 32) | (h & M64)) & M64)
+
+
+def blocks(data: bytes):
+    """[(coff, csize, isize)] by walking BSIZE (no framing checks beyond magic)."""
+    out, p = [], 0
+    while p < len(data):
+        assert data[p:p + 4] == b"\x1f\x8b\x08\x04", p
+        bsize = struct.unpack_from("<H", data, p + 16)[0] + 1
+        isize = struct.unpack_from("<I", data, p + bsize - 4)[0]
+        out.append((p, bsize, isize))
+        p += bsize
+    return out
+
+
+def inflate(data: bytes):
+    bl = blocks(data)
+    parts, ustart = [], []
+    u = 0
+    for coff, csize, isize in bl:
+        raw = zlib.decompressobj(-15).decompress(data[coff + 18:coff + csize - 8])
+        assert len(raw) == isize
+        parts.append(raw)
+        ustart.append(u)
+        u += isize
+    return bl, ustart, b"".join(parts)
+
+
+def voff(bl, ustart, pos):
+    for k, (coff, csize, isize) in enumerate(bl):
+        if ustart[k] == pos:
+            return coff << 16
+        if ustart[k] < pos < ustart[k] + isize:
+            return (coff << 16) | (pos - ustart[k])
+    coff, csize, _ = bl[-1]
+    return (coff + csize) << 16
+
+
+def records(data: bytes):
+    """[(voff, key)] for every record of a well-formed BAM (no empty mid blocks)."""
+    bl, ustart, u = inflate(data)
+    assert u[:4] == b"BAM\x01"
+    l_text = struct.unpack_from("<i", u, 4)[0]
+    p = 8 + l_text
+    n_ref = struct.unpack_from("<i", u, p)[0]
+    p += 4
+    for _ in range(n_ref):
+        ln = struct.unpack_from("<i", u, p)[0]
+        p += 4 + ln + 4
+    out = []
+    while len(u) - p >= 4:
+        bs = struct.unpack_from("<i", u, p)[0]
+        ref, pos0 = struct.unpack_from("<ii", u, p + 4)
+        flag = struct.unpack_from("<H", u, p + 18)[0]
+        out.append((voff(bl, ustart, p), get_key(ref, pos0, flag, u[p + 36:p + 4 + bs])))
+        p += 4 + bs
+    return out
+
+
+def splitting_index(data: bytes, g: int) -> bytes:
+    bl, ustart, u = inflate(data)
+    l_text = struct.unpack_from("<i", u, 4)[0]
+    p = 8 + l_text
+    n_ref = struct.unpack_from("<i", u, p)[0]
+    p += 4
+    for _ in range(n_ref):
+        ln = struct.unpack_from("<i", u, p)[0]
+        p += 4 + ln + 4
+    ent = [voff(bl, ustart, p)]
+    i = 0
+    while p < len(u):
+        ptr = voff(bl, ustart, p)
+        bs = struct.unpack_from("<i", u, p)[0]
+        p += 4
+        i += 1
+        if i == g:
+            i = 0
+            ent.append(ptr)
+        if bs > 0:
+            p += bs
+    ent.append(len(data) << 16)
+    return b"".join(struct.pack(">Q", v) for v in ent)
