@@ -1,0 +1,170 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X BAM read hot path (BASELINE.json metric).
+
+One "step" = one full pass of the hot path over one synthetic BAM resident in
+HBM: BGZF block discovery -> inflate (Huffman phase + LZ77 phase) -> record
+boundary scan -> fused field decode + sort keys + voffs.  Workload: config C2,
+a synthetic 10M x 150 bp paired-end coordinate-sorted BAM (generated on the
+box, zlib level 5 as htsjdk writes).  With N GPUs each rank owns one C2-sized
+BGZF shard (weak scaling; shards are independent, no data-path collective).
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "hadoop-bam_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+METRIC = "uncompressed BAM decode GB/s + records/sec per GPU and 8-GPU node"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(data, info, seconds):
+    """Oracle (zlib inflate + htsjdk-rule record chain + keys) on the host, one
+    thread, on a prefix of the same BAM sized to ~`seconds` of work."""
+    import orc
+    import numpy as np
+    # calibrate on a small prefix (whole BGZF blocks), then scale up
+    blocks = []
+    p = 0
+    while p < len(data):
+        bs = int.from_bytes(data[p + 16:p + 18], "little") + 1
+        blocks.append((p, bs))
+        p += bs
+    def run(nb):
+        end = blocks[nb - 1][0] + blocks[nb - 1][1]
+        t = time.perf_counter()
+        s = orc.Stream(data[:end])
+        rc, r = s.decode_span(s.first_record_voff, (1 << 64) - 1)
+        dt = time.perf_counter() - t
+        return dt, len(s.data), len(r["key"])
+    nb = min(len(blocks), 200)
+    dt, u, n = run(nb)
+    target = max(nb, min(len(blocks), int(nb * seconds / max(dt, 1e-3))))
+    dt, u, n = run(target)
+    return {"value": round(u / dt / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "records_per_s": round(n / dt, 1),
+            "sample": f"first {target} BGZF blocks ({u} inflated bytes, {n} records) of the same C2 BAM, "
+                      f"oracle/hbam_oracle.c (system zlib) single thread, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--records", type=int, default=10_000_000)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--save-bam", default=None)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+
+    import numpy as np
+    import hbam
+    from hbam import synth
+
+    t0 = time.time()
+    data, info = synth.make_bam(args.records, seed=0x48424D00 + 7919 * rank, as_numpy=True)
+    log(f"[rank {rank}] generated C2 shard: {info} in {time.time() - t0:.1f}s")
+    if args.save_bam and rank == 0:
+        data.tofile(args.save_bam)
+
+    g = hbam.Gpu(local_rank)
+    g.load(data)
+
+    def barrier():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        st = g.run(timing=True)
+    barrier()
+    stats = []
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        stats.append(g.run(timing=True))
+    barrier()
+    elapsed = time.perf_counter() - t
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        tot = torch.tensor([float(info["uncompressed"]), float(stats[-1]["records"]), float(info["compressed"])],
+                           dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(tot)
+        u_all, n_all, c_all = (float(x) for x in tot.tolist())
+    else:
+        u_all, n_all, c_all = float(info["uncompressed"]), float(stats[-1]["records"]), float(info["compressed"])
+
+    st = stats[-1]
+    assert st["records"] == args.records, (st["records"], args.records)
+    ms_step = elapsed / args.steps * 1e3
+    value = u_all * args.steps / elapsed / 1e9
+
+    # dominant kernel pair: inflate (phase A huff + phase B lz77), HIP events on the pipeline stream
+    infl_ms = sum(s["ms_huff"] + s["ms_lz77"] for s in stats) / len(stats)
+    huff_ms = sum(s["ms_huff"] for s in stats) / len(stats)
+    alg_bytes = info["compressed"] + info["uncompressed"]  # C read + U written per launch pair
+    achieved = alg_bytes / (infl_ms * 1e-3) / 1e9
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (tools/gen_synth_bam.c, zlib level 5 BGZF, generated on the box)",
+        "config": {"workload": "C2: synthetic 10M x 150bp paired-end coordinate-sorted BAM per GPU",
+                   "records_per_gpu": args.records, "compressed_bytes_per_gpu": info["compressed"],
+                   "uncompressed_bytes_per_gpu": info["uncompressed"], "bgzf_blocks_per_gpu": info["blocks"],
+                   "parallelism": f"bgzf-shard x{world}"},
+        "records_per_s": round(n_all * args.steps / elapsed, 1),
+        "stages_ms": {k: round(st[k], 3) for k in ("ms_locate", "ms_inflate", "ms_huff", "ms_lz77", "ms_chain",
+                                                    "ms_decode", "ms_total")},
+        "roofline": {"bound": "hbm", "kernel": "k_inflate_huff+k_inflate_lz77",
+                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "avg_launch_ms": round(infl_ms, 3), "huff_ms": round(huff_ms, 3),
+                     "alg_bytes_per_launch": alg_bytes},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(data.tobytes(), info, args.cpu_seconds)
+        except Exception as e:  # reported, never substituted for the GPU number
+            out["cpu_baseline"] = {"error": str(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,372 @@
+// hbam_abi.cpp -- extern "C" boundary (include/hbam.h) over the C++ mirror.
+#include "../../include/hbam.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "hbam_host.h"
+
+using hadoop_bam::BAMInputFormat;
+using hadoop_bam::BamFile;
+using hadoop_bam::BAMRecordReader;
+using hadoop_bam::FileSplit;
+using hadoop_bam::FileVirtualSplit;
+using hadoop_bam::SplittingBAMIndexer;
+
+struct hbam_ctx {
+  std::unique_ptr<BamFile> f;
+  std::string err;
+  BAMRecordReader::Host batch;
+  std::string text;
+};
+
+struct hbam_gpu {
+  std::unique_ptr<hbam::Pipeline> p;
+  std::string err;
+  uint64_t first_pos = 0;  // inflated-stream position of the first record
+  hbam::SpanDev span;
+};
+
+namespace {
+std::string g_open_err;
+
+int open_common(const void* data, uint64_t len, const hbam_opts* opts, bool header, hbam_ctx** out) {
+  *out = nullptr;
+  hbam_opts o{};
+  if (opts) o = *opts;
+  auto* c = new hbam_ctx();
+  std::string err;
+  int rc = BamFile::open(static_cast<const uint8_t*>(data), len, o.device, header, o.check_crc != 0, &c->f, &err);
+  if (rc != HBAM_OK) {
+    g_open_err = err;
+    c->err = err;
+    *out = c;  // caller may read hbam_last_error, then must hbam_close
+    return rc;
+  }
+  *out = c;
+  return HBAM_OK;
+}
+
+bool read_file(const char* path, std::vector<uint8_t>* buf, std::string* err) {
+  FILE* fp = fopen(path, "rb");
+  if (!fp) {
+    *err = std::string("cannot open ") + path;
+    return false;
+  }
+  fseek(fp, 0, SEEK_END);
+  long n = ftell(fp);
+  fseek(fp, 0, SEEK_SET);
+  buf->resize(n > 0 ? (size_t)n : 0);
+  size_t got = n > 0 ? fread(buf->data(), 1, (size_t)n, fp) : 0;
+  fclose(fp);
+  if ((long)got != n) {
+    *err = std::string("short read on ") + path;
+    return false;
+  }
+  return true;
+}
+}  // namespace
+
+extern "C" {
+
+int32_t hbam_abi_version(void) { return HBAM_ABI_VERSION; }
+
+int hbam_open_mem(const void* data, uint64_t len, const hbam_opts* opts, hbam_ctx** out) {
+  return open_common(data, len, opts, true, out);
+}
+
+int hbam_open_bgzf(const void* data, uint64_t len, const hbam_opts* opts, hbam_ctx** out) {
+  return open_common(data, len, opts, false, out);
+}
+
+int hbam_open(const char* path, const hbam_opts* opts, hbam_ctx** out) {
+  std::vector<uint8_t> buf;
+  std::string err;
+  if (!read_file(path, &buf, &err)) {
+    *out = new hbam_ctx();
+    (*out)->err = err;
+    return HBAM_E_IO;
+  }
+  return open_common(buf.data(), buf.size(), opts, true, out);
+}
+
+void hbam_close(hbam_ctx* ctx) { delete ctx; }
+
+const char* hbam_last_error(hbam_ctx* ctx) { return ctx ? ctx->err.c_str() : g_open_err.c_str(); }
+
+void hbam_free(void* p) { free(p); }
+
+int hbam_header(hbam_ctx* ctx, hbam_header_info* out) {
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  BamFile& f = *ctx->f;
+  out->n_ref = f.n_ref();
+  out->l_text = f.l_text();
+  out->first_record_voff = f.first_record_voff();
+  out->file_size = f.file_size();
+  out->n_blocks = f.pipe().blocks().size();
+  out->uncompressed_size = f.pipe().total_u();
+  out->text = f.text().c_str();
+  return HBAM_OK;
+}
+
+int hbam_ref(hbam_ctx* ctx, int32_t i, const char** name, int32_t* length) {
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  if (i < 0 || i >= ctx->f->n_ref()) {
+    ctx->err = "reference index out of range";
+    return HBAM_E_ARG;
+  }
+  *name = ctx->f->ref_names()[(size_t)i].c_str();
+  *length = ctx->f->ref_lens()[(size_t)i];
+  return HBAM_OK;
+}
+
+int hbam_decode_span(hbam_ctx* ctx, uint64_t vstart, uint64_t vend, hbam_batch* out) {
+  memset(out, 0, sizeof *out);
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  hbam::SpanDev span;
+  int rc = ctx->f->pipe().decode_span(vstart, vend, hbam::kReader, true, &span);
+  if (rc != HBAM_OK) {
+    ctx->err = ctx->f->pipe().error();
+    return rc;
+  }
+  rc = hadoop_bam::fetch_span(ctx->f->pipe(), span, &ctx->batch, &ctx->err);
+  if (rc != HBAM_OK) return rc;
+  auto& h = ctx->batch;
+  out->n = span.n;
+  out->ref_id = h.ref_id.data();
+  out->pos = h.pos.data();
+  out->l_seq = h.l_seq.data();
+  out->next_ref_id = h.next_ref_id.data();
+  out->next_pos = h.next_pos.data();
+  out->tlen = h.tlen.data();
+  out->l_read_name = h.l_read_name.data();
+  out->mapq = h.mapq.data();
+  out->bin = h.bin.data();
+  out->n_cigar = h.n_cigar.data();
+  out->flag = h.flag.data();
+  out->key = h.key.data();
+  out->voff = h.voff.data();
+  out->rest_off = h.rest_off.data();
+  out->rest_len = h.rest_len.data();
+  out->data = h.data.data();
+  out->data_len = h.data.size();
+  out->status = span.status;
+  if (span.status != HBAM_OK) {
+    ctx->err = span.error;
+    return span.status;
+  }
+  return HBAM_OK;
+}
+
+int hbam_build_splitting_index(hbam_ctx* ctx, int32_t granularity, uint8_t** buf, uint64_t* len) {
+  *buf = nullptr;
+  *len = 0;
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  std::vector<uint8_t> out;
+  int rc = SplittingBAMIndexer::index(*ctx->f, granularity, &out);
+  if (rc != HBAM_OK) {
+    ctx->err = ctx->f->error();
+    return rc;
+  }
+  *buf = static_cast<uint8_t*>(malloc(out.size() ? out.size() : 1));
+  if (!*buf) return HBAM_E_NOMEM;
+  memcpy(*buf, out.data(), out.size());
+  *len = out.size();
+  return HBAM_OK;
+}
+
+int hbam_guess_record_starts(hbam_ctx* ctx, const uint64_t* begs, const uint64_t* ends, uint64_t n, uint64_t* out) {
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  std::vector<uint64_t> b(begs, begs + n), e(ends, ends + n), r;
+  hadoop_bam::BAMSplitGuesser g(*ctx->f);
+  int rc = g.guessNextBAMRecordStarts(b, e, &r);
+  if (rc != HBAM_OK) {
+    ctx->err = ctx->f->error();
+    return rc;
+  }
+  memcpy(out, r.data(), n * 8);
+  return HBAM_OK;
+}
+
+int hbam_get_splits(hbam_ctx* ctx, const uint64_t* starts, const uint64_t* lengths, uint64_t n, const uint8_t* sbi,
+                    uint64_t sbi_len, uint64_t* vstarts, uint64_t* vends, uint64_t* nout) {
+  *nout = 0;
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  std::vector<FileSplit> sp(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    sp[i].path = "bam";
+    sp[i].start = starts[i];
+    sp[i].length = lengths[i];
+  }
+  std::vector<FileVirtualSplit> out;
+  int rc = BAMInputFormat::getSplits(*ctx->f, sp, sbi, sbi_len, &out);
+  if (rc != HBAM_OK) {
+    ctx->err = ctx->f->error();
+    return rc;
+  }
+  for (size_t i = 0; i < out.size(); ++i) {
+    vstarts[i] = out[i].vStart;
+    vends[i] = out[i].vEnd;
+  }
+  *nout = out.size();
+  return HBAM_OK;
+}
+
+int hbam_blocks(hbam_ctx* ctx, uint64_t* coff, uint32_t* csize, uint32_t* isize, uint64_t* ustart, uint64_t cap,
+                uint64_t* n) {
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  const auto& b = ctx->f->pipe().blocks();
+  *n = b.size();
+  for (size_t i = 0; i < b.size() && i < cap; ++i) {
+    if (coff) coff[i] = b[i].coff;
+    if (csize) csize[i] = b[i].csize;
+    if (isize) isize[i] = b[i].isize;
+    if (ustart) ustart[i] = b[i].ustart;
+  }
+  return HBAM_OK;
+}
+
+int hbam_read_inflated(hbam_ctx* ctx, uint64_t pos, uint64_t len, uint8_t* dst) {
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  std::vector<uint8_t> v;
+  int rc = ctx->f->pipe().read_stream(pos, len, &v);
+  if (rc != HBAM_OK) {
+    ctx->err = ctx->f->pipe().error();
+    return rc;
+  }
+  if (v.size() != len) {
+    ctx->err = "range beyond the inflated stream";
+    return HBAM_E_ARG;
+  }
+  memcpy(dst, v.data(), len);
+  return HBAM_OK;
+}
+
+int64_t hbam_get_key0(int32_t ref_idx, int32_t alignment_start0) {
+  return BAMRecordReader::getKey0(ref_idx, alignment_start0);
+}
+int64_t hbam_get_key(int32_t ref_idx, int32_t alignment_start) {
+  return BAMRecordReader::getKey(ref_idx, alignment_start);
+}
+int64_t hbam_murmurhash3(const void* key, uint64_t len, int32_t seed) {
+  return hadoop_bam::murmurhash3(static_cast<const uint8_t*>(key), len, seed);
+}
+
+// ---- device-resident pipeline ------------------------------------------------
+int32_t hbam_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int hbam_gpu_create(int32_t device, hbam_gpu** out) {
+  *out = nullptr;
+  int n = hbam_device_count();
+  if (device < 0 || device >= n) {
+    g_open_err = "no HIP device " + std::to_string(device);
+    return HBAM_E_DEVICE;
+  }
+  auto* g = new hbam_gpu();
+  g->p.reset(new hbam::Pipeline(device));
+  if (!g->p->error().empty()) {
+    g_open_err = g->p->error();
+    delete g;
+    return HBAM_E_DEVICE;
+  }
+  *out = g;
+  return HBAM_OK;
+}
+
+void hbam_gpu_destroy(hbam_gpu* g) { delete g; }
+
+const char* hbam_gpu_error(hbam_gpu* g) { return g ? g->err.c_str() : g_open_err.c_str(); }
+
+int hbam_gpu_load(hbam_gpu* g, const void* data, uint64_t len, uint64_t base_offset, int32_t n_ref,
+                  uint64_t first_pos) {
+  int rc = g->p->load(static_cast<const uint8_t*>(data), len, base_offset);
+  if (rc == HBAM_OK) rc = g->p->locate();
+  if (rc != HBAM_OK) {
+    g->err = g->p->error();
+    return rc;
+  }
+  if (first_pos == UINT64_MAX) {
+    // whole file: parse the header with the same GPU-backed reader
+    std::unique_ptr<BamFile> tmp;
+    std::string err;
+    rc = BamFile::open(static_cast<const uint8_t*>(data), len, g->p->device(), true, false, &tmp, &err);
+    if (rc != HBAM_OK) {
+      g->err = err;
+      return rc;
+    }
+    g->p->set_n_ref(tmp->n_ref());
+    g->first_pos = tmp->header_end();
+  } else {
+    g->p->set_n_ref(n_ref);
+    g->first_pos = first_pos;
+  }
+  return HBAM_OK;
+}
+
+int hbam_gpu_run(hbam_gpu* g, int32_t flags, hbam_gpu_stats* st) {
+  memset(st, 0, sizeof *st);
+  hbam::Pipeline& p = *g->p;
+  p.timing = (flags & 1) != 0;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, p.stream());
+  int rc = p.locate();
+  if (rc == HBAM_OK) rc = p.inflate(0, (uint32_t)p.blocks().size(), true);
+  float ms_inflate = p.times.inflate, ms_huff = p.times.huff, ms_lz = p.times.lz77;
+  if (rc == HBAM_OK) {
+    rc = p.decode_span(p.voff_of(g->first_pos), ~0ull, hbam::kReader, (flags & 2) == 0, &g->span);
+  }
+  (void)hipEventRecord(e1, p.stream());
+  (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&st->ms_total, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (rc != HBAM_OK) {
+    g->err = p.error();
+    st->status = rc;
+    return rc;
+  }
+  st->n_blocks = p.blocks().size();
+  st->compressed_bytes = p.file_len();
+  st->inflated_bytes = p.total_u();
+  st->records = g->span.n;
+  st->status = g->span.status;
+  if (p.timing) {
+    st->ms_locate = p.times.locate;
+    st->ms_inflate = ms_inflate;
+    st->ms_huff = ms_huff;
+    st->ms_lz77 = ms_lz;
+    st->ms_chain = p.times.chain;
+    st->ms_decode = p.times.decode;
+  }
+  if (g->span.n) {
+    (void)hipMemcpy(&st->first_voff, g->span.rec_voff, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(&st->last_voff, g->span.rec_voff + g->span.n - 1, 8, hipMemcpyDeviceToHost);
+  }
+  if (g->span.status != HBAM_OK) g->err = g->span.error;
+  return g->span.status;
+}
+
+int hbam_gpu_fetch(hbam_gpu* g, int64_t* keys, uint64_t* voffs, uint64_t cap) {
+  const uint64_t n = std::min<uint64_t>(cap, g->span.n);
+  if (keys && n && g->span.col.key) {
+    if (hipMemcpy(keys, g->span.col.key, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return HBAM_E_DEVICE;
+  }
+  if (voffs && n) {
+    if (hipMemcpy(voffs, g->span.rec_voff, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return HBAM_E_DEVICE;
+  }
+  return HBAM_OK;
+}
+
+}  // extern "C"

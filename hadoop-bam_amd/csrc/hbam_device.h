@@ -1,0 +1,64 @@
+// hbam_device.h -- device data layout shared by the gfx950 kernels and the host pipeline.
+//
+// Layout in HBM (one pipeline = one GPU):
+//   file    : the compressed BGZF bytes, resident, padded with kFilePad zero bytes
+//   blocks  : BlockInfo[nblocks] (AoS, 32 B) from bgzf_locate
+//   u       : the inflated stream, block k at u + ustart_k (contiguous, padded)
+//   tokens  : per-chunk LZ77 token stream (phase A -> phase B of inflate)
+//   records : rec_pos / voff / SoA columns (one slot per record of the span)
+#pragma once
+#include <stdint.h>
+
+namespace hbam {
+
+constexpr uint64_t kFilePad = 8192;      // zero bytes after the file (ring prefetch)
+constexpr uint64_t kUPad = 4096;         // zero bytes after the inflated stream
+constexpr uint32_t kMaxIsize = 65536;    // BGZF ISIZE limit handled on device
+constexpr uint64_t kNone = ~0ull;
+
+// status codes (== include/hbam.h)
+enum : int {
+  kOk = 0,
+  kErrFormat = 1,  // SAMFormatException
+  kErrTrunc = 2,   // FileTruncatedException / RuntimeEOFException
+  kErrArg = 3,     // IllegalArgumentException
+  kErrIO = 4,      // IOException / RuntimeIOException (DataFormatException)
+  kErrDevice = 5,
+  kErrState = 6,
+  kErrNoMem = 7,
+};
+
+struct BlockInfo {
+  uint64_t coff;    // compressed offset in the file
+  uint64_t ustart;  // offset of the block's first inflated byte in u
+  uint32_t csize;   // BSIZE + 1
+  uint32_t isize;   // ISIZE footer
+  uint32_t crc;     // CRC32 footer
+  uint32_t flags;   // reserved
+};
+static_assert(sizeof(BlockInfo) == 32, "BlockInfo is 32 bytes");
+
+// Per-block result of inflate phase A.
+struct HuffOut {
+  uint32_t ntok;
+  int32_t status;
+};
+
+// Record-chain transition rules.
+enum ChainMode : int {
+  kReader = 0,  // [htsjdk] BAMRecordCodec.decode (BAMRecordReader path)
+  kIndexer = 1, // SplittingBAMIndexer.readAlignment + fullySkip
+};
+
+// Decoded SoA columns of one span (device pointers).  Field set of
+// LazyBAMRecordFactory.createBAMRecord (LazyBAMRecordFactory.java:37-50).
+struct Columns {
+  int32_t *ref_id, *pos, *l_seq, *next_ref_id, *next_pos, *tlen;
+  uint8_t *l_read_name, *mapq;
+  uint16_t *bin, *n_cigar, *flag;
+  int64_t *key;
+  uint64_t *voff, *rest_off;
+  uint32_t *rest_len;
+};
+
+}  // namespace hbam

@@ -1,0 +1,1144 @@
+// hbam_kernels.hip -- gfx950 kernels for the Hadoop-BAM read hot path.
+//
+//   bgzf_scan / bgzf_verify / bgzf_walk   BGZF block discovery
+//        ([htsjdk] BlockCompressedInputStream.readBlock; heuristic twin
+//         BaseSplitGuesser.java:31-108)
+//   inflate_huff   (phase A) one wavefront per BGZF block: DEFLATE bit
+//        stream -> LZ77 tokens.  Huffman tables, canonical-decode arrays and a
+//        2 KiB compressed-input ring live in LDS (~8.4 KiB per wave); the
+//        decode state is wave-uniform (SGPRs); tokens are collected in one VGPR
+//        across the 64 lanes (v_writelane) and stored 256 B at a time.
+//        ([htsjdk] BlockGunzipper.unzipBlock -> java.util.zip.Inflater)
+//   inflate_lz77   (phase B) one 256-thread workgroup per BGZF block: tokens
+//        -> bytes in a 64 KiB LDS image, block-wide prefix sums place tokens,
+//        back-references resolve in dependency rounds, then 16 B coalesced
+//        stores into the contiguous inflated stream.
+//   rec_guess / rec_link / rec_count / rec_emit   BAM record-boundary scan
+//        ([htsjdk] BAMRecordCodec.decode chain; SplittingBAMIndexer.java:340-368)
+//   rec_decode     fused field decode + sort key + voff
+//        (LazyBAMRecordFactory.java:37-50; BAMRecordReader.java:81-121;
+//         util/MurmurHash3.java:32-102)
+//   sbi_emit       .splitting-bai entries (SplittingBAMIndexer.java:262-287)
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+#include "hbam_device.h"
+#include "hbam_launch.h"
+
+namespace hbam {
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// unaligned little-endian u32 from a 4-aligned base (reads 8 bytes: pad!)
+__device__ __forceinline__ uint32_t ldu32(const uint8_t* base, uint64_t off) {
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(base + (off & ~3ull));
+  uint32_t lo = p[0], hi = p[1];
+  return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(off & 3));
+}
+__device__ __forceinline__ uint64_t ldu64(const uint8_t* base, uint64_t off) {
+  return (uint64_t)ldu32(base, off) | ((uint64_t)ldu32(base, off + 4) << 32);
+}
+
+// ---------------------------------------------------------------------------
+// BGZF block discovery
+// ---------------------------------------------------------------------------
+// A candidate is a position whose 16 header bytes read 1f 8b 08 04 .. .. .. ..
+// .. .. 06 00 'B' 'C' 02 00 (ID1 ID2 CM FLG, XLEN=6, BC subfield, SLEN=2): the
+// exact framing htsjdk writes and requires (XLEN==6), plus the BC subfield id
+// for selectivity.  Candidates are appended unordered, sorted, then the BSIZE
+// chain is verified; any break falls back to the serial walk (bgzf_walk).
+__global__ void k_bgzf_scan(const uint8_t* __restrict__ file, uint64_t lo, uint64_t hi,
+                            uint64_t* __restrict__ cand, uint32_t cap, uint32_t* __restrict__ count) {
+  const uint64_t a0 = lo & ~3ull;
+  const uint64_t nd = (hi - a0 + 3) / 4;  // dwords to inspect
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nd;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(file + a0) + t;
+    uint32_t w0 = w[0], w1 = w[1];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      uint64_t p = a0 + 4 * t + s;
+      if (p < lo || p >= hi) continue;
+      uint32_t magic = __builtin_amdgcn_alignbyte(w1, w0, s);
+      if (magic != 0x04088b1fu) continue;
+      if (p + 18 > hi) continue;
+      uint32_t xlen = ldu32(file, p + 10) & 0xffffu;
+      uint32_t sub = ldu32(file, p + 12);
+      if (xlen != 6 || sub != 0x00024342u) continue;
+      uint32_t i = atomicAdd(count, 1u);
+      if (i < cap) cand[i] = p;
+    }
+  }
+}
+
+// Verify the sorted candidate chain and fill BlockInfo.  flags[0] |= 1 on any
+// break (fallback), flags[1] = first block index with ISIZE > 64 KiB.
+__global__ void k_bgzf_verify(const uint8_t* __restrict__ file, uint64_t lo, uint64_t hi,
+                              const uint64_t* __restrict__ cand, uint32_t n,
+                              BlockInfo* __restrict__ blocks, uint32_t* __restrict__ flags) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t c = cand[i];
+  if (i == 0 && c != lo) atomicOr(&flags[0], 1u);
+  uint32_t total = (ldu32(file, c + 16) & 0xffffu) + 1;
+  uint64_t next = c + total;
+  uint64_t expect = (i + 1 < n) ? cand[i + 1] : hi;
+  if (next != expect || total < 26) {
+    atomicOr(&flags[0], 1u);
+    return;
+  }
+  BlockInfo b;
+  b.coff = c;
+  b.ustart = 0;
+  b.csize = total;
+  b.crc = ldu32(file, next - 8);
+  b.isize = ldu32(file, next - 4);
+  b.flags = 0;
+  if (b.isize > kMaxIsize) atomicMin(&flags[1], i);
+  blocks[i] = b;
+}
+
+// Serial fallback: walk BSIZE from lo with htsjdk's framing rules.
+// out[0] = nblocks, out[1] = status, out[2] = failing offset (low 32), out[3] = hi 32.
+__global__ void k_bgzf_walk(const uint8_t* __restrict__ file, uint64_t lo, uint64_t hi,
+                            BlockInfo* __restrict__ blocks, uint32_t cap, uint32_t* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t p = lo;
+  uint32_t n = 0;
+  int st = kOk;
+  while (p < hi) {
+    if (hi - p < 18) { st = kErrIO; break; }
+    uint32_t total = (ldu32(file, p + 16) & 0xffffu) + 1;
+    if (total < 18) { st = kErrIO; break; }
+    if (p + total > hi) { st = kErrTrunc; break; }
+    uint32_t w0 = ldu32(file, p);
+    uint32_t xlen = ldu32(file, p + 10) & 0xffffu;
+    if (w0 != 0x04088b1fu || xlen != 6 || total < 26) { st = kErrFormat; break; }
+    if (n >= cap) { st = kErrState; break; }
+    BlockInfo b;
+    b.coff = p;
+    b.ustart = 0;
+    b.csize = total;
+    b.crc = ldu32(file, p + total - 8);
+    b.isize = ldu32(file, p + total - 4);
+    b.flags = 0;
+    if (b.isize > kMaxIsize) { st = kErrFormat; break; }
+    blocks[n++] = b;
+    p += total;
+  }
+  out[0] = n;
+  out[1] = (uint32_t)st;
+  out[2] = (uint32_t)p;
+  out[3] = (uint32_t)(p >> 32);
+}
+
+__global__ void k_block_isize(const BlockInfo* __restrict__ blocks, uint32_t n, uint64_t* __restrict__ isz) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) isz[i] = blocks[i].isize;
+}
+__global__ void k_block_ustart(BlockInfo* __restrict__ blocks, uint32_t n, const uint64_t* __restrict__ us) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) blocks[i].ustart = us[i];
+}
+
+// ---------------------------------------------------------------------------
+// Inflate phase A: Huffman decode, one wavefront per BGZF block
+// ---------------------------------------------------------------------------
+constexpr int kLitRoot = 10;
+constexpr int kDistRoot = 8;
+enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_LONG = 3, K_BAD = 4 };
+constexpr uint32_t kBadEntry = K_BAD << 8;
+constexpr uint32_t kLongEntry = K_LONG << 8;
+
+__constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                                      31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
+                                      2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t kDistBase[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,
+                                       33,  49,  65,  97,  129, 193,  257,  385,  513,  769,
+                                       1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2,  3,  3,  4,  4,  5,  5,  6,
+                                       6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+struct HuffLds {
+  uint32_t lit[1 << kLitRoot];    // litlen fast table
+  uint32_t dist[1 << kDistRoot];  // distance fast table (also the code-length table)
+  uint32_t ring[512];             // 2 x 1 KiB compressed-input ring
+  uint32_t cnt_lit[16];
+  uint32_t cnt_dist[16];
+  uint32_t offs[16];
+  uint32_t firstc[16];
+  uint16_t sort_lit[288];
+  uint16_t sort_dist[32];
+  uint8_t lens[320];
+  uint8_t cl_lens[20];
+};
+
+// mode 0 litlen, 1 distance, 2 code-length codes
+__device__ __forceinline__ uint32_t make_entry(int mode, uint32_t s, uint32_t len) {
+  if (mode == 0) {
+    if (s < 256) return len | (K_LIT << 8) | (s << 16);
+    if (s == 256) return len | (K_EOB << 8);
+    if (s < 286) {
+      uint32_t i = s - 257;
+      return len | ((uint32_t)kLenExtra[i] << 4) | (K_LEN << 8) | ((uint32_t)kLenBase[i] << 16);
+    }
+    return len | kBadEntry;
+  }
+  if (mode == 1) {
+    if (s < 30) return len | ((uint32_t)kDistExtra[s] << 4) | (K_LIT << 8) | ((uint32_t)kDistBase[s] << 16);
+    return len | kBadEntry;
+  }
+  return len | (K_LIT << 8) | (s << 16);
+}
+
+// Canonical Huffman table build, all 64 lanes of the wave.  Validity follows
+// zlib inflate_table: over-subscribed -> error; incomplete -> error unless
+// the only code has length 1 (LENS/DISTS); no codes -> all-invalid table
+// (DISTS) or error (CODES).  Returns 0 on success.
+__device__ int build_table(HuffLds& L, const uint8_t* lens, int nsym, int root, int mode, uint32_t* tab,
+                           uint32_t* cnt, uint16_t* sorted) {
+  const uint32_t lane = lane_id();
+  if (lane < 16) cnt[lane] = 0;
+  __syncthreads();
+  for (int s = lane; s < nsym; s += 64) {
+    uint32_t l = lens[s];
+    if (l) atomicAdd(&cnt[l], 1u);
+  }
+  __syncthreads();
+  int left = 1, maxl = 0, over = 0;
+  uint32_t c[16];
+  c[0] = 0;
+#pragma unroll
+  for (int l = 1; l < 16; ++l) {
+    c[l] = rfl(cnt[l]);
+    left <<= 1;
+    left -= (int)c[l];
+    if (c[l]) maxl = l;
+    if (left < 0) over = 1;
+  }
+  for (int i = lane; i < (1 << root); i += 64) tab[i] = kBadEntry;
+  if (over) return 1;
+  if (maxl == 0) {
+    __syncthreads();
+    return mode == 2 ? 1 : 0;
+  }
+  if (left > 0 && (mode == 2 || maxl != 1)) return 1;
+  if (lane == 0) {
+    uint32_t o = 0, code = 0;
+#pragma unroll
+    for (int l = 1; l < 16; ++l) {
+      L.offs[l] = o;
+      o += c[l];
+      code = (code + c[l - 1]) << 1;
+      L.firstc[l] = code;
+    }
+  }
+  __syncthreads();
+  uint32_t base[16];
+#pragma unroll
+  for (int l = 0; l < 16; ++l) base[l] = 0;
+  const uint64_t ltmask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int c0 = 0; c0 < nsym; c0 += 64) {
+    int s = c0 + (int)lane;
+    uint32_t l = s < nsym ? lens[s] : 0;
+    uint32_t rank = 0;
+#pragma unroll
+    for (int q = 1; q < 16; ++q) {
+      uint64_t m = __ballot(l == (uint32_t)q);
+      if (l == (uint32_t)q) rank = base[q] + (uint32_t)__popcll(m & ltmask);
+      base[q] += (uint32_t)__popcll(m);
+    }
+    if (l) {
+      sorted[L.offs[l] + rank] = (uint16_t)s;
+      uint32_t code = L.firstc[l] + rank;
+      uint32_t rev = __brev(code) >> (32 - l);
+      if ((int)l <= root) {
+        uint32_t e = make_entry(mode, (uint32_t)s, l);
+        for (uint32_t i = rev; i < (1u << root); i += (1u << l)) tab[i] = e;
+      } else {
+        tab[rev & ((1u << root) - 1)] = kLongEntry;
+      }
+    }
+  }
+  __syncthreads();
+  return 0;
+}
+
+// puff-style canonical decode for codes longer than the table root (rare).
+__device__ uint32_t slow_decode(uint64_t bits, const uint32_t* cnt, const uint16_t* sorted, int mode) {
+  int code = 0, first = 0, index = 0;
+  for (int len = 1; len < 16; ++len) {
+    code |= (int)(bits & 1);
+    bits >>= 1;
+    int count = (int)rfl(cnt[len]);
+    if (code - count < first) {
+      uint32_t s = rfl(sorted[index + (code - first)]);
+      return make_entry(mode, s, (uint32_t)len);
+    }
+    index += count;
+    first += count;
+    first <<= 1;
+    code <<= 1;
+  }
+  return kBadEntry;
+}
+
+struct BitState {
+  uint64_t buf;
+  uint32_t cnt;
+  uint32_t rd;     // next dword (relative to the 16-aligned chunk base) to pull
+  uint32_t chunk;  // chunk index currently being read (rd / 256)
+};
+
+// Wave-cooperative ring maintenance: chunk c of the block's compressed data is
+// the 1 KiB at abase + 1024 c; ring half (c & 1) holds it.
+__device__ __forceinline__ void ring_store(HuffLds& L, uint32_t half, uint4 v) {
+  reinterpret_cast<uint4*>(L.ring)[half * 64 + lane_id()] = v;
+}
+__device__ __forceinline__ uint4 ring_load(const uint8_t* file, uint64_t abase, uint32_t c) {
+  return *reinterpret_cast<const uint4*>(file + abase + 1024ull * c + 16ull * lane_id());
+}
+
+__global__ __launch_bounds__(64) void k_inflate_huff(const uint8_t* __restrict__ file,
+                                                     const BlockInfo* __restrict__ blocks, uint32_t b0,
+                                                     uint64_t chunk_ustart, uint32_t* __restrict__ tokens,
+                                                     HuffOut* __restrict__ hout) {
+  __shared__ HuffLds L;
+  const uint32_t bi = b0 + blockIdx.x;
+  const uint32_t lane = lane_id();
+  const BlockInfo blk = blocks[bi];
+  const uint32_t isize = blk.isize;
+  if (isize == 0) {  // inflate(buf,off,0) returns 0 without reading: nothing to validate
+    if (lane == 0) { hout[bi].ntok = 0; hout[bi].status = kOk; }
+    return;
+  }
+  uint32_t* tok_out = tokens + (blk.ustart - chunk_ustart);
+  const uint64_t sbyte = blk.coff + 18;             // cdata start
+  const uint32_t clen = blk.csize - 26;             // cdata length
+  const uint64_t abase = sbyte & ~15ull;
+  const uint32_t lead = (uint32_t)(sbyte - abase);  // junk bytes before cdata
+  const uint64_t end_bits = 8ull * (lead + clen);
+
+  // prime the ring: chunks 0, 1 resident; chunk 2 in flight
+  ring_store(L, 0, ring_load(file, abase, 0));
+  ring_store(L, 1, ring_load(file, abase, 1));
+  uint4 pf = ring_load(file, abase, 2);
+  __syncthreads();
+
+  BitState bs;
+  bs.buf = 0;
+  bs.cnt = 0;
+  bs.rd = lead >> 2;
+  bs.chunk = 0;
+  int err = kOk;
+
+#define REFILL()                                                         \
+  do {                                                                   \
+    while (bs.cnt <= 32) {                                               \
+      uint32_t w = rfl(L.ring[bs.rd & 511]);                             \
+      bs.buf |= (uint64_t)w << bs.cnt;                                   \
+      bs.cnt += 32;                                                      \
+      bs.rd++;                                                           \
+      if ((bs.rd & 255) == 0) {                                          \
+        /* entered chunk c = rd/256: half (c+1)&1 is free for c+1 */     \
+        uint32_t c = bs.rd >> 8;                                         \
+        ring_store(L, (c + 1) & 1, pf);                                  \
+        pf = ring_load(file, abase, c + 2);                              \
+        bs.chunk = c;                                                    \
+        if (32ull * bs.rd - bs.cnt > end_bits + 64) { err = kErrFormat; } \
+      }                                                                  \
+    }                                                                    \
+  } while (0)
+#define CONSUME(n)   \
+  do {               \
+    bs.buf >>= (n);  \
+    bs.cnt -= (n);   \
+  } while (0)
+
+  REFILL();
+  CONSUME(8 * (lead & 3));
+
+  uint32_t outpos = 0, ntok = 0, tokv = 0, lacc = 0, lnum = 0;
+
+#define EMIT(t)                                                                       \
+  do {                                                                                \
+    tokv = (lane == (ntok & 63)) ? (uint32_t)(t) : tokv;                            \
+    if ((ntok & 63) == 63) tok_out[(ntok & ~63u) + lane] = tokv;                      \
+    ntok++;                                                                           \
+  } while (0)
+#define FLUSH_LITS()                        \
+  do {                                      \
+    if (lnum) {                             \
+      EMIT(lacc | (lnum << 24));            \
+      lacc = 0;                             \
+      lnum = 0;                             \
+    }                                       \
+  } while (0)
+#define LITERAL(b)                         \
+  do {                                     \
+    lacc |= (uint32_t)(b) << (8 * lnum);   \
+    lnum++;                                \
+    outpos++;                              \
+    if (lnum == 3) {                       \
+      EMIT(lacc | (3u << 24));             \
+      lacc = 0;                            \
+      lnum = 0;                            \
+    }                                      \
+  } while (0)
+
+  uint32_t final_blk = 0;
+  while (!final_blk && outpos < isize && err == kOk) {
+    REFILL();
+    uint32_t hdr = (uint32_t)bs.buf & 7;
+    CONSUME(3);
+    final_blk = hdr & 1;
+    uint32_t type = hdr >> 1;
+    if (type == 0) {  // stored
+      uint32_t drop = bs.cnt & 7;
+      CONSUME(drop);
+      REFILL();
+      uint32_t len = (uint32_t)bs.buf & 0xffff, nlen = (uint32_t)(bs.buf >> 16) & 0xffff;
+      CONSUME(32);
+      if (len != (~nlen & 0xffffu)) { err = kErrIO; break; }
+      for (uint32_t j = 0; j < len && outpos < isize && err == kOk; ++j) {
+        REFILL();
+        uint32_t b = (uint32_t)bs.buf & 255;
+        CONSUME(8);
+        LITERAL(b);
+      }
+      continue;
+    } else if (type == 1) {  // fixed Huffman
+      for (int s = lane; s < 320; s += 64) {
+        uint8_t l;
+        if (s < 144) l = 8; else if (s < 256) l = 9; else if (s < 280) l = 7; else if (s < 288) l = 8; else l = 5;
+        L.lens[s] = l;
+      }
+      __syncthreads();
+      if (build_table(L, L.lens, 288, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit) ||
+          build_table(L, L.lens + 288, 32, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist)) {
+        err = kErrIO;
+        break;
+      }
+    } else if (type == 2) {  // dynamic Huffman
+      REFILL();
+      uint32_t hlit = ((uint32_t)bs.buf & 31) + 257;
+      uint32_t hdist = ((uint32_t)(bs.buf >> 5) & 31) + 1;
+      uint32_t hclen = ((uint32_t)(bs.buf >> 10) & 15) + 4;
+      CONSUME(14);
+      if (hlit > 286 || hdist > 30) { err = kErrIO; break; }
+      if (lane < 20) L.cl_lens[lane] = 0;
+      __syncthreads();
+      for (uint32_t i = 0; i < hclen; ++i) {
+        REFILL();
+        uint32_t v = (uint32_t)bs.buf & 7;
+        CONSUME(3);
+        if (lane == 0) L.cl_lens[kClOrder[i]] = (uint8_t)v;
+      }
+      __syncthreads();
+      if (build_table(L, L.cl_lens, 19, 7, 2, L.dist, L.cnt_dist, L.sort_dist)) { err = kErrIO; break; }
+      const uint32_t ntot = hlit + hdist;
+      uint32_t i = 0, last = 0;
+      while (i < ntot) {
+        REFILL();
+        if (err != kOk) break;
+        uint32_t e = rfl(L.dist[(uint32_t)bs.buf & 127]);
+        if (((e >> 8) & 7) == K_BAD) { err = kErrIO; break; }
+        CONSUME(e & 15);
+        uint32_t sym = e >> 16, rep, val;
+        if (sym < 16) {
+          rep = 1;
+          val = sym;
+        } else if (sym == 16) {
+          if (i == 0) { err = kErrIO; break; }
+          rep = 3 + ((uint32_t)bs.buf & 3);
+          CONSUME(2);
+          val = last;
+        } else if (sym == 17) {
+          rep = 3 + ((uint32_t)bs.buf & 7);
+          CONSUME(3);
+          val = 0;
+        } else {
+          rep = 11 + ((uint32_t)bs.buf & 127);
+          CONSUME(7);
+          val = 0;
+        }
+        if (i + rep > ntot) { err = kErrIO; break; }
+        for (uint32_t j = lane; j < rep; j += 64) L.lens[i + j] = (uint8_t)val;
+        i += rep;
+        last = val;
+      }
+      if (err != kOk) break;
+      __syncthreads();
+      if (rfl(L.lens[256]) == 0) { err = kErrIO; break; }
+      if (build_table(L, L.lens, (int)hlit, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit) ||
+          build_table(L, L.lens + hlit, (int)hdist, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist)) {
+        err = kErrIO;
+        break;
+      }
+    } else {
+      err = kErrIO;  // invalid block type
+      break;
+    }
+
+    // ---- symbol loop ----
+    while (outpos < isize) {
+      REFILL();
+      if (err != kOk) break;
+      uint32_t e = rfl(L.lit[(uint32_t)bs.buf & ((1u << kLitRoot) - 1)]);
+      uint32_t kind = (e >> 8) & 7;
+      if (kind == K_LONG) {
+        e = slow_decode(bs.buf, L.cnt_lit, L.sort_lit, 0);
+        kind = (e >> 8) & 7;
+      }
+      CONSUME(e & 15);
+      if (kind == K_LIT) {
+        LITERAL(e >> 16);
+        continue;
+      }
+      if (kind == K_LEN) {
+        uint32_t ex = (e >> 4) & 15;
+        uint32_t len = (e >> 16) + ((uint32_t)bs.buf & ((1u << ex) - 1));
+        CONSUME(ex);
+        REFILL();
+        uint32_t d = rfl(L.dist[(uint32_t)bs.buf & ((1u << kDistRoot) - 1)]);
+        if (((d >> 8) & 7) == K_LONG) d = slow_decode(bs.buf, L.cnt_dist, L.sort_dist, 1);
+        if (((d >> 8) & 7) != K_LIT) { err = kErrIO; break; }
+        CONSUME(d & 15);
+        uint32_t dx = (d >> 4) & 15;
+        uint32_t dist = (d >> 16) + ((uint32_t)bs.buf & ((1u << dx) - 1));
+        CONSUME(dx);
+        if (dist > outpos) { err = kErrIO; break; }  // invalid distance too far back
+        FLUSH_LITS();
+        EMIT(0x80000000u | ((dist - 1) << 16) | len);
+        outpos += len;
+        continue;
+      }
+      if (kind == K_EOB) break;
+      err = kErrIO;  // invalid literal/length code
+      break;
+    }
+    if (32ull * bs.rd - bs.cnt > end_bits) err = kErrFormat;  // ran past the input
+  }
+  FLUSH_LITS();
+  if (ntok & 63) {
+    if (lane < (ntok & 63)) tok_out[(ntok & ~63u) + lane] = tokv;
+  }
+  if (err == kOk && outpos < isize) err = kErrFormat;  // "Did not inflate expected amount"
+  if (err == kOk && 32ull * bs.rd - bs.cnt > end_bits) err = kErrFormat;
+  if (lane == 0) {
+    hout[bi].ntok = ntok;
+    hout[bi].status = err;
+  }
+#undef REFILL
+#undef CONSUME
+#undef EMIT
+#undef FLUSH_LITS
+#undef LITERAL
+}
+
+// ---------------------------------------------------------------------------
+// Inflate phase B: tokens -> bytes, one 256-thread workgroup per BGZF block
+// ---------------------------------------------------------------------------
+constexpr int kLzThreads = 256;
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t t = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d) v += t;
+  }
+  return v;
+}
+
+// exclusive scan over the workgroup; returns the prefix, *total = sum
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
+  const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
+  uint32_t inc = wave_incl_scan(v);
+  if (lane == 63) scratch[wid] = inc;
+  __syncthreads();
+  uint32_t w0 = scratch[0], w1 = scratch[1], w2 = scratch[2], w3 = scratch[3];
+  uint32_t off = (wid > 0 ? w0 : 0) + (wid > 1 ? w1 : 0) + (wid > 2 ? w2 : 0);
+  *total = w0 + w1 + w2 + w3;
+  __syncthreads();
+  return off + inc - v;
+}
+
+__device__ __forceinline__ uint32_t block_min(uint32_t v, uint32_t* scratch) {
+  const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v = min(v, (uint32_t)__shfl_xor(v, d, 64));
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  uint32_t r = min(min(scratch[0], scratch[1]), min(scratch[2], scratch[3]));
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __restrict__ blocks, uint32_t b0,
+                                                             uint64_t chunk_ustart,
+                                                             const uint32_t* __restrict__ tokens,
+                                                             const HuffOut* __restrict__ hout,
+                                                             uint8_t* __restrict__ u) {
+  __shared__ __attribute__((aligned(16))) uint8_t out[kMaxIsize + 16];
+  __shared__ uint32_t scratch[8];
+  const BlockInfo blk = blocks[b0 + blockIdx.x];
+  const HuffOut ho = hout[b0 + blockIdx.x];
+  if (ho.status != kOk || blk.isize == 0) return;
+  const uint32_t isize = blk.isize;
+  const uint32_t o0 = (uint32_t)(blk.ustart & 15);
+  const uint32_t* tk = tokens + (blk.ustart - chunk_ustart);
+  const uint32_t ntok = ho.ntok;
+  uint32_t P = 0;
+  for (uint32_t c = 0; c < ntok; c += kLzThreads) {
+    const uint32_t i = c + threadIdx.x;
+    const uint32_t t = i < ntok ? tk[i] : 0u;
+    const bool ismatch = (t >> 31) != 0;
+    const uint32_t len = ismatch ? (t & 0xffffu) : ((t >> 24) & 3u);
+    uint32_t total;
+    const uint32_t pos = P + block_excl_scan(len, scratch, &total);
+    P += total;
+    if (!ismatch) {
+      for (uint32_t j = 0; j < len; ++j)
+        if (pos + j < isize) out[o0 + pos + j] = (uint8_t)(t >> (8 * j));
+    }
+    const uint32_t dist = ((t >> 16) & 0x7fffu) + 1;
+    bool pending = ismatch && pos < isize;
+    __syncthreads();
+    for (;;) {
+      uint32_t first = block_min(pending ? pos : 0xffffffffu, scratch);
+      if (first == 0xffffffffu) break;
+      if (pending) {
+        uint32_t need_end = pos - dist + min(len, dist);
+        if (pos == first || need_end <= first) {
+          uint32_t n = min(len, isize - pos);
+          uint8_t* dst = out + o0 + pos;
+          for (uint32_t k = 0; k < n; ++k) dst[k] = dst[(int)k - (int)dist];
+          pending = false;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  // write back: 16 B aligned segments of global memory
+  const uint64_t g0 = blk.ustart & ~15ull;
+  const uint64_t gend = blk.ustart + isize;
+  const uint32_t nseg = (uint32_t)((gend - g0 + 15) >> 4);
+  for (uint32_t s = threadIdx.x; s < nseg; s += kLzThreads) {
+    const uint64_t ga = g0 + 16ull * s;
+    if (ga >= blk.ustart && ga + 16 <= gend) {
+      *reinterpret_cast<uint4*>(u + ga) = *reinterpret_cast<const uint4*>(out + 16 * s);
+    } else {
+      for (int j = 0; j < 16; ++j) {
+        uint64_t g = ga + j;
+        if (g >= blk.ustart && g < gend) u[g] = out[16 * s + j];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Record chain
+// ---------------------------------------------------------------------------
+struct ChainEnv {
+  const uint8_t* u;        // inflated stream
+  const BlockInfo* blocks;
+  uint64_t e_inf;          // end of inflated (available) data
+  uint64_t e_true;         // end of the logical stream (all blocks)
+  uint64_t p0;             // span start position (first record, read after seek)
+  uint64_t q_end;          // records with position >= q_end are outside the span
+  const uint64_t* dead;    // sorted dead positions (empty block after exhausted one)
+  uint32_t ndead;
+  int32_t n_ref;
+  uint32_t k0, k1;         // block range [k0, k1)
+};
+
+__device__ __forceinline__ bool is_dead(const ChainEnv& E, uint64_t q) {
+  uint32_t lo = 0, hi = E.ndead;  // sorted; usually 0 or 1 entries (the EOF marker)
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (E.dead[mid] < q) lo = mid + 1; else hi = mid;
+  }
+  return lo < E.ndead && E.dead[lo] == q;
+}
+__device__ __forceinline__ bool dead_in_record(const ChainEnv& E, uint64_t q, int32_t bs) {
+  if (E.ndead == 0) return false;
+  const uint8_t offs[11] = {4, 8, 12, 13, 14, 16, 18, 20, 24, 28, 32};
+  for (int i = 0; i < 11; ++i)
+    if (is_dead(E, q + offs[i])) return true;
+  return bs > 32 && is_dead(E, q + 36);
+}
+
+// Necessary conditions for a record of a well-formed BAM (guess only; the
+// true chain is fixed by the link step, never by this test).
+__device__ __forceinline__ bool plausible(const ChainEnv& E, uint64_t q) {
+  if (q + 36 > E.e_inf) return false;
+  int32_t bs = (int32_t)ldu32(E.u, q);
+  int32_t ref = (int32_t)ldu32(E.u, q + 4);
+  int32_t pos = (int32_t)ldu32(E.u, q + 8);
+  uint32_t lrn = ldu32(E.u, q + 12) & 0xffu;
+  uint32_t ncig = ldu32(E.u, q + 16) & 0xffffu;
+  int32_t lseq = (int32_t)ldu32(E.u, q + 20);
+  int32_t nref = (int32_t)ldu32(E.u, q + 24);
+  int32_t npos = (int32_t)ldu32(E.u, q + 28);
+  if (ref < -1 || ref >= E.n_ref || nref < -1 || nref >= E.n_ref) return false;
+  if (pos < -1 || npos < -1 || lrn < 1 || lseq < 0) return false;
+  int64_t need = 32 + (int64_t)lrn + 4 * (int64_t)ncig + (int64_t)lseq + ((int64_t)lseq + 1) / 2;
+  if ((int64_t)bs < need) return false;
+  if (q + 4 + (uint64_t)bs > E.e_true) return false;
+  if (q + 36 + lrn > E.e_inf) return false;
+  return E.u[q + 36 + lrn - 1] == 0;
+}
+
+// One chain step from q under the given rules.  Returns false if the walk
+// cannot continue (data unavailable or malformed record); *nq = next position.
+template <int MODE>
+__device__ __forceinline__ bool chain_step(const ChainEnv& E, uint64_t q, uint64_t* nq) {
+  if (q + 4 > E.e_inf) return false;
+  int32_t bs = (int32_t)ldu32(E.u, q);
+  if (MODE == kReader) {
+    if (bs < 32) return false;
+    *nq = q + 4 + (uint64_t)bs;
+  } else {
+    *nq = q + 4 + (bs > 0 ? (uint64_t)bs : 0);
+  }
+  return true;
+}
+
+// Per block guess of the first record start and the chain exit.  One wave per
+// block.  g = kNone when no candidate survives; exit < block end means the
+// walk stopped inside the block.
+template <int MODE>
+__global__ __launch_bounds__(64) void k_rec_guess(ChainEnv E, uint64_t* __restrict__ g_out,
+                                                  uint64_t* __restrict__ x_out) {
+  const uint32_t k = E.k0 + blockIdx.x;
+  const BlockInfo b = E.blocks[k];
+  const uint64_t bend = b.ustart + b.isize;
+  const uint32_t lane = lane_id();
+  uint64_t g = kNone, x = kNone;
+  if (bend > E.p0 && b.ustart < E.q_end && b.isize > 0) {
+    if (b.ustart <= E.p0) {  // the block holding the span start: entry is known
+      g = E.p0;
+      uint64_t q = g, nq;
+      while (q < bend && chain_step<MODE>(E, q, &nq)) q = nq;
+      x = q;
+    } else {
+      for (uint64_t c0 = b.ustart; c0 < bend && g == kNone; c0 += 64) {
+        uint64_t p = c0 + lane;
+        bool ok = p < bend && plausible(E, p);
+        uint64_t m = __ballot(ok);
+        while (m) {
+          uint64_t c = c0 + (uint64_t)(__ffsll((long long)m) - 1);
+          m &= m - 1;
+          uint64_t q = c;
+          bool valid = true;
+          while (q < bend) {
+            if (!plausible(E, q)) { valid = false; break; }
+            q += 4 + (uint64_t)(int32_t)ldu32(E.u, q);
+          }
+          if (valid) { g = c; x = q; break; }
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+    g_out[blockIdx.x] = g;
+    x_out[blockIdx.x] = x;
+  }
+}
+
+// Link the per-block guesses into the true chain (serial in block order, with
+// a 256-block tile fast path when every block of the tile links to the next).
+// entry[i] = true first record position of block k0+i, or kNone.
+// summary[0] = final chain position, summary[1] = 1 if the chain stopped
+// inside a block (malformed record / data unavailable).
+template <int MODE>
+__global__ __launch_bounds__(256) void k_rec_link(ChainEnv E, const uint64_t* __restrict__ g,
+                                                  const uint64_t* __restrict__ x, uint64_t* __restrict__ entry,
+                                                  uint64_t* __restrict__ summary) {
+  __shared__ uint64_t s_cur;
+  __shared__ int s_stop;
+  const uint32_t nb = E.k1 - E.k0;
+  if (threadIdx.x == 0) { s_cur = E.p0; s_stop = 0; }
+  __syncthreads();
+  for (uint32_t t0 = 0; t0 < nb; t0 += 256) {
+    const uint32_t i = t0 + threadIdx.x;
+    const uint64_t cur = s_cur;
+    const int stop = s_stop;
+    bool fast = true;
+    if (i < nb) {
+      const BlockInfo b = E.blocks[E.k0 + i];
+      const uint64_t bend = b.ustart + b.isize;
+      const uint64_t gi = g[i], xi = x[i];
+      const uint64_t expect = (threadIdx.x == 0) ? cur : x[i - 1];
+      fast = !stop && gi != kNone && gi == expect && gi < E.q_end && xi != kNone && xi >= bend;
+    }
+    const int all_fast = __syncthreads_and(fast);
+    if (all_fast) {
+      if (i < nb) entry[i] = g[i];
+      __syncthreads();
+      if (threadIdx.x == 0) s_cur = x[min(t0 + 255, nb - 1)];
+      __syncthreads();
+      continue;
+    }
+    if (threadIdx.x == 0) {
+      uint64_t c = cur;
+      int st = stop;
+      for (uint32_t j = t0; j < min(t0 + 256, nb); ++j) {
+        const BlockInfo b = E.blocks[E.k0 + j];
+        const uint64_t bend = b.ustart + b.isize;
+        if (st || c >= E.q_end || c >= bend || b.isize == 0) {
+          entry[j] = kNone;
+          continue;
+        }
+        entry[j] = c;
+        if (g[j] == c) {
+          c = x[j];
+        } else {
+          uint64_t q = c, nq;
+          while (q < bend && chain_step<MODE>(E, q, &nq)) q = nq;
+          c = q;
+        }
+        if (c < bend) st = 1;
+      }
+      s_cur = c;
+      s_stop = st;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    summary[0] = s_cur;
+    summary[1] = (uint64_t)s_stop;
+  }
+}
+
+// Count (and validate) the records of each block of the span under the
+// reader / indexer rules.  One thread per block.
+//   cnt[i], err[i] = status code, errpos[i] = position of the failing record,
+//   *need = furthest byte the span needs inflated (atomicMax).
+template <int MODE>
+__global__ void k_rec_count(ChainEnv E, const uint64_t* __restrict__ entry, uint32_t* __restrict__ cnt,
+                            int32_t* __restrict__ err, unsigned long long* __restrict__ need) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nb = E.k1 - E.k0;
+  if (i >= nb) return;
+  uint32_t n = 0;
+  int st = kOk;
+  const uint64_t e = entry[i];
+  if (e != kNone) {
+    const BlockInfo b = E.blocks[E.k0 + i];
+    const uint64_t lim = min(b.ustart + b.isize, E.q_end);
+    uint64_t q = e;
+    bool first = (MODE == kReader) && (e == E.p0);  // reader: first record follows a seek
+    while (q < lim) {
+      if (!first && is_dead(E, q)) break;  // readInt at an exhausted block + empty block: EOF
+      first = false;
+      const uint64_t avail = E.e_true - q;
+      if (avail < 4) {
+        if (MODE == kIndexer && avail > 0) st = kErrIO;  // "less than 4 bytes long"
+        break;
+      }
+      if (q + 4 > E.e_inf) { atomicMax(need, (unsigned long long)(q + 4)); break; }
+      const int32_t bs = (int32_t)ldu32(E.u, q);
+      if (MODE == kReader) {
+        if (bs < 32) { st = kErrFormat; break; }
+        if (dead_in_record(E, q, bs) || avail - 4 < (uint64_t)bs) { st = kErrTrunc; break; }
+        if (q + 4 + (uint64_t)bs > E.e_inf) { atomicMax(need, (unsigned long long)(q + 4 + (uint64_t)bs)); break; }
+        const int32_t ref = (int32_t)ldu32(E.u, q + 4), nref = (int32_t)ldu32(E.u, q + 24);
+        if (ref < -1 || ref >= E.n_ref || nref < -1 || nref >= E.n_ref) { st = kErrArg; break; }
+        ++n;
+        q += 4 + (uint64_t)bs;
+      } else {
+        ++n;
+        if (bs > 0) {
+          if ((uint64_t)bs > avail - 4 || is_dead(E, q + 4)) { st = kErrIO; break; }  // "Skip failed"
+          q += 4 + (uint64_t)bs;
+        } else {
+          q += 4;
+        }
+      }
+    }
+  }
+  cnt[i] = n;
+  err[i] = st;
+}
+
+// Second walk: write record positions and normalized voffs at base[i].
+template <int MODE>
+__global__ void k_rec_emit(ChainEnv E, const uint64_t* __restrict__ entry, const uint32_t* __restrict__ cnt,
+                           const uint64_t* __restrict__ base, uint64_t* __restrict__ rec_pos,
+                           uint64_t* __restrict__ rec_voff) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nb = E.k1 - E.k0;
+  if (i >= nb) return;
+  const uint32_t n = cnt[i];
+  if (n == 0) return;
+  const BlockInfo b = E.blocks[E.k0 + i];
+  uint64_t q = entry[i];
+  uint64_t o = base[i];
+  for (uint32_t r = 0; r < n; ++r) {
+    rec_pos[o + r] = q;
+    rec_voff[o + r] = (b.coff << 16) | (q - b.ustart);
+    const int32_t bs = (int32_t)ldu32(E.u, q);
+    q += 4 + (uint64_t)(MODE == kReader ? bs : (bs > 0 ? bs : 0));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused record decode: SoA columns + BAMRecordReader.getKey
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+// MurmurHash3.murmurhash3(byte[], seed) (util/MurmurHash3.java:32-102) over
+// len bytes of u at off.
+__device__ uint64_t murmur3_dev(const uint8_t* u, uint64_t off, uint32_t len, int32_t seed) {
+  const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+  uint64_t h1 = (uint64_t)(int64_t)seed, h2 = h1;
+  const uint32_t nblocks = len / 16;
+  for (uint32_t i = 0; i < nblocks; ++i) {
+    uint64_t k1 = ldu64(u, off + 16ull * i), k2 = ldu64(u, off + 16ull * i + 8);
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    h2 = (h2 << 31) | (h1 >> 33); h2 += h1; h2 = h2 * 5 + 0x38495ab5;  // :59
+  }
+  const uint64_t t = off + 16ull * nblocks;
+  const uint32_t r = len & 15;
+  if (r) {
+    // tail bytes via two 8-byte loads (padding makes the over-read safe), masked
+    uint64_t lo = ldu64(u, t), hi = ldu64(u, t + 8);
+    if (r > 8) {
+      uint64_t k2 = hi & (~0ull >> (64 - 8 * (r - 8)));
+      k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    }
+    uint64_t k1 = r >= 8 ? lo : (lo & (~0ull >> (64 - 8 * r)));
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+  }
+  h1 ^= (uint64_t)len;
+  h2 ^= (uint64_t)len;
+  h1 += h2;
+  h2 += h1;
+  h1 = fmix64(h1);
+  h2 = fmix64(h2);
+  h1 += h2;
+  return h1;
+}
+
+__global__ void k_rec_decode(const uint8_t* __restrict__ u, const uint64_t* __restrict__ rec_pos, uint64_t n,
+                             Columns col) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t q = rec_pos[i];
+    const int32_t bs = (int32_t)ldu32(u, q);
+    const int32_t ref = (int32_t)ldu32(u, q + 4);
+    const int32_t pos = (int32_t)ldu32(u, q + 8);
+    const uint32_t w12 = ldu32(u, q + 12);
+    const uint32_t w16 = ldu32(u, q + 16);
+    const int32_t lseq = (int32_t)ldu32(u, q + 20);
+    const int32_t nref = (int32_t)ldu32(u, q + 24);
+    const int32_t npos = (int32_t)ldu32(u, q + 28);
+    const int32_t tlen = (int32_t)ldu32(u, q + 32);
+    const uint16_t flag = (uint16_t)(w16 >> 16);
+    col.ref_id[i] = ref;
+    col.pos[i] = pos;
+    col.l_read_name[i] = (uint8_t)w12;
+    col.mapq[i] = (uint8_t)(w12 >> 8);
+    col.bin[i] = (uint16_t)(w12 >> 16);
+    col.n_cigar[i] = (uint16_t)w16;
+    col.flag[i] = flag;
+    col.l_seq[i] = lseq;
+    col.next_ref_id[i] = nref;
+    col.next_pos[i] = npos;
+    col.tlen[i] = tlen;
+    col.rest_off[i] = q + 36;
+    col.rest_len[i] = (uint32_t)(bs - 32);
+    // BAMRecordReader.getKey (:81-121): alignmentStart = pos+1
+    const int32_t start = (int32_t)((uint32_t)pos + 1u);
+    int64_t key;
+    if (!((flag & 4) || ref < 0 || start < 0)) {
+      key = (int64_t)(((uint64_t)(int64_t)ref << 32) | (uint64_t)(int64_t)(int32_t)(start - 1));
+    } else {
+      const int32_t h = (int32_t)murmur3_dev(u, q + 36, (uint32_t)(bs - 32), 0);
+      key = (int64_t)((0x7fffffffull << 32) | (uint64_t)(int64_t)h);
+    }
+    col.key[i] = key;
+  }
+}
+
+// first block (index) whose status is non-zero -> *first (atomicMin), status -> code[]
+__global__ void k_first_error_hout(const HuffOut* __restrict__ hout, uint32_t b0, uint32_t nb,
+                                   uint32_t* __restrict__ first) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nb && hout[b0 + i].status != kOk) atomicMin(first, i);
+}
+__global__ void k_first_error_i32(const int32_t* __restrict__ err, uint32_t nb, uint32_t* __restrict__ first) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nb && err[i] != kOk) atomicMin(first, i);
+}
+// zero the counts of blocks after `cut` (the first failing block)
+__global__ void k_truncate_counts(uint32_t* __restrict__ cnt, uint32_t nb, const uint32_t* __restrict__ cut) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nb && i > *cut) cnt[i] = 0;
+}
+
+// .splitting-bai: entry (o+1)/g = voff of record o when (o+1) % g == 0.
+__global__ void k_sbi_emit(const uint64_t* __restrict__ voff, uint64_t n, uint32_t g, uint64_t* __restrict__ ent) {
+  for (uint64_t o = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; o < n;
+       o += (uint64_t)gridDim.x * blockDim.x) {
+    if ((o + 1) % g == 0) ent[(o + 1) / g] = voff[o];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host launch wrappers (hbam_launch.h)
+// ---------------------------------------------------------------------------
+static inline unsigned grid_for(uint64_t n, unsigned bs, unsigned cap = 65535u * 4) {
+  uint64_t g = (n + bs - 1) / bs;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+hipError_t launch_bgzf_scan(const uint8_t* file, uint64_t lo, uint64_t hi, uint64_t* cand, uint32_t cap,
+                            uint32_t* count, hipStream_t s) {
+  uint64_t nd = (hi - (lo & ~3ull) + 3) / 4;
+  hipLaunchKernelGGL(k_bgzf_scan, dim3(grid_for(nd, 256, 8192)), dim3(256), 0, s, file, lo, hi, cand, cap, count);
+  return hipGetLastError();
+}
+hipError_t launch_bgzf_verify(const uint8_t* file, uint64_t lo, uint64_t hi, const uint64_t* cand, uint32_t n,
+                              BlockInfo* blocks, uint32_t* flags, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bgzf_verify, dim3((n + 255) / 256), dim3(256), 0, s, file, lo, hi, cand, n, blocks, flags);
+  return hipGetLastError();
+}
+hipError_t launch_bgzf_walk(const uint8_t* file, uint64_t lo, uint64_t hi, BlockInfo* blocks, uint32_t cap,
+                            uint32_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_bgzf_walk, dim3(1), dim3(64), 0, s, file, lo, hi, blocks, cap, out);
+  return hipGetLastError();
+}
+hipError_t launch_block_ustart(BlockInfo* blocks, uint32_t n, uint64_t* tmp_isize, uint64_t* tmp_ustart,
+                               void* scan_tmp, size_t* scan_bytes, hipStream_t s) {
+  if (scan_tmp == nullptr) {  // size query
+    return hipcub::DeviceScan::ExclusiveSum(nullptr, *scan_bytes, tmp_isize, tmp_ustart, (int)n, s);
+  }
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_block_isize, dim3((n + 255) / 256), dim3(256), 0, s, blocks, n, tmp_isize);
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, *scan_bytes, tmp_isize, tmp_ustart, (int)n, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_block_ustart, dim3((n + 255) / 256), dim3(256), 0, s, blocks, n, tmp_ustart);
+  return hipGetLastError();
+}
+hipError_t sort_u64(void* tmp, size_t* tmp_bytes, uint64_t* keys_in, uint64_t* keys_out, uint32_t n,
+                    hipStream_t s) {
+  return hipcub::DeviceRadixSort::SortKeys(tmp, *tmp_bytes, keys_in, keys_out, (int)n, 0, 64, s);
+}
+hipError_t scan_u32_to_u64(void* tmp, size_t* tmp_bytes, const uint32_t* in, uint64_t* out, uint32_t n,
+                           hipStream_t s) {
+  return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, in, out, (int)n, s);
+}
+
+hipError_t launch_inflate(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
+                          uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint8_t* u, hipStream_t s) {
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_inflate_huff, dim3(nb), dim3(64), 0, s, file, blocks, b0, chunk_ustart, tokens, hout);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_inflate_lz77, dim3(nb), dim3(kLzThreads), 0, s, blocks, b0, chunk_ustart, tokens, hout, u);
+  return hipGetLastError();
+}
+hipError_t launch_inflate_huff(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
+                               uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, hipStream_t s) {
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_inflate_huff, dim3(nb), dim3(64), 0, s, file, blocks, b0, chunk_ustart, tokens, hout);
+  return hipGetLastError();
+}
+hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb, uint64_t chunk_ustart,
+                               const uint32_t* tokens, const HuffOut* hout, uint8_t* u, hipStream_t s) {
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_inflate_lz77, dim3(nb), dim3(kLzThreads), 0, s, blocks, b0, chunk_ustart, tokens, hout, u);
+  return hipGetLastError();
+}
+
+hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s) {
+  ChainEnv E;
+  E.u = a.u;
+  E.blocks = a.blocks;
+  E.e_inf = a.e_inf;
+  E.e_true = a.e_true;
+  E.p0 = a.p0;
+  E.q_end = a.q_end;
+  E.dead = a.dead;
+  E.ndead = a.ndead;
+  E.n_ref = a.n_ref;
+  E.k0 = a.k0;
+  E.k1 = a.k1;
+  const uint32_t nb = a.k1 - a.k0;
+  if (nb == 0) return hipSuccess;
+  const unsigned tb = 64, gb = (nb + tb - 1) / tb;
+  switch (stage) {
+    case 0:
+      if (mode == kReader) hipLaunchKernelGGL(k_rec_guess<kReader>, dim3(nb), dim3(64), 0, s, E, a.g, a.x);
+      else hipLaunchKernelGGL(k_rec_guess<kIndexer>, dim3(nb), dim3(64), 0, s, E, a.g, a.x);
+      break;
+    case 1:
+      if (mode == kReader) hipLaunchKernelGGL(k_rec_link<kReader>, dim3(1), dim3(256), 0, s, E, a.g, a.x, a.entry, a.summary);
+      else hipLaunchKernelGGL(k_rec_link<kIndexer>, dim3(1), dim3(256), 0, s, E, a.g, a.x, a.entry, a.summary);
+      break;
+    case 2:
+      if (mode == kReader) hipLaunchKernelGGL(k_rec_count<kReader>, dim3(gb), dim3(tb), 0, s, E, a.entry, a.cnt, a.err, a.need);
+      else hipLaunchKernelGGL(k_rec_count<kIndexer>, dim3(gb), dim3(tb), 0, s, E, a.entry, a.cnt, a.err, a.need);
+      break;
+    case 3:
+      if (mode == kReader) hipLaunchKernelGGL(k_rec_emit<kReader>, dim3(gb), dim3(tb), 0, s, E, a.entry, a.cnt, a.base, a.rec_pos, a.rec_voff);
+      else hipLaunchKernelGGL(k_rec_emit<kIndexer>, dim3(gb), dim3(tb), 0, s, E, a.entry, a.cnt, a.base, a.rec_pos, a.rec_voff);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_rec_decode(const uint8_t* u, const uint64_t* rec_pos, uint64_t n, const Columns& col,
+                             hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rec_decode, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, u, rec_pos, n, col);
+  return hipGetLastError();
+}
+hipError_t launch_first_error_hout(const HuffOut* hout, uint32_t b0, uint32_t nb, uint32_t* first, hipStream_t s) {
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_first_error_hout, dim3((nb + 255) / 256), dim3(256), 0, s, hout, b0, nb, first);
+  return hipGetLastError();
+}
+hipError_t launch_first_error_i32(const int32_t* err, uint32_t nb, uint32_t* first, hipStream_t s) {
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_first_error_i32, dim3((nb + 255) / 256), dim3(256), 0, s, err, nb, first);
+  return hipGetLastError();
+}
+hipError_t launch_truncate_counts(uint32_t* cnt, uint32_t nb, const uint32_t* cut, hipStream_t s) {
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_truncate_counts, dim3((nb + 255) / 256), dim3(256), 0, s, cnt, nb, cut);
+  return hipGetLastError();
+}
+hipError_t launch_sbi_emit(const uint64_t* voff, uint64_t n, uint32_t g, uint64_t* ent, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sbi_emit, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, voff, n, g, ent);
+  return hipGetLastError();
+}
+
+}  // namespace hbam

@@ -1,0 +1,54 @@
+// hbam_launch.h -- host-callable launch wrappers for the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hbam_device.h"
+
+namespace hbam {
+
+struct ChainArgs {
+  const uint8_t* u;
+  const BlockInfo* blocks;
+  uint64_t e_inf, e_true, p0, q_end;
+  const uint64_t* dead;
+  uint32_t ndead;
+  int32_t n_ref;
+  uint32_t k0, k1;
+  // per-block scratch (indexed by k - k0)
+  uint64_t *g, *x, *entry, *summary, *base;
+  uint32_t* cnt;
+  int32_t* err;
+  unsigned long long* need;
+  // outputs
+  uint64_t *rec_pos, *rec_voff;
+};
+
+hipError_t launch_bgzf_scan(const uint8_t* file, uint64_t lo, uint64_t hi, uint64_t* cand, uint32_t cap,
+                            uint32_t* count, hipStream_t s);
+hipError_t launch_bgzf_verify(const uint8_t* file, uint64_t lo, uint64_t hi, const uint64_t* cand, uint32_t n,
+                              BlockInfo* blocks, uint32_t* flags, hipStream_t s);
+hipError_t launch_bgzf_walk(const uint8_t* file, uint64_t lo, uint64_t hi, BlockInfo* blocks, uint32_t cap,
+                            uint32_t* out, hipStream_t s);
+hipError_t launch_block_ustart(BlockInfo* blocks, uint32_t n, uint64_t* tmp_isize, uint64_t* tmp_ustart,
+                               void* scan_tmp, size_t* scan_bytes, hipStream_t s);
+hipError_t sort_u64(void* tmp, size_t* tmp_bytes, uint64_t* keys_in, uint64_t* keys_out, uint32_t n,
+                    hipStream_t s);
+hipError_t scan_u32_to_u64(void* tmp, size_t* tmp_bytes, const uint32_t* in, uint64_t* out, uint32_t n,
+                           hipStream_t s);
+hipError_t launch_inflate(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
+                          uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint8_t* u, hipStream_t s);
+hipError_t launch_inflate_huff(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
+                               uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, hipStream_t s);
+hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb, uint64_t chunk_ustart,
+                               const uint32_t* tokens, const HuffOut* hout, uint8_t* u, hipStream_t s);
+// stage: 0 guess, 1 link, 2 count, 3 emit
+hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s);
+hipError_t launch_rec_decode(const uint8_t* u, const uint64_t* rec_pos, uint64_t n, const Columns& col,
+                             hipStream_t s);
+hipError_t launch_first_error_hout(const HuffOut* hout, uint32_t b0, uint32_t nb, uint32_t* first, hipStream_t s);
+hipError_t launch_first_error_i32(const int32_t* err, uint32_t nb, uint32_t* first, hipStream_t s);
+hipError_t launch_truncate_counts(uint32_t* cnt, uint32_t nb, const uint32_t* cut, hipStream_t s);
+hipError_t launch_sbi_emit(const uint64_t* voff, uint64_t n, uint32_t g, uint64_t* ent, hipStream_t s);
+
+}  // namespace hbam

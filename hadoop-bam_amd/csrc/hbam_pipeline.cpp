@@ -1,0 +1,454 @@
+// hbam_pipeline.cpp -- host orchestration of the gfx950 BAM read pipeline.
+#include "hbam_pipeline.h"
+
+#include <algorithm>
+#include <cstring>
+
+#include "hbam_launch.h"
+
+namespace hbam {
+
+namespace {
+constexpr uint32_t kInflateChunkBlocks = 16384;  // blocks per phase-A/B launch pair
+constexpr int kMaxChainIters = 64;
+}  // namespace
+
+Pipeline::Pipeline(int device) : device_(device) {
+  if (hipSetDevice(device) != hipSuccess) {
+    err_ = "hipSetDevice failed";
+    return;
+  }
+  if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) err_ = "hipStreamCreate failed";
+  for (auto& e : ev_) (void)hipEventCreate(&e);
+}
+
+Pipeline::~Pipeline() {
+  (void)hipSetDevice(device_);
+  if (own_file_ && dfile_) (void)hipFree(dfile_);
+  for (auto& e : ev_) (void)hipEventDestroy(e);
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+int Pipeline::fail(int code, const std::string& msg) {
+  err_ = msg;
+  return code;
+}
+
+int Pipeline::hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return kOk;
+  err_ = std::string(what) + ": " + hipGetErrorString(e);
+  return kErrDevice;
+}
+
+#define HIPCHK(expr)                                   \
+  do {                                                 \
+    int _rc = hip_check((expr), #expr);                \
+    if (_rc != kOk) return _rc;                        \
+  } while (0)
+
+int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base_offset) {
+  HIPCHK(hipSetDevice(device_));
+  if (own_file_ && dfile_) (void)hipFree(dfile_);
+  dfile_ = nullptr;
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(&dfile_), len + kFilePad));
+  own_file_ = true;
+  if (len) HIPCHK(hipMemcpyAsync(dfile_, data, len, hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipMemsetAsync(dfile_ + len, 0, kFilePad, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  flen_ = len;
+  base_ = base_offset;
+  hblocks_.clear();
+  total_u_ = 0;
+  return kOk;
+}
+
+int Pipeline::attach_device(const uint8_t* dptr, uint64_t len, uint64_t base_offset) {
+  if (own_file_ && dfile_) (void)hipFree(dfile_);
+  dfile_ = const_cast<uint8_t*>(dptr);
+  own_file_ = false;
+  flen_ = len;
+  base_ = base_offset;
+  hblocks_.clear();
+  total_u_ = 0;
+  return kOk;
+}
+
+int Pipeline::locate() {
+  HIPCHK(hipSetDevice(device_));
+  if (timing) HIPCHK(hipEventRecord(ev_[0], stream_));
+  const uint8_t* fbase = dfile_ - base_;  // absolute file coordinates
+  const uint64_t lo = base_, hi = base_ + flen_;
+  // candidate capacity assumes >= 1 KiB per block on average; denser files
+  // (or any chain break) take the serial walk, whose table bound is len/26.
+  const uint32_t cap = (uint32_t)std::min<uint64_t>(flen_ / 1024 + 4096, 0x7fffffffu);
+  const uint32_t walk_cap = (uint32_t)std::min<uint64_t>(flen_ / 26 + 16, 0x7fffffffu);
+  DevBuf<uint64_t> cand, sorted;
+  HIPCHK(cand.reserve(cap));
+  HIPCHK(flags_.reserve(4));
+  uint32_t init[4] = {0, 0, 0xffffffffu, 0};
+  HIPCHK(hipMemcpyAsync(flags_.p, init, sizeof init, hipMemcpyHostToDevice, stream_));
+  // flags_[0] = candidate count, flags_[1] = chain break, flags_[2] = first big ISIZE
+  HIPCHK(launch_bgzf_scan(fbase, lo, hi, cand.p, cap, flags_.p, stream_));
+  uint32_t count = 0;
+  HIPCHK(hipMemcpyAsync(&count, flags_.p, 4, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  bool serial = count > cap || (count == 0 && flen_ > 0);
+  uint32_t n = serial ? 0 : count;
+  if (!serial && n > 0) {
+    HIPCHK(dblocks_.reserve(n + 1));
+    HIPCHK(sorted.reserve(n));
+    size_t tmp_bytes = 0;
+    HIPCHK(sort_u64(nullptr, &tmp_bytes, cand.p, sorted.p, n, stream_));
+    HIPCHK(scan_tmp_.reserve(tmp_bytes + 16));
+    HIPCHK(sort_u64(scan_tmp_.p, &tmp_bytes, cand.p, sorted.p, n, stream_));
+    HIPCHK(launch_bgzf_verify(fbase, lo, hi, sorted.p, n, dblocks_.p, flags_.p + 1, stream_));
+    uint32_t fl[2];
+    HIPCHK(hipMemcpyAsync(fl, flags_.p + 1, 8, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    if (fl[0]) serial = true;
+    else if (fl[1] != 0xffffffffu) return fail(kErrFormat, "BGZF block with ISIZE > 65536 (unsupported on device)");
+  }
+  if (serial) {
+    uint32_t out[4];
+    HIPCHK(dblocks_.reserve(walk_cap + 1));
+    HIPCHK(hipMemsetAsync(flags_.p, 0, 16, stream_));
+    HIPCHK(launch_bgzf_walk(fbase, lo, hi, dblocks_.p, walk_cap, flags_.p, stream_));
+    HIPCHK(hipMemcpyAsync(out, flags_.p, 16, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    n = out[0];
+    if (out[1] != kOk) {
+      uint64_t at = (uint64_t)out[2] | ((uint64_t)out[3] << 32);
+      return fail((int)out[1], "malformed BGZF block at offset " + std::to_string(at));
+    }
+  }
+  HIPCHK(dblocks_.reserve(n + 1));
+  DevBuf<uint64_t> isz, ust;
+  HIPCHK(isz.reserve(n + 1));
+  HIPCHK(ust.reserve(n + 1));
+  size_t sb = 0;
+  HIPCHK(launch_block_ustart(dblocks_.p, n, isz.p, ust.p, nullptr, &sb, stream_));
+  HIPCHK(scan_tmp_.reserve(sb + 16));
+  HIPCHK(launch_block_ustart(dblocks_.p, n, isz.p, ust.p, scan_tmp_.p, &sb, stream_));
+  hblocks_.resize(n);
+  if (n) HIPCHK(hipMemcpyAsync(hblocks_.data(), dblocks_.p, n * sizeof(BlockInfo), hipMemcpyDeviceToHost, stream_));
+  if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  if (timing) (void)hipEventElapsedTime(&times.locate, ev_[0], ev_[1]);
+  total_u_ = n ? hblocks_[n - 1].ustart + hblocks_[n - 1].isize : 0;
+  HIPCHK(du_.reserve(total_u_ + kUPad));
+  HIPCHK(hipMemsetAsync(du_.p + total_u_, 0, kUPad, stream_));
+  inflated_.assign(n, 0);
+  HIPCHK(hout_.reserve(n + 1));
+  // dead positions: [htsjdk] an empty block right after an exhausted one
+  std::vector<uint64_t> dead;
+  for (uint32_t k = 1; k < n; ++k)
+    if (hblocks_[k].isize == 0 && (dead.empty() || dead.back() != hblocks_[k].ustart)) dead.push_back(hblocks_[k].ustart);
+  HIPCHK(dead_.reserve(dead.size() + 1));
+  if (!dead.empty())
+    HIPCHK(hipMemcpyAsync(dead_.p, dead.data(), dead.size() * 8, hipMemcpyHostToDevice, stream_));
+  ndead_ = (uint32_t)dead.size();
+  HIPCHK(hipStreamSynchronize(stream_));
+  return kOk;
+}
+
+int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force) {
+  HIPCHK(hipSetDevice(device_));
+  const uint32_t nblk = (uint32_t)hblocks_.size();
+  b1 = std::min(b1, nblk);
+  if (b0 >= b1) return kOk;
+  const uint8_t* fbase = dfile_ - base_;
+  if (timing) HIPCHK(hipEventRecord(ev_[2], stream_));
+  float huff_ms = 0, lz_ms = 0;
+  uint32_t b = b0;
+  bool any = false;
+  while (b < b1) {
+    if (!force && inflated_[b]) { ++b; continue; }
+    uint32_t e = b;
+    while (e < b1 && e - b < kInflateChunkBlocks && (force || !inflated_[e])) ++e;
+    const uint64_t cu = hblocks_[b].ustart;
+    const uint64_t uend = hblocks_[e - 1].ustart + hblocks_[e - 1].isize;
+    HIPCHK(tokens_.reserve(std::max<uint64_t>(uend - cu, 64)));
+    if (timing) {
+      HIPCHK(hipEventRecord(ev_[4], stream_));
+      HIPCHK(launch_inflate_huff(fbase, dblocks_.p, b, e - b, cu, tokens_.p, hout_.p, stream_));
+      HIPCHK(hipEventRecord(ev_[5], stream_));
+      HIPCHK(launch_inflate_lz77(dblocks_.p, b, e - b, cu, tokens_.p, hout_.p, du_.p, stream_));
+      HIPCHK(hipEventRecord(ev_[6], stream_));
+      HIPCHK(hipEventSynchronize(ev_[6]));
+      float a = 0, c = 0;
+      (void)hipEventElapsedTime(&a, ev_[4], ev_[5]);
+      (void)hipEventElapsedTime(&c, ev_[5], ev_[6]);
+      huff_ms += a;
+      lz_ms += c;
+    } else {
+      HIPCHK(launch_inflate(fbase, dblocks_.p, b, e - b, cu, tokens_.p, hout_.p, du_.p, stream_));
+    }
+    for (uint32_t k = b; k < e; ++k) inflated_[k] = 1;
+    any = true;
+    b = e;
+  }
+  if (!any) return kOk;
+  HIPCHK(flags_.reserve(4));
+  const uint32_t none = 0xffffffffu;
+  HIPCHK(hipMemcpyAsync(flags_.p + 3, &none, 4, hipMemcpyHostToDevice, stream_));
+  HIPCHK(launch_first_error_hout(hout_.p, b0, b1 - b0, flags_.p + 3, stream_));
+  uint32_t first = none;
+  HIPCHK(hipMemcpyAsync(&first, flags_.p + 3, 4, hipMemcpyDeviceToHost, stream_));
+  if (timing) HIPCHK(hipEventRecord(ev_[3], stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  if (timing) {
+    (void)hipEventElapsedTime(&times.inflate, ev_[2], ev_[3]);
+    times.huff = huff_ms;
+    times.lz77 = lz_ms;
+  }
+  if (first != none) {
+    HuffOut ho;
+    HIPCHK(hipMemcpy(&ho, hout_.p + b0 + first, sizeof ho, hipMemcpyDeviceToHost));
+    for (uint32_t k = b0; k < b1; ++k) inflated_[k] = 0;
+    const BlockInfo& bad = hblocks_[b0 + first];
+    const char* what = ho.status == kErrFormat ? "Did not inflate expected amount" : "invalid DEFLATE data";
+    return fail(ho.status, std::string(what) + " in BGZF block at offset " + std::to_string(bad.coff));
+  }
+  return kOk;
+}
+
+uint32_t Pipeline::block_containing(uint64_t pos) const {
+  // first block with ustart + isize > pos (non-empty block containing pos)
+  uint32_t lo = 0, hi = (uint32_t)hblocks_.size();
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) / 2;
+    if (hblocks_[mid].ustart + hblocks_[mid].isize > pos) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+
+// [htsjdk] BlockCompressedInputStream.getFilePointer normalization.
+uint64_t Pipeline::voff_of(uint64_t pos) const {
+  const uint32_t n = (uint32_t)hblocks_.size();
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) / 2;
+    if (hblocks_[mid].ustart >= pos) hi = mid; else lo = mid + 1;
+  }
+  if (lo < n && hblocks_[lo].ustart == pos) return hblocks_[lo].coff << 16;
+  if (lo == 0) return base_ << 16;
+  const BlockInfo& b = hblocks_[lo - 1];
+  if (pos - b.ustart < b.isize) return (b.coff << 16) | (pos - b.ustart);
+  return (b.coff + b.csize) << 16;
+}
+
+int64_t Pipeline::pos_of_voff(uint64_t voff) const {
+  const uint64_t coff = voff >> 16, uoff = voff & 0xffff;
+  const uint32_t n = (uint32_t)hblocks_.size();
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) / 2;
+    if (hblocks_[mid].coff >= coff) hi = mid; else lo = mid + 1;
+  }
+  if (lo >= n) return (coff == base_ + flen_ && uoff == 0) ? (int64_t)total_u_ : -1;
+  if (hblocks_[lo].coff != coff || uoff > hblocks_[lo].isize) return -1;
+  return (int64_t)(hblocks_[lo].ustart + uoff);
+}
+
+// Smallest position q with voff_of(q) >= vend (voffs increase with q).
+uint64_t Pipeline::q_end_of(uint64_t vend) const {
+  const uint64_t c = vend >> 16, u = vend & 0xffff;
+  const uint32_t n = (uint32_t)hblocks_.size();
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) / 2;
+    if (hblocks_[mid].coff >= c) hi = mid; else lo = mid + 1;
+  }
+  if (lo >= n) return total_u_ + 1;  // every position qualifies
+  const BlockInfo& b = hblocks_[lo];
+  if (b.coff == c) return b.ustart + std::min<uint64_t>(u, b.isize);
+  return b.ustart;
+}
+
+int Pipeline::read_stream(uint64_t pos, uint64_t len, std::vector<uint8_t>* out) {
+  out->clear();
+  if (pos >= total_u_) return kOk;
+  len = std::min(len, total_u_ - pos);
+  uint32_t b0 = block_containing(pos), b1 = block_containing(pos + len - 1) + 1;
+  int rc = inflate(b0, b1);
+  if (rc != kOk) return rc;
+  out->resize(len);
+  HIPCHK(hipMemcpyAsync(out->data(), du_.p + pos, len, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  return kOk;
+}
+
+int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool decode, SpanDev* out) {
+  HIPCHK(hipSetDevice(device_));
+  *out = SpanDev();
+  const int64_t sp = pos_of_voff(vstart);
+  if (sp < 0) return fail(kErrIO, "Invalid file pointer: " + std::to_string(vstart));
+  const uint64_t p0 = (uint64_t)sp;
+  const uint64_t q_end = q_end_of(vend);
+  out->p0 = p0;
+  out->q_end = q_end;
+  const uint32_t nblk = (uint32_t)hblocks_.size();
+  if (p0 >= q_end || p0 >= total_u_) return kOk;
+  const uint32_t k0 = block_containing(p0);
+  uint32_t k1 = std::min(nblk, block_containing(std::min(q_end, total_u_) - 1) + 1);
+  uint32_t inf_end = std::min(nblk, k1 + 2);
+  ChainArgs a{};
+  a.blocks = dblocks_.p;
+  a.e_true = total_u_;
+  a.p0 = p0;
+  a.q_end = q_end;
+  a.dead = dead_.p;
+  a.ndead = ndead_;
+  a.n_ref = n_ref_;
+  a.k0 = k0;
+  if (timing) HIPCHK(hipEventRecord(ev_[0], stream_));
+  float infl_ms = 0;
+  for (int it = 0;; ++it) {
+    if (it >= kMaxChainIters) return fail(kErrState, "record chain did not converge");
+    int rc = inflate(k0, inf_end);
+    if (timing) infl_ms += times.inflate;
+    if (rc != kOk) return rc;
+    a.u = du_.p;
+    a.e_inf = inf_end < nblk ? hblocks_[inf_end].ustart : total_u_;
+    a.k1 = k1;
+    const uint32_t nb = k1 - k0;
+    HIPCHK(g_.reserve(nb));
+    HIPCHK(x_.reserve(nb));
+    HIPCHK(entry_.reserve(nb));
+    HIPCHK(summary_.reserve(4));
+    HIPCHK(cnt_.reserve(nb + 1));
+    HIPCHK(errv_.reserve(nb + 1));
+    HIPCHK(need_.reserve(1));
+    a.g = g_.p;
+    a.x = x_.p;
+    a.entry = entry_.p;
+    a.summary = summary_.p;
+    a.cnt = cnt_.p;
+    a.err = errv_.p;
+    a.need = need_.p;
+    HIPCHK(hipMemsetAsync(need_.p, 0, 8, stream_));
+    HIPCHK(launch_chain(a, mode, 0, stream_));
+    HIPCHK(launch_chain(a, mode, 1, stream_));
+    HIPCHK(launch_chain(a, mode, 2, stream_));
+    uint64_t sm[2] = {0, 0};
+    unsigned long long need = 0;
+    HIPCHK(hipMemcpyAsync(sm, summary_.p, 16, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipMemcpyAsync(&need, need_.p, 8, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    const uint64_t final_pos = sm[0];
+    const bool stopped = sm[1] != 0;
+    if (need > a.e_inf && inf_end < nblk) {  // a record needs bytes beyond the inflated range
+      inf_end = std::min(nblk, block_containing(std::min<uint64_t>(need, total_u_) - 1) + 2);
+      continue;
+    }
+    if (stopped && final_pos + 36 > a.e_inf && inf_end < nblk) {
+      inf_end = std::min(nblk, inf_end + 4);
+      continue;
+    }
+    if (!stopped && final_pos < q_end && final_pos < total_u_ && k1 < nblk && final_pos >= hblocks_[k1].ustart) {
+      k1 = std::min(nblk, block_containing(std::min(final_pos, q_end - 1)) + 1);
+      inf_end = std::max(inf_end, std::min(nblk, k1 + 2));
+      continue;
+    }
+    break;
+  }
+  const uint32_t nb = k1 - k0;
+  // first failing block: records before it stand, later blocks are dropped
+  const uint32_t none = 0xffffffffu;
+  HIPCHK(hipMemcpyAsync(flags_.p + 3, &none, 4, hipMemcpyHostToDevice, stream_));
+  HIPCHK(launch_first_error_i32(errv_.p, nb, flags_.p + 3, stream_));
+  uint32_t first = none;
+  HIPCHK(hipMemcpyAsync(&first, flags_.p + 3, 4, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  if (first != none) {
+    int32_t code = 0;
+    HIPCHK(hipMemcpy(&code, errv_.p + first, 4, hipMemcpyDeviceToHost));
+    HIPCHK(launch_truncate_counts(cnt_.p, nb, flags_.p + 3, stream_));
+    out->status = code;
+    const BlockInfo& b = hblocks_[k0 + first];
+    const char* what = code == kErrFormat ? "Invalid record length"
+                       : code == kErrTrunc ? "Premature EOF in BAM record"
+                       : code == kErrArg   ? "Reference index not found in sequence dictionary"
+                                           : "Invalid alignment";
+    out->error = std::string(what) + " (BGZF block at offset " + std::to_string(b.coff) + ")";
+  }
+  HIPCHK(base_arr_.reserve(nb + 1));
+  size_t tb = 0;
+  HIPCHK(scan_u32_to_u64(nullptr, &tb, cnt_.p, base_arr_.p, nb, stream_));
+  HIPCHK(scan_tmp_.reserve(tb + 16));
+  HIPCHK(scan_u32_to_u64(scan_tmp_.p, &tb, cnt_.p, base_arr_.p, nb, stream_));
+  uint64_t last_base = 0;
+  uint32_t last_cnt = 0;
+  HIPCHK(hipMemcpyAsync(&last_base, base_arr_.p + nb - 1, 8, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipMemcpyAsync(&last_cnt, cnt_.p + nb - 1, 4, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  const uint64_t total = last_base + last_cnt;
+  HIPCHK(rec_pos_.reserve(total + 1));
+  HIPCHK(rec_voff_.reserve(total + 1));
+  a.base = base_arr_.p;
+  a.rec_pos = rec_pos_.p;
+  a.rec_voff = rec_voff_.p;
+  HIPCHK(launch_chain(a, mode, 3, stream_));
+  if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
+  out->n = total;
+  out->rec_pos = rec_pos_.p;
+  out->rec_voff = rec_voff_.p;
+  if (decode && mode == kReader) {
+    // SoA backing store: 8-byte columns first, then 4, 2, 1 (alignment)
+    const uint64_t n = std::max<uint64_t>(total, 1);
+    const uint64_t per = 8 * 2 + 4 * 7 + 2 * 3 + 1 * 2;
+    if (cols_cap_ < n) {
+      HIPCHK(cols_.reserve(n * per + 256));
+      cols_cap_ = n;
+    }
+    uint8_t* p = cols_.p;
+    auto take = [&](uint64_t bytes) {
+      uint8_t* r = p;
+      p += (bytes + 15) & ~15ull;
+      return r;
+    };
+    Columns& c = out->col;
+    c.key = reinterpret_cast<int64_t*>(take(8 * n));
+    c.rest_off = reinterpret_cast<uint64_t*>(take(8 * n));
+    c.voff = rec_voff_.p;
+    c.ref_id = reinterpret_cast<int32_t*>(take(4 * n));
+    c.pos = reinterpret_cast<int32_t*>(take(4 * n));
+    c.l_seq = reinterpret_cast<int32_t*>(take(4 * n));
+    c.next_ref_id = reinterpret_cast<int32_t*>(take(4 * n));
+    c.next_pos = reinterpret_cast<int32_t*>(take(4 * n));
+    c.tlen = reinterpret_cast<int32_t*>(take(4 * n));
+    c.rest_len = reinterpret_cast<uint32_t*>(take(4 * n));
+    c.bin = reinterpret_cast<uint16_t*>(take(2 * n));
+    c.n_cigar = reinterpret_cast<uint16_t*>(take(2 * n));
+    c.flag = reinterpret_cast<uint16_t*>(take(2 * n));
+    c.l_read_name = take(n);
+    c.mapq = take(n);
+    HIPCHK(launch_rec_decode(du_.p, rec_pos_.p, total, c, stream_));
+  }
+  if (timing) HIPCHK(hipEventRecord(ev_[2], stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  if (timing) {
+    float all = 0, dec = 0;
+    (void)hipEventElapsedTime(&all, ev_[0], ev_[1]);
+    (void)hipEventElapsedTime(&dec, ev_[1], ev_[2]);
+    times.chain = all - infl_ms;
+    times.decode = dec;
+    times.inflate = infl_ms;
+  }
+  return kOk;
+}
+
+int Pipeline::splitting_entries(const SpanDev& span, uint32_t g, std::vector<uint64_t>* out) {
+  out->clear();
+  const uint64_t m = span.n / g;
+  if (m == 0) return kOk;
+  DevBuf<uint64_t> ent;
+  HIPCHK(ent.reserve(m + 1));
+  HIPCHK(launch_sbi_emit(span.rec_voff, span.n, g, ent.p, stream_));
+  out->resize(m);
+  HIPCHK(hipMemcpyAsync(out->data(), ent.p + 1, m * 8, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  return kOk;
+}
+
+}  // namespace hbam

@@ -1,0 +1,142 @@
+// hbam_pipeline.h -- one-GPU device pipeline for the BAM read hot path.
+//
+// Owns the device-resident compressed file, its BGZF block table, the
+// inflated stream and the per-span record arrays.  All compute runs in the
+// gfx950 kernels of hbam_kernels.hip; the host only sizes buffers, launches,
+// and reads back counters.  There is no CPU fallback: any HIP failure is an
+// error returned to the caller.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "hbam_device.h"
+
+namespace hbam {
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;  // elements
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  // grow-only (contents not preserved)
+  hipError_t reserve(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    release();
+    size_t c = count ? count : 1;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), c * sizeof(T));
+    if (e == hipSuccess) n = c;
+    return e;
+  }
+};
+
+// Result of one span decode, resident on the device.
+struct SpanDev {
+  uint64_t n = 0;                 // records
+  uint64_t p0 = 0, q_end = 0;     // logical positions
+  int status = kOk;               // status of the first failing record (records before it are valid)
+  std::string error;
+  uint64_t* rec_pos = nullptr;    // device
+  uint64_t* rec_voff = nullptr;   // device
+  Columns col{};                  // device (reader mode + decode)
+};
+
+struct StageTimes {  // milliseconds of the last decode (HIP events)
+  float locate = 0, inflate = 0, huff = 0, lz77 = 0, chain = 0, decode = 0;
+};
+
+class Pipeline {
+ public:
+  explicit Pipeline(int device);
+  ~Pipeline();
+  Pipeline(const Pipeline&) = delete;
+  Pipeline& operator=(const Pipeline&) = delete;
+
+  int device() const { return device_; }
+  hipStream_t stream() const { return stream_; }
+  const std::string& error() const { return err_; }
+
+  // Copy a BGZF file (or a BGZF-aligned shard) into HBM.  base_offset is the
+  // file offset of data[0] (shards); voffs are reported in file coordinates.
+  int load(const uint8_t* data, uint64_t len, uint64_t base_offset = 0);
+  // Use an already device-resident buffer (must be padded by kFilePad bytes).
+  int attach_device(const uint8_t* dptr, uint64_t len, uint64_t base_offset = 0);
+  uint64_t file_len() const { return flen_; }
+  const uint8_t* d_file() const { return dfile_; }
+
+  // BGZF block discovery over the whole loaded range.
+  int locate();
+  const std::vector<BlockInfo>& blocks() const { return hblocks_; }
+  uint64_t total_u() const { return total_u_; }
+  const BlockInfo* d_blocks() const { return dblocks_.p; }
+
+  // Inflate blocks [b0, b1) into the contiguous inflated stream.
+  int inflate(uint32_t b0, uint32_t b1, bool force = false);
+  const uint8_t* d_u() const { return du_.p; }
+
+  // Record chain over the span [vstart, vend) under reader or indexer rules;
+  // decode=true also fills the SoA columns + keys (reader mode only).
+  int decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool decode, SpanDev* out);
+
+  // Header bytes: inflate the first blocks until `need` stream bytes exist.
+  int read_stream(uint64_t pos, uint64_t len, std::vector<uint8_t>* out);
+
+  // .splitting-bai entries (without the leading header voff / trailing size)
+  int splitting_entries(const SpanDev& span, uint32_t granularity, std::vector<uint64_t>* out);
+
+  // host helpers on the block table
+  int64_t pos_of_voff(uint64_t voff) const;
+  uint64_t voff_of(uint64_t pos) const;
+  uint64_t q_end_of(uint64_t vend) const;
+  uint32_t block_containing(uint64_t pos) const;  // non-empty block with ustart <= pos < end, or nblocks
+
+  void set_n_ref(int32_t n) { n_ref_ = n; }
+  int32_t n_ref() const { return n_ref_; }
+
+  StageTimes times;
+  bool timing = false;  // record per-stage HIP event times
+
+ private:
+  int fail(int code, const std::string& msg);
+  int hip_check(hipError_t e, const char* what);
+
+  int device_ = 0;
+  hipStream_t stream_ = nullptr;
+  std::string err_;
+
+  uint8_t* dfile_ = nullptr;
+  bool own_file_ = false;
+  uint64_t flen_ = 0, base_ = 0;
+
+  DevBuf<BlockInfo> dblocks_;
+  std::vector<BlockInfo> hblocks_;
+  uint64_t total_u_ = 0;
+  uint32_t ndead_ = 0;
+  int32_t n_ref_ = 0;
+
+  DevBuf<uint8_t> du_;
+  std::vector<uint8_t> inflated_;  // per block flag
+  DevBuf<uint32_t> tokens_;
+  DevBuf<HuffOut> hout_;
+
+  // span scratch
+  DevBuf<uint64_t> g_, x_, entry_, base_arr_, summary_, dead_;
+  DevBuf<uint32_t> cnt_, flags_;
+  DevBuf<int32_t> errv_;
+  DevBuf<unsigned long long> need_;
+  DevBuf<uint64_t> rec_pos_, rec_voff_;
+  DevBuf<uint8_t> scan_tmp_;
+  DevBuf<uint8_t> cols_;  // SoA backing store
+  uint64_t cols_cap_ = 0;
+
+  hipEvent_t ev_[8];
+};
+
+}  // namespace hbam

@@ -1,0 +1,304 @@
+"""ctypes binding of libhbam.so (include/hbam.h) for tests and bench.py.
+
+There is no Python or CPU implementation of the hot path here: every call goes
+through the C ABI into the gfx950 kernels.  If the library is missing this
+module raises at import time (no silent fallback).
+"""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG, "lib", "libhbam.so")
+HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "hbam.h")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} is not built: run `make -C hadoop-bam_amd` (libhbam has no CPU fallback)")
+
+_L = C.CDLL(LIB_PATH)
+
+OK, E_FORMAT, E_TRUNC, E_ARG, E_IO, E_DEVICE, E_STATE, E_NOMEM = range(8)
+ERROR_NAMES = {1: "SAMFormatException", 2: "FileTruncatedException", 3: "IllegalArgumentException",
+               4: "IOException", 5: "DeviceError", 6: "IllegalStateException", 7: "OutOfMemoryError"}
+
+u64, i64, i32, u32, P = C.c_uint64, C.c_int64, C.c_int32, C.c_uint32, C.c_void_p
+
+
+class Opts(C.Structure):
+    _fields_ = [("device", i32), ("check_crc", i32), ("reserved0", i32), ("reserved1", i32)]
+
+
+class HeaderInfo(C.Structure):
+    _fields_ = [("n_ref", i32), ("l_text", i32), ("first_record_voff", u64), ("file_size", u64),
+                ("n_blocks", u64), ("uncompressed_size", u64), ("text", C.c_char_p)]
+
+
+_COLS = [("ref_id", np.int32), ("pos", np.int32), ("l_seq", np.int32), ("next_ref_id", np.int32),
+         ("next_pos", np.int32), ("tlen", np.int32), ("l_read_name", np.uint8), ("mapq", np.uint8),
+         ("bin", np.uint16), ("n_cigar", np.uint16), ("flag", np.uint16), ("key", np.int64),
+         ("voff", np.uint64), ("rest_off", np.uint64), ("rest_len", np.uint32)]
+
+
+class Batch(C.Structure):
+    _fields_ = [("n", u64)] + [(n, P) for n, _ in _COLS] + [("data", P), ("data_len", u64),
+                                                            ("status", i32), ("reserved", i32)]
+
+
+class GpuStats(C.Structure):
+    _fields_ = [("n_blocks", u64), ("compressed_bytes", u64), ("inflated_bytes", u64), ("records", u64),
+                ("first_voff", u64), ("last_voff", u64), ("key_xor", u64), ("voff_sum", u64),
+                ("ms_locate", C.c_float), ("ms_inflate", C.c_float), ("ms_huff", C.c_float),
+                ("ms_lz77", C.c_float), ("ms_chain", C.c_float), ("ms_decode", C.c_float),
+                ("ms_total", C.c_float), ("status", i32), ("reserved", i32)]
+
+
+def _sig(name, res, args):
+    f = getattr(_L, name)
+    f.restype = res
+    f.argtypes = args
+    return f
+
+
+_sig("hbam_abi_version", i32, [])
+_sig("hbam_open", C.c_int, [C.c_char_p, C.POINTER(Opts), C.POINTER(P)])
+_sig("hbam_open_mem", C.c_int, [P, u64, C.POINTER(Opts), C.POINTER(P)])
+_sig("hbam_open_bgzf", C.c_int, [P, u64, C.POINTER(Opts), C.POINTER(P)])
+_sig("hbam_close", None, [P])
+_sig("hbam_last_error", C.c_char_p, [P])
+_sig("hbam_free", None, [P])
+_sig("hbam_header", C.c_int, [P, C.POINTER(HeaderInfo)])
+_sig("hbam_ref", C.c_int, [P, i32, C.POINTER(C.c_char_p), C.POINTER(i32)])
+_sig("hbam_decode_span", C.c_int, [P, u64, u64, C.POINTER(Batch)])
+_sig("hbam_build_splitting_index", C.c_int, [P, i32, C.POINTER(P), C.POINTER(u64)])
+_sig("hbam_guess_record_starts", C.c_int, [P, P, P, u64, P])
+_sig("hbam_get_splits", C.c_int, [P, P, P, u64, P, u64, P, P, C.POINTER(u64)])
+_sig("hbam_blocks", C.c_int, [P, P, P, P, P, u64, C.POINTER(u64)])
+_sig("hbam_read_inflated", C.c_int, [P, u64, u64, P])
+_sig("hbam_get_key0", i64, [i32, i32])
+_sig("hbam_get_key", i64, [i32, i32])
+_sig("hbam_murmurhash3", i64, [P, u64, i32])
+_sig("hbam_device_count", i32, [])
+_sig("hbam_gpu_create", C.c_int, [i32, C.POINTER(P)])
+_sig("hbam_gpu_destroy", None, [P])
+_sig("hbam_gpu_error", C.c_char_p, [P])
+_sig("hbam_gpu_load", C.c_int, [P, P, u64, u64, i32, u64])
+_sig("hbam_gpu_run", C.c_int, [P, i32, C.POINTER(GpuStats)])
+_sig("hbam_gpu_fetch", C.c_int, [P, P, P, u64])
+
+
+def lib():
+    return _L
+
+
+def exported_symbols_from_header(path=HEADER_PATH):
+    """Function names declared in include/hbam.h."""
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(hbam_[a-z0-9_]+)\s*\(", txt)))
+
+
+class HbamError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{ERROR_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+def device_count():
+    return _L.hbam_device_count()
+
+
+def murmurhash3(data: bytes, seed=0):
+    return _L.hbam_murmurhash3(C.c_char_p(bytes(data)), len(data), seed)
+
+
+def get_key0(ref_idx, start0):
+    return _L.hbam_get_key0(ref_idx, start0)
+
+
+def get_key(ref_idx, alignment_start):
+    return _L.hbam_get_key(ref_idx, alignment_start)
+
+
+class BamFile:
+    """An opened BAM (or plain BGZF with bam=False) on one GPU."""
+
+    def __init__(self, data: bytes = None, path: str = None, device=0, bam=True, check_crc=False):
+        self._h = P()
+        o = Opts(device, int(check_crc), 0, 0)
+        if path is not None:
+            rc = _L.hbam_open(path.encode(), C.byref(o), C.byref(self._h))
+            self.size = os.path.getsize(path)
+        else:
+            self._buf = C.create_string_buffer(bytes(data), len(data))
+            fn = _L.hbam_open_mem if bam else _L.hbam_open_bgzf
+            rc = fn(self._buf, len(data), C.byref(o), C.byref(self._h))
+            self.size = len(data)
+        if rc != OK:
+            msg = _L.hbam_last_error(self._h).decode(errors="replace")
+            _L.hbam_close(self._h)
+            self._h = None
+            raise HbamError(rc, msg)
+        self.bam = bam
+
+    def close(self):
+        if self._h:
+            _L.hbam_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _err(self, rc):
+        return HbamError(rc, _L.hbam_last_error(self._h).decode(errors="replace"))
+
+    def header(self):
+        h = HeaderInfo()
+        rc = _L.hbam_header(self._h, C.byref(h))
+        if rc != OK:
+            raise self._err(rc)
+        text = C.string_at(h.text, h.l_text).decode(errors="replace") if h.l_text else ""
+        return {"n_ref": h.n_ref, "l_text": h.l_text, "first_record_voff": h.first_record_voff,
+                "file_size": h.file_size, "n_blocks": h.n_blocks,
+                "uncompressed_size": h.uncompressed_size, "text": text}
+
+    def ref(self, i):
+        name = C.c_char_p()
+        ln = i32()
+        rc = _L.hbam_ref(self._h, i, C.byref(name), C.byref(ln))
+        if rc != OK:
+            raise self._err(rc)
+        return name.value.decode(), ln.value
+
+    def decode_span(self, vstart, vend, raise_on_error=True):
+        """SoA dict for FileVirtualSplit [vstart, vend); 'status' holds the
+        status of a record that ended the span early."""
+        b = Batch()
+        rc = _L.hbam_decode_span(self._h, vstart, vend, C.byref(b))
+        if rc != OK and (raise_on_error or b.n == 0 and rc not in (E_FORMAT, E_TRUNC, E_ARG, E_IO)):
+            raise self._err(rc)
+        out = {"status": rc}
+        for name, dt in _COLS:
+            p = getattr(b, name)
+            nb = b.n * np.dtype(dt).itemsize
+            out[name] = np.frombuffer(C.string_at(p, nb), dt).copy() if b.n else np.zeros(0, dt)
+        out["data"] = C.string_at(b.data, b.data_len) if b.data_len else b""
+        return out
+
+    def decode_all(self, raise_on_error=True):
+        return self.decode_span(self.header()["first_record_voff"], (1 << 64) - 1, raise_on_error)
+
+    def splitting_index(self, granularity=4096) -> bytes:
+        p = P()
+        n = u64()
+        rc = _L.hbam_build_splitting_index(self._h, granularity, C.byref(p), C.byref(n))
+        if rc != OK:
+            raise self._err(rc)
+        b = C.string_at(p, n.value)
+        _L.hbam_free(p)
+        return b
+
+    def guess_record_starts(self, begs, ends):
+        n = len(begs)
+        b = np.ascontiguousarray(begs, np.uint64)
+        e = np.ascontiguousarray(ends, np.uint64)
+        out = np.zeros(max(n, 1), np.uint64)
+        rc = _L.hbam_guess_record_starts(self._h, b.ctypes.data, e.ctypes.data, n, out.ctypes.data)
+        if rc != OK:
+            raise self._err(rc)
+        return [int(x) for x in out[:n]]
+
+    def get_splits(self, starts, lengths, sbi: bytes = None):
+        n = len(starts)
+        s = np.ascontiguousarray(starts, np.uint64)
+        ln = np.ascontiguousarray(lengths, np.uint64)
+        vs = np.zeros(max(n, 1), np.uint64)
+        ve = np.zeros(max(n, 1), np.uint64)
+        nout = u64()
+        sb = C.create_string_buffer(sbi, len(sbi)) if sbi is not None else None
+        rc = _L.hbam_get_splits(self._h, s.ctypes.data, ln.ctypes.data, n, sb,
+                                len(sbi) if sbi is not None else 0, vs.ctypes.data, ve.ctypes.data,
+                                C.byref(nout))
+        if rc != OK:
+            raise self._err(rc)
+        return [(int(vs[i]), int(ve[i])) for i in range(nout.value)]
+
+    def blocks(self):
+        n = u64()
+        _L.hbam_blocks(self._h, None, None, None, None, 0, C.byref(n))
+        k = n.value
+        coff = np.zeros(max(k, 1), np.uint64)
+        csize = np.zeros(max(k, 1), np.uint32)
+        isize = np.zeros(max(k, 1), np.uint32)
+        ustart = np.zeros(max(k, 1), np.uint64)
+        rc = _L.hbam_blocks(self._h, coff.ctypes.data, csize.ctypes.data, isize.ctypes.data,
+                            ustart.ctypes.data, k, C.byref(n))
+        if rc != OK:
+            raise self._err(rc)
+        return {"coff": coff[:k], "csize": csize[:k], "isize": isize[:k], "ustart": ustart[:k]}
+
+    def read_inflated(self, pos, length):
+        buf = C.create_string_buffer(max(length, 1))
+        rc = _L.hbam_read_inflated(self._h, pos, length, buf)
+        if rc != OK:
+            raise self._err(rc)
+        return buf.raw[:length]
+
+
+class Gpu:
+    """Device-resident pipeline session (bench.py / multi-GPU shards)."""
+
+    def __init__(self, device=0):
+        self._h = P()
+        rc = _L.hbam_gpu_create(device, C.byref(self._h))
+        if rc != OK:
+            raise HbamError(rc, _L.hbam_gpu_error(None).decode())
+
+    def close(self):
+        if self._h:
+            _L.hbam_gpu_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load(self, data, base_offset=0, n_ref=0, first_pos=None):
+        if isinstance(data, np.ndarray):
+            ptr, n = data.ctypes.data, data.nbytes
+            self._keep = data
+        else:
+            self._keep = C.create_string_buffer(bytes(data), len(data))
+            ptr, n = self._keep, len(data)
+        fp = (1 << 64) - 1 if first_pos is None else first_pos
+        rc = _L.hbam_gpu_load(self._h, ptr, n, base_offset, n_ref, fp)
+        if rc != OK:
+            raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
+        self._keep = None
+
+    def run(self, timing=False, decode=True):
+        st = GpuStats()
+        rc = _L.hbam_gpu_run(self._h, (1 if timing else 0) | (0 if decode else 2), C.byref(st))
+        if rc != OK:
+            raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
+        return {f: getattr(st, f) for f, _ in GpuStats._fields_}
+
+    def fetch(self, n):
+        keys = np.zeros(max(n, 1), np.int64)
+        voffs = np.zeros(max(n, 1), np.uint64)
+        rc = _L.hbam_gpu_fetch(self._h, keys.ctypes.data, voffs.ctypes.data, n)
+        if rc != OK:
+            raise HbamError(rc, "fetch failed")
+        return keys[:n], voffs[:n]

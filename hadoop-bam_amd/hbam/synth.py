@@ -1,0 +1,53 @@
+"""Synthetic BAM inputs (ctypes over lib/libhbamgen.so, tools/gen_synth_bam.c).
+
+Input generation only: the generator compresses with zlib; nothing here is on
+the read path being measured.
+"""
+import ctypes as C
+import os
+
+_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib", "libhbamgen.so")
+_G = None
+
+STRATEGY = {"default": 0, "filtered": 1, "huffman": 2, "rle": 3, "fixed": 4}
+
+
+class _Params(C.Structure):
+    _fields_ = [("n_records", C.c_uint64), ("mode", C.c_int32), ("level", C.c_int32), ("strategy", C.c_int32),
+                ("block_payload", C.c_int32), ("threads", C.c_int32), ("eof_block", C.c_int32),
+                ("all_unmapped", C.c_int32), ("seed", C.c_uint64)]
+
+
+def _lib():
+    global _G
+    if _G is None:
+        if not os.path.exists(_LIB):
+            raise ImportError(f"{_LIB} not built: run `make -C hadoop-bam_amd`")
+        _G = C.CDLL(_LIB)
+        _G.gen_bam.argtypes = [C.POINTER(_Params), C.POINTER(C.c_void_p), C.POINTER(C.c_uint64),
+                               C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        _G.gen_free.argtypes = [C.c_void_p]
+    return _G
+
+
+def make_bam(n_records, mode="short", level=5, strategy="default", block_payload=65280, threads=None,
+             eof_block=True, all_unmapped=False, seed=0x48424D00, as_numpy=False):
+    """Return (bam_bytes_or_uint8_array, info dict)."""
+    import numpy as np
+    p = _Params(n_records, 1 if mode == "long" else 0, level, STRATEGY[strategy], block_payload,
+                threads or min(16, os.cpu_count() or 8), int(eof_block), int(all_unmapped), seed)
+    out = C.c_void_p()
+    n = C.c_uint64()
+    nb = C.c_uint64()
+    u = C.c_uint64()
+    rc = _lib().gen_bam(C.byref(p), C.byref(out), C.byref(n), C.byref(nb), C.byref(u))
+    if rc != 0:
+        raise RuntimeError(f"gen_bam failed ({rc})")
+    if as_numpy:
+        arr = np.empty(n.value, np.uint8)
+        C.memmove(arr.ctypes.data, out, n.value)
+        data = arr
+    else:
+        data = C.string_at(out, n.value)
+    _lib().gen_free(out)
+    return data, {"n_records": n_records, "compressed": n.value, "blocks": nb.value, "uncompressed": u.value}

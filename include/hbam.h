@@ -1,0 +1,176 @@
+/*
+ * hbam.h -- C ABI of the MI355X-native Hadoop-BAM read path (libhbam.so).
+ *
+ * This is the boundary a JNI shim behind org.seqdoop.hadoop_bam binds (see
+ * INTEGRATION.md).  Plain C: pointers, sizes and status codes only.  Every
+ * entry point names the reference interface it replaces (paths relative to
+ * /root/reference/src/main/java/org/seqdoop/hadoop_bam/).
+ *
+ * Status codes map 1:1 onto the Java exception a caller must raise:
+ *   HBAM_E_FORMAT -> htsjdk.samtools.SAMFormatException
+ *   HBAM_E_TRUNC  -> htsjdk.samtools.FileTruncatedException / RuntimeEOFException
+ *   HBAM_E_ARG    -> java.lang.IllegalArgumentException
+ *   HBAM_E_IO     -> java.io.IOException (RuntimeIOException for bad DEFLATE data)
+ *   HBAM_E_DEVICE -> java.io.IOException (HIP runtime failure; never a silent CPU path)
+ * The message is available from hbam_last_error(ctx).
+ *
+ * Threading: a ctx is single-threaded (RecordReader contract); the library is
+ * re-entrant across ctxs.  Each ctx owns one HIP stream on its device.
+ * Ownership: memory returned inside hbam_batch / hbam_header_info belongs to
+ * the ctx and stays valid until the next call on that ctx or hbam_close.
+ * Buffers returned through uint8_t** are released with hbam_free.
+ */
+#ifndef HBAM_H
+#define HBAM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HBAM_OK 0
+#define HBAM_E_FORMAT 1
+#define HBAM_E_TRUNC 2
+#define HBAM_E_ARG 3
+#define HBAM_E_IO 4
+#define HBAM_E_DEVICE 5
+#define HBAM_E_STATE 6
+#define HBAM_E_NOMEM 7
+
+#define HBAM_ABI_VERSION 1
+
+typedef struct hbam_ctx hbam_ctx;
+
+/* Reader options: the hadoopbam.* Configuration properties a JNI shim reads. */
+typedef struct hbam_opts {
+  int32_t device;     /* hadoopbam.gpu.device: HIP device ordinal (default 0) */
+  int32_t check_crc;  /* BlockCompressedInputStream.setCheckCrcs (default 0) */
+  int32_t reserved0;
+  int32_t reserved1;
+} hbam_opts;
+
+/* BAM header summary ([htsjdk] BAMFileReader.readHeader). */
+typedef struct hbam_header_info {
+  int32_t n_ref;                /* binary reference count (SAMSequenceDictionary size) */
+  int32_t l_text;               /* SAM header text length */
+  uint64_t first_record_voff;   /* getFilePointerSpanningReads().getFirstOffset() */
+  uint64_t file_size;           /* compressed bytes */
+  uint64_t n_blocks;            /* BGZF blocks */
+  uint64_t uncompressed_size;   /* inflated bytes of all blocks */
+  const char *text;             /* l_text bytes, owned by ctx */
+} hbam_header_info;
+
+/* One decoded span in SoA form: exactly the argument list of
+ * LazyBAMRecordFactory.createBAMRecord (LazyBAMRecordFactory.java:37-50)
+ * plus the BAMRecordReader key (BAMRecordReader.java:81-121) and the BGZF
+ * virtual offset of each record.  pos / next_pos are the 0-based BAM fields
+ * (htsjdk alignmentStart = pos + 1).  The rest of record i (read name, cigar,
+ * seq, qual, aux = getVariableBinaryRepresentation()) is
+ * data[rest_off[i] .. rest_off[i] + rest_len[i]). */
+typedef struct hbam_batch {
+  uint64_t n;
+  const int32_t *ref_id, *pos, *l_seq, *next_ref_id, *next_pos, *tlen;
+  const uint8_t *l_read_name, *mapq;
+  const uint16_t *bin, *n_cigar, *flag;
+  const int64_t *key;
+  const uint64_t *voff, *rest_off;
+  const uint32_t *rest_len;
+  const uint8_t *data;
+  uint64_t data_len;
+  int32_t status;      /* status of the record that ended the span early (0 = clean end) */
+  int32_t reserved;
+} hbam_batch;
+
+/* Open a BAM file / in-memory BAM: loads the compressed bytes into HBM,
+ * discovers every BGZF block on the GPU, inflates and parses the header.
+ * Replaces BAMRecordReader.initialize's SamReader construction
+ * (BAMRecordReader.java:142-149,186-200) and SAMHeaderReader.readSAMHeaderFrom
+ * (util/SAMHeaderReader.java:57-75). */
+int hbam_open(const char *path, const hbam_opts *opts, hbam_ctx **out);
+int hbam_open_mem(const void *data, uint64_t len, const hbam_opts *opts, hbam_ctx **out);
+/* Same, for a plain BGZF file (VCF/BCF payloads): no BAM header parse. */
+int hbam_open_bgzf(const void *data, uint64_t len, const hbam_opts *opts, hbam_ctx **out);
+void hbam_close(hbam_ctx *ctx);
+const char *hbam_last_error(hbam_ctx *ctx);
+void hbam_free(void *p);
+int32_t hbam_abi_version(void);
+
+int hbam_header(hbam_ctx *ctx, hbam_header_info *out);
+/* reference i of the binary dictionary: name (NUL-terminated, ctx-owned) and length */
+int hbam_ref(hbam_ctx *ctx, int32_t i, const char **name, int32_t *length);
+
+/* Decode every record of FileVirtualSplit [vstart, vend) (vStart inclusive,
+ * vEnd exclusive: FileVirtualSplit.java:82-86) exactly as
+ * BAMRecordReader.initialize + nextKeyValue loop would
+ * (BAMRecordReader.java:151-154,181-182,223-232).  Records before a failing
+ * record are returned with out->status set and the call returns that status. */
+int hbam_decode_span(hbam_ctx *ctx, uint64_t vstart, uint64_t vend, hbam_batch *out);
+
+/* SplittingBAMIndexer.index(in, out, inputSize, granularity)
+ * (SplittingBAMIndexer.java:248-290): the .splitting-bai bytes, big-endian u64
+ * entries, byte-identical to the reference.  *buf released with hbam_free. */
+int hbam_build_splitting_index(hbam_ctx *ctx, int32_t granularity, uint8_t **buf, uint64_t *len);
+
+/* BAMSplitGuesser.guessNextBAMRecordStart(beg, end) (BAMSplitGuesser.java:108-235)
+ * for n split points at once (one GPU launch); out[i] == ends[i] when no
+ * record start is found, as in the reference. */
+int hbam_guess_record_starts(hbam_ctx *ctx, const uint64_t *begs, const uint64_t *ends, uint64_t n,
+                             uint64_t *out);
+
+/* BAMInputFormat.getSplits for the FileSplits of one file
+ * (BAMInputFormat.java:222-318 addIndexedSplits, 469-530 addProbabilisticSplits).
+ * sbi = .splitting-bai bytes or NULL.  vstarts/vends need room for n entries. */
+int hbam_get_splits(hbam_ctx *ctx, const uint64_t *starts, const uint64_t *lengths, uint64_t n,
+                    const uint8_t *sbi, uint64_t sbi_len, uint64_t *vstarts, uint64_t *vends,
+                    uint64_t *nout);
+
+/* BGZF block table (coff, csize, isize, ustart) and inflated bytes: used by
+ * tests and by the BGZF text formats. */
+int hbam_blocks(hbam_ctx *ctx, uint64_t *coff, uint32_t *csize, uint32_t *isize, uint64_t *ustart,
+                uint64_t cap, uint64_t *n);
+int hbam_read_inflated(hbam_ctx *ctx, uint64_t pos, uint64_t len, uint8_t *dst);
+
+/* Static key helpers (BAMRecordReader.getKey0 :119-121, getKey(int,int) :114-116,
+ * MurmurHash3.murmurhash3(byte[],int) util/MurmurHash3.java:32-102): scalar API
+ * for the SAM/CRAM readers that call getKey; the batch path computes keys on
+ * the GPU. */
+int64_t hbam_get_key0(int32_t ref_idx, int32_t alignment_start0);
+int64_t hbam_get_key(int32_t ref_idx, int32_t alignment_start);
+int64_t hbam_murmurhash3(const void *key, uint64_t len, int32_t seed);
+
+/* ---- device-resident pipeline (benchmark / multi-GPU shard driver) ---- */
+typedef struct hbam_gpu hbam_gpu;
+
+typedef struct hbam_gpu_stats {
+  uint64_t n_blocks;          /* BGZF blocks discovered */
+  uint64_t compressed_bytes;  /* C */
+  uint64_t inflated_bytes;    /* U */
+  uint64_t records;           /* N */
+  uint64_t first_voff, last_voff;
+  uint64_t key_xor, voff_sum; /* order-independent digests of the keys / voffs */
+  float ms_locate, ms_inflate, ms_huff, ms_lz77, ms_chain, ms_decode, ms_total;
+  int32_t status;
+  int32_t reserved;
+} hbam_gpu_stats;
+
+int hbam_gpu_create(int32_t device, hbam_gpu **out);
+void hbam_gpu_destroy(hbam_gpu *g);
+const char *hbam_gpu_error(hbam_gpu *g);
+/* Load a whole BAM (base_offset = 0) or a BGZF-aligned shard of one. For a
+ * shard, first_pos is the inflated-stream offset (within the shard) of its
+ * first record start; for a whole file pass UINT64_MAX (use the header). */
+int hbam_gpu_load(hbam_gpu *g, const void *data, uint64_t len, uint64_t base_offset, int32_t n_ref,
+                  uint64_t first_pos);
+/* One pass of the hot path over the resident bytes: BGZF discovery, inflate,
+ * record scan, field decode + keys + voffs (flags bit0: also timing per stage,
+ * bit1: skip decode). */
+int hbam_gpu_run(hbam_gpu *g, int32_t flags, hbam_gpu_stats *stats);
+/* Copy results of the last run to the host (any pointer may be NULL). */
+int hbam_gpu_fetch(hbam_gpu *g, int64_t *keys, uint64_t *voffs, uint64_t cap);
+int32_t hbam_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HBAM_H */

@@ -1,0 +1,50 @@
+"""CPU: libhbam.so loads, exports every entry point include/hbam.h declares,
+its scalar key helpers match the oracle, and the product fails loudly without
+a GPU (no CPU fallback)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import hbam
+import orc
+import py_oracle
+
+
+def test_exports_every_declared_symbol():
+    names = hbam.exported_symbols_from_header()
+    assert len(names) >= 25
+    lib = C.CDLL(hbam.LIB_PATH)
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_abi_version():
+    assert hbam.lib().hbam_abi_version() == 1
+
+
+def test_static_keys_match_reference_semantics():
+    # BAMRecordReader.getKey0 / getKey (BAMRecordReader.java:114-121)
+    assert hbam.get_key0(1, 99) == 0x0000000100000063
+    assert hbam.get_key(1, 100) == 0x0000000100000063
+    assert hbam.get_key0(3, -1) == -1
+    assert hbam.get_key0(0x7FFFFFFF, -2) == -2
+    assert hbam.get_key0(-1, 5) == (-1 << 32) | 5
+
+
+def test_murmur_helper_matches_oracles():
+    rng = np.random.default_rng(1)
+    for n in list(range(0, 34)) + [255, 256, 257, 4096]:
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        for seed in (0, 123, -1):
+            assert hbam.murmurhash3(b, seed) == orc.murmurhash3(b, seed) == py_oracle.murmurhash3(b, seed)
+
+
+def test_no_gpu_fails_loudly(test_bam):
+    if hbam.device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(hbam.HbamError) as e:
+        hbam.BamFile(test_bam)
+    assert e.value.code == hbam.E_DEVICE
+    with pytest.raises(hbam.HbamError):
+        hbam.Gpu(0)

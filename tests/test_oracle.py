@@ -1,0 +1,126 @@
+"""CPU: the oracle (oracle/hbam_oracle.c) against the reference's own pins,
+the committed golden vectors and the independent Python restatement."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import orc
+import py_oracle
+from conftest import GOLDEN, golden_path
+
+
+def test_first_record_voff_pin(test_bam, golden):
+    # TestBAMSplitGuesser.java:17-23: guessNextBAMRecordStart(0, ..) == first record voff
+    s = orc.Stream(test_bam)
+    assert s.first_record_voff == 0x196A == golden["first_record_voff"]
+    assert s.guess_record_start(0, 3 * 0xFFFF + 0xFFFE) == 0x196A
+
+
+def test_records_match_golden(test_bam):
+    s = orc.Stream(test_bam)
+    rc, r = s.decode_all()
+    assert rc == 0
+    g = np.load(golden_path("test.bam.records.npz"))
+    for k in g.files:
+        np.testing.assert_array_equal(r[k], g[k], err_msg=k)
+    assert hashlib.sha256(r["key"].tobytes()).hexdigest().startswith("9cec72cb")
+
+
+@pytest.mark.parametrize("g", [1, 2, 10, 4096])
+def test_splitting_index_golden(test_bam, g):
+    s = orc.Stream(test_bam)
+    want = open(golden_path(f"test.bam.g{g}.splitting-bai"), "rb").read()
+    got = s.splitting_index(g)
+    assert got == want
+    # TestSplittingBAMIndexer.java:31-32: bamSize() == file length
+    assert int.from_bytes(got[-8:], "big") >> 16 == len(test_bam)
+    n = {1: 2279, 2: 1140, 10: 229, 4096: 2}[g]
+    assert len(got) // 8 == n
+
+
+def test_index_matches_processAlignment_semantics(test_bam):
+    # TestSplittingBAMIndexer: index() and processAlignment() give equal SplittingBAMIndex sets
+    s = orc.Stream(test_bam)
+    rc, r = s.decode_all()
+    for g in (2, 10, 4096):
+        ent = []
+        for c, v in enumerate(r["voff"]):
+            if c == 0 or (c + 1) % g == 0:
+                ent.append(int(v))
+        ent.append(len(test_bam) << 16)
+        idx = s.splitting_index(g)
+        got = {int.from_bytes(idx[i:i + 8], "big") for i in range(0, len(idx), 8)}
+        assert got == set(ent)
+
+
+def test_bgzf_text_fixtures(golden):
+    for f, t in golden["bgzf_text"].items():
+        data = open(golden_path(f), "rb").read()
+        x = orc.Stream(data, check_crc=True, parse_header=False)
+        assert hashlib.sha256(x.data).hexdigest() == t["sha256"] and len(x.data) == t["len"]
+        assert [int(b["coff"]) for b in x.blocks] == t["coffs"]
+
+
+@pytest.mark.parametrize("f,first,last", [("test.vcf.bgzf.gz", 821, 821), ("HiSeq.10000.vcf.bgzf.gz", 16688, 509222)])
+def test_bgzf_split_guesser_pins(f, first, last):
+    # TestBGZFSplitGuesser.java:32-63
+    data = open(golden_path(f), "rb").read()
+    bnd, start = [], 1
+    while True:
+        ns = orc.guess_next_bgzf_block_start(data, start, len(data))
+        if ns == len(data):
+            break
+        bnd.append(ns)
+        start = ns + 1
+    assert bnd[0] == first and bnd[-1] == last and bnd[-1] == len(data) - 28
+
+
+def test_guesser_golden(test_bam, golden):
+    s = orc.Stream(test_bam)
+    for beg, end, want in golden["guesses"]:
+        assert s.guess_record_start(beg, end) == want, (beg, end)
+
+
+def test_split_planning_golden(test_bam, golden):
+    s = orc.Stream(test_bam)
+    sbi = s.splitting_index(4096)
+    for p in golden["plans"]:
+        assert [list(x) for x in s.get_splits(p["starts"], p["lengths"], sbi)] == p["indexed"]
+        assert [list(x) for x in s.get_splits(p["starts"], p["lengths"], None)] == p["probabilistic"]
+
+
+def test_murmur_c_vs_python():
+    rng = np.random.default_rng(7)
+    for n in list(range(0, 40)) + [300, 331, 1000]:
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        for seed in (0, 1, -5):
+            assert orc.murmurhash3(b, seed) == py_oracle.murmurhash3(b, seed)
+
+
+def test_key_edge_cases():
+    # BAMRecordReader.java:81-121 worked examples
+    assert orc.get_key(1, 99, 0, b"") == 0x0000000100000063
+    assert orc.get_key(3, -1, 0, b"") == -1          # pos -1 mapped: sign-extended
+    k = orc.get_key(0, 5, 4, b"abc")                  # unmapped -> murmur branch
+    h = py_oracle.murmurhash3(b"abc") & 0xFFFFFFFF
+    h = h - (1 << 32) if h >> 31 else h
+    assert k == ((0x7FFFFFFF << 32) | (h & 0xFFFFFFFFFFFFFFFF)) - (1 << 64) * (h < 0)
+    assert orc.get_key(-1, -1, 0, b"xyz") == py_oracle.get_key(-1, -1, 0, b"xyz")
+    assert orc.get_key(2, -2, 0, b"q") == py_oracle.get_key(2, -2, 0, b"q")  # start < 0 -> hash
+
+
+@pytest.mark.parametrize("kw", [dict(n_records=1500), dict(n_records=60, mode="long"), dict(n_records=800, level=0),
+                                dict(n_records=800, strategy="fixed"), dict(n_records=400, all_unmapped=True)])
+def test_oracle_vs_python_synthetic(kw):
+    from hbam import synth
+    d, _ = synth.make_bam(**kw)
+    s = orc.Stream(d, check_crc=True)
+    rc, r = s.decode_all()
+    assert rc == 0
+    pr = py_oracle.records(d)
+    assert [k for _, k in pr] == [int(x) for x in r["key"]]
+    assert [v for v, _ in pr] == [int(x) for x in r["voff"]]
+    for g in (1, 7, 4096):
+        assert s.splitting_index(g) == py_oracle.splitting_index(d, g)
