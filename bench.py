@@ -46,7 +46,7 @@ def cpu_baseline(data, info, seconds):
         s = orc.Stream(data[:end])
         rc, r = s.decode_span(s.first_record_voff, (1 << 64) - 1)
         dt = time.perf_counter() - t
-        return dt, len(s.data), len(r["key"])
+        return dt, s.data_len, len(r["key"])
     nb = min(len(blocks), 200)
     dt, u, n = run(nb)
     target = max(nb, min(len(blocks), int(nb * seconds / max(dt, 1e-3))))

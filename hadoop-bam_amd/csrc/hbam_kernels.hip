@@ -744,6 +744,9 @@ __global__ __launch_bounds__(64) void k_rec_guess(ChainEnv E, uint64_t* __restri
             if (!plausible(E, q)) { valid = false; break; }
             q += 4 + (uint64_t)(int32_t)ldu32(E.u, q);
           }
+          // the exit must itself look like a record (or be the end / unreadable):
+          // rejects false starts whose garbage block_size jumps far ahead
+          if (valid && !(q == E.e_true || q + 36 > E.e_inf || plausible(E, q))) valid = false;
           if (valid) { g = c; x = q; break; }
         }
       }
@@ -818,6 +821,51 @@ __global__ __launch_bounds__(256) void k_rec_link(ChainEnv E, const uint64_t* __
     summary[0] = s_cur;
     summary[1] = (uint64_t)s_stop;
   }
+}
+
+// Parallel link.  y[i] = guess exit of block i (0 when the block has no
+// guess); in[i] = max(y[0..i-1]) is the position the chain enters block i
+// with, IF every guess is on the true chain.  k_rec_link_check verifies that
+// claim block by block (entry = guess where the chain enters the block,
+// pass-through elsewhere) and counts violations; any violation sends the span
+// to the exact serial link (k_rec_link).
+__global__ void k_rec_link_y(const uint64_t* __restrict__ g, const uint64_t* __restrict__ x, uint32_t nb,
+                             uint64_t* __restrict__ y) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nb) y[i] = (g[i] != kNone && x[i] != kNone) ? x[i] : 0;
+}
+
+__global__ void k_rec_link_check(ChainEnv E, const uint64_t* __restrict__ g, const uint64_t* __restrict__ x,
+                                 const uint64_t* __restrict__ in_scan, uint64_t* __restrict__ entry,
+                                 uint32_t* __restrict__ fails) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nb = E.k1 - E.k0;
+  if (i >= nb) return;
+  if (i == 0) {  // block of the span start: entry known
+    entry[0] = E.p0;
+    const BlockInfo b = E.blocks[E.k0];
+    if (x[0] < b.ustart + b.isize) atomicAdd(fails, 1u);  // chain stops in the first block: serial path
+    return;
+  }
+  const BlockInfo b = E.blocks[E.k0 + i];
+  const uint64_t bend = b.ustart + b.isize;
+  const uint64_t in = in_scan[i];
+  const uint64_t gi = g[i];
+  bool bad = false;
+  uint64_t e = kNone;
+  if (in >= E.q_end) {
+    e = kNone;                       // beyond the span
+  } else if (in >= bend || b.isize == 0) {
+    e = kNone;                       // no record starts here: pass-through
+    bad = gi != kNone && x[i] > in;  // a stray guess would corrupt later in[]
+  } else if (in < b.ustart) {
+    bad = true;                      // a block before had records but no guess
+  } else {
+    e = in;
+    bad = gi != in;                  // guess disagrees with the entering chain
+  }
+  entry[i] = e;
+  if (bad) atomicAdd(fails, 1u);
 }
 
 // Count (and validate) the records of each block of the span under the
@@ -1108,10 +1156,24 @@ hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s) 
       if (mode == kReader) hipLaunchKernelGGL(k_rec_emit<kReader>, dim3(gb), dim3(tb), 0, s, E, a.entry, a.cnt, a.base, a.rec_pos, a.rec_voff);
       else hipLaunchKernelGGL(k_rec_emit<kIndexer>, dim3(gb), dim3(tb), 0, s, E, a.entry, a.cnt, a.base, a.rec_pos, a.rec_voff);
       break;
+    case 4: {  // parallel link: y, exclusive max-scan, check
+      hipLaunchKernelGGL(k_rec_link_y, dim3(gb), dim3(tb), 0, s, a.g, a.x, nb, a.x2);
+      size_t sb = a.scan_bytes;
+      hipError_t e = hipcub::DeviceScan::ExclusiveScan(a.scan_tmp, sb, a.x2, a.base, hipcub::Max(),
+                                                       (uint64_t)0, (int)nb, s);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(k_rec_link_check, dim3(gb), dim3(tb), 0, s, E, a.g, a.x, a.base, a.entry, a.changed);
+      break;
+    }
     default:
       return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+hipError_t link_scan_bytes(uint32_t nb, size_t* bytes) {
+  uint64_t* p = nullptr;
+  return hipcub::DeviceScan::ExclusiveScan(nullptr, *bytes, p, p, hipcub::Max(), (uint64_t)0, (int)nb, (hipStream_t)0);
 }
 
 hipError_t launch_rec_decode(const uint8_t* u, const uint64_t* rec_pos, uint64_t n, const Columns& col,

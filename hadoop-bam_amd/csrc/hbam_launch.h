@@ -17,6 +17,10 @@ struct ChainArgs {
   uint32_t k0, k1;
   // per-block scratch (indexed by k - k0)
   uint64_t *g, *x, *entry, *summary, *base;
+  uint64_t* x2;        // parallel link: y (guess exits)
+  uint32_t* changed;   // parallel link: violation count
+  void* scan_tmp;      // parallel link: hipcub temp storage
+  size_t scan_bytes;
   uint32_t* cnt;
   int32_t* err;
   unsigned long long* need;
@@ -42,8 +46,9 @@ hipError_t launch_inflate_huff(const uint8_t* file, const BlockInfo* blocks, uin
                                uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, hipStream_t s);
 hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb, uint64_t chunk_ustart,
                                const uint32_t* tokens, const HuffOut* hout, uint8_t* u, hipStream_t s);
-// stage: 0 guess, 1 link, 2 count, 3 emit
+// stage: 0 guess, 1 serial link, 2 count, 3 emit, 4 parallel link (base = in[] scratch)
 hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s);
+hipError_t link_scan_bytes(uint32_t nb, size_t* bytes);
 hipError_t launch_rec_decode(const uint8_t* u, const uint64_t* rec_pos, uint64_t n, const Columns& col,
                              hipStream_t s);
 hipError_t launch_first_error_hout(const HuffOut* hout, uint32_t b0, uint32_t nb, uint32_t* first, hipStream_t s);

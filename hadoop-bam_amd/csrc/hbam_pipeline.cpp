@@ -82,7 +82,8 @@ int Pipeline::locate() {
   // (or any chain break) take the serial walk, whose table bound is len/26.
   const uint32_t cap = (uint32_t)std::min<uint64_t>(flen_ / 1024 + 4096, 0x7fffffffu);
   const uint32_t walk_cap = (uint32_t)std::min<uint64_t>(flen_ / 26 + 16, 0x7fffffffu);
-  DevBuf<uint64_t> cand, sorted;
+  DevBuf<uint64_t>& cand = cand_;
+  DevBuf<uint64_t>& sorted = sorted_;
   HIPCHK(cand.reserve(cap));
   HIPCHK(flags_.reserve(4));
   uint32_t init[4] = {0, 0, 0xffffffffu, 0};
@@ -122,7 +123,8 @@ int Pipeline::locate() {
     }
   }
   HIPCHK(dblocks_.reserve(n + 1));
-  DevBuf<uint64_t> isz, ust;
+  DevBuf<uint64_t>& isz = isz_;
+  DevBuf<uint64_t>& ust = ust_;
   HIPCHK(isz.reserve(n + 1));
   HIPCHK(ust.reserve(n + 1));
   size_t sb = 0;
@@ -187,7 +189,10 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force) {
     any = true;
     b = e;
   }
-  if (!any) return kOk;
+  if (!any) {
+    times.inflate = times.huff = times.lz77 = 0;
+    return kOk;
+  }
   HIPCHK(flags_.reserve(4));
   const uint32_t none = 0xffffffffu;
   HIPCHK(hipMemcpyAsync(flags_.p + 3, &none, 4, hipMemcpyHostToDevice, stream_));
@@ -327,12 +332,39 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
     a.err = errv_.p;
     a.need = need_.p;
     HIPCHK(hipMemsetAsync(need_.p, 0, 8, stream_));
-    HIPCHK(launch_chain(a, mode, 0, stream_));
-    HIPCHK(launch_chain(a, mode, 1, stream_));
-    HIPCHK(launch_chain(a, mode, 2, stream_));
+    HIPCHK(launch_chain(a, mode, 0, stream_));  // per-block guesses
+    // link: parallel check of the guesses, exact serial link on any violation
+    HIPCHK(x2_.reserve(nb));
+    HIPCHK(base_arr_.reserve(nb + 1));
+    size_t lsb = 0;
+    HIPCHK(link_scan_bytes(nb, &lsb));
+    HIPCHK(scan_tmp_.reserve(lsb + 16));
+    HIPCHK(hipMemsetAsync(flags_.p + 2, 0, 4, stream_));
+    a.x2 = x2_.p;
+    a.base = base_arr_.p;
+    a.changed = flags_.p + 2;
+    a.scan_tmp = scan_tmp_.p;
+    a.scan_bytes = lsb;
+    HIPCHK(launch_chain(a, mode, 4, stream_));
+    uint32_t fails = 0;
+    HIPCHK(hipMemcpyAsync(&fails, flags_.p + 2, 4, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    link_fallbacks_ += fails ? 1 : 0;
+    if (fails) HIPCHK(launch_chain(a, mode, 1, stream_));  // exact serial link (writes entry)
     uint64_t sm[2] = {0, 0};
     unsigned long long need = 0;
-    HIPCHK(hipMemcpyAsync(sm, summary_.p, 16, hipMemcpyDeviceToHost, stream_));
+    if (fails) {
+      HIPCHK(hipMemcpyAsync(sm, summary_.p, 16, hipMemcpyDeviceToHost, stream_));
+    } else {  // final chain position = max of every guess exit; no stop
+      uint64_t t[2] = {0, 0};
+      HIPCHK(hipMemcpyAsync(&t[0], base_arr_.p + nb - 1, 8, hipMemcpyDeviceToHost, stream_));
+      HIPCHK(hipMemcpyAsync(&t[1], x2_.p + nb - 1, 8, hipMemcpyDeviceToHost, stream_));
+      HIPCHK(hipStreamSynchronize(stream_));
+      sm[0] = nb == 1 ? t[1] : std::max(t[0], t[1]);
+      sm[1] = 0;
+    }
+    HIPCHK(hipStreamSynchronize(stream_));
+    HIPCHK(launch_chain(a, mode, 2, stream_));  // count + validate
     HIPCHK(hipMemcpyAsync(&need, need_.p, 8, hipMemcpyDeviceToHost, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
     const uint64_t final_pos = sm[0];

@@ -100,6 +100,7 @@ class Pipeline {
   void set_n_ref(int32_t n) { n_ref_ = n; }
   int32_t n_ref() const { return n_ref_; }
 
+  uint64_t link_fallbacks() const { return link_fallbacks_; }
   StageTimes times;
   bool timing = false;  // record per-stage HIP event times
 
@@ -120,6 +121,7 @@ class Pipeline {
   uint64_t total_u_ = 0;
   uint32_t ndead_ = 0;
   int32_t n_ref_ = 0;
+  uint64_t link_fallbacks_ = 0;
 
   DevBuf<uint8_t> du_;
   std::vector<uint8_t> inflated_;  // per block flag
@@ -127,7 +129,8 @@ class Pipeline {
   DevBuf<HuffOut> hout_;
 
   // span scratch
-  DevBuf<uint64_t> g_, x_, entry_, base_arr_, summary_, dead_;
+  DevBuf<uint64_t> g_, x_, x2_, entry_, base_arr_, summary_, dead_;
+  DevBuf<uint64_t> cand_, sorted_, isz_, ust_;  // locate scratch
   DevBuf<uint32_t> cnt_, flags_;
   DevBuf<int32_t> errv_;
   DevBuf<unsigned long long> need_;

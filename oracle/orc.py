@@ -120,6 +120,10 @@ class Stream:
         return C.string_at(L.orc_data(self._h), n) if n else b""
 
     @property
+    def data_len(self):
+        return lib().orc_data_len(self._h)
+
+    @property
     def n_ref(self):
         return lib().orc_n_ref(self._h)
 

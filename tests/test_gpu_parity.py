@@ -167,9 +167,9 @@ def test_error_bad_deflate():
     s = orc.Stream(d)
     b1 = s.blocks[1]
     bad = _corrupt(d, int(b1["coff"]) + 18, 0xFF)  # first DEFLATE header byte: type 3 (invalid)
-    f = hbam.BamFile(bad)
-    with pytest.raises(hbam.HbamError) as e:
-        f.decode_all()
+    with pytest.raises(hbam.HbamError) as e:   # surfaces at open or at decode, as in htsjdk
+        with hbam.BamFile(bad) as f:
+            f.decode_all()
     with pytest.raises(orc.OracleError) as e2:
         orc.Stream(bad)
     assert e.value.code == e2.value.code == hbam.E_IO
