@@ -149,11 +149,21 @@ __global__ void k_block_ustart(BlockInfo* __restrict__ blocks, uint32_t n, const
 // ---------------------------------------------------------------------------
 // Inflate phase A: Huffman decode, one wavefront per BGZF block
 // ---------------------------------------------------------------------------
+// Table entries (u32):
+//   litlen  [15:0] payload  [20:16] bits to consume  [25:24] literal count  [28:26] kind
+//           kind 0 LIT : payload = 1 or 2 literal bytes; (e & 0x0300ffff) IS the token
+//           kind 1 LEN : payload [8:0] base (3..258), [12:9] extra bits
+//           kind 2 EOB, 3 LONG (code longer than the root: canonical slow path), 4 BAD
+//   dist    [14:0] base  [20:16] bits  [24:21] extra  [28:26] kind (0 ok, 3 LONG, 4 BAD)
+//   codes   [15:0] symbol [20:16] bits (code-length alphabet, root 7: always direct)
+// Tokens (u32): literal  bit31=0, [25:24] count (1..2), [15:0] bytes
+//               match    bit31=1, [30:16] dist-1, [15:0] length
 constexpr int kLitRoot = 10;
 constexpr int kDistRoot = 8;
 enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_LONG = 3, K_BAD = 4 };
-constexpr uint32_t kBadEntry = K_BAD << 8;
-constexpr uint32_t kLongEntry = K_LONG << 8;
+constexpr uint32_t kBadEntry = K_BAD << 26;
+constexpr uint32_t kLongEntry = K_LONG << 26;
+constexpr uint32_t kKindLit = 1u << 26;  // e < kKindLit  <=>  literal entry
 
 __constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
                                       31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -167,13 +177,15 @@ __constant__ uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2,  3,  3,  4,  4,  
 __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 struct HuffLds {
-  uint32_t lit[1 << kLitRoot];    // litlen fast table
+  uint32_t ring[512];             // 2 x 1 KiB compressed-input ring (LDS-DMA target, 16 B aligned)
+  uint32_t lit[1 << kLitRoot];    // litlen fast table (with literal pairs)
   uint32_t dist[1 << kDistRoot];  // distance fast table (also the code-length table)
-  uint32_t ring[512];             // 2 x 1 KiB compressed-input ring
   uint32_t cnt_lit[16];
   uint32_t cnt_dist[16];
   uint32_t offs[16];
   uint32_t firstc[16];
+  uint32_t base[16];
+  uint32_t bt_status;
   uint16_t sort_lit[288];
   uint16_t sort_dist[32];
   uint8_t lens[320];
@@ -183,84 +195,84 @@ struct HuffLds {
 // mode 0 litlen, 1 distance, 2 code-length codes
 __device__ __forceinline__ uint32_t make_entry(int mode, uint32_t s, uint32_t len) {
   if (mode == 0) {
-    if (s < 256) return len | (K_LIT << 8) | (s << 16);
-    if (s == 256) return len | (K_EOB << 8);
+    if (s < 256) return (len << 16) | (1u << 24) | s;
+    if (s == 256) return (len << 16) | (K_EOB << 26);
     if (s < 286) {
-      uint32_t i = s - 257;
-      return len | ((uint32_t)kLenExtra[i] << 4) | (K_LEN << 8) | ((uint32_t)kLenBase[i] << 16);
+      const uint32_t i = s - 257;
+      return (len << 16) | (K_LEN << 26) | ((uint32_t)kLenExtra[i] << 9) | (uint32_t)kLenBase[i];
     }
-    return len | kBadEntry;
+    return (len << 16) | kBadEntry;
   }
   if (mode == 1) {
-    if (s < 30) return len | ((uint32_t)kDistExtra[s] << 4) | (K_LIT << 8) | ((uint32_t)kDistBase[s] << 16);
-    return len | kBadEntry;
+    if (s < 30) return (len << 16) | ((uint32_t)kDistExtra[s] << 21) | (uint32_t)kDistBase[s];
+    return (len << 16) | kBadEntry;
   }
-  return len | (K_LIT << 8) | (s << 16);
+  return (len << 16) | s;
 }
 
 // Canonical Huffman table build, all 64 lanes of the wave.  Validity follows
 // zlib inflate_table: over-subscribed -> error; incomplete -> error unless
 // the only code has length 1 (LENS/DISTS); no codes -> all-invalid table
-// (DISTS) or error (CODES).  Returns 0 on success.
-__device__ int build_table(HuffLds& L, const uint8_t* lens, int nsym, int root, int mode, uint32_t* tab,
-                           uint32_t* cnt, uint16_t* sorted) {
+// (DISTS) or error (CODES).  Returns 0 on success.  Per-length state lives in
+// LDS (not in unrolled SGPR arrays) to keep the decode loop's registers free.
+// Callers must rfl() the result: a call's return value is divergent to the
+// compiler, and one divergent branch here turns the whole decode state into
+// VGPRs with exec-masked control flow (measured: ~5x the instructions).
+__device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* lens, int nsym, int root, int mode,
+                                                     uint32_t* tab, uint32_t* cnt, uint16_t* sorted) {
   const uint32_t lane = lane_id();
-  if (lane < 16) cnt[lane] = 0;
+  if (lane < 16) {
+    cnt[lane] = 0;
+    L.base[lane] = 0;
+  }
   __syncthreads();
   for (int s = lane; s < nsym; s += 64) {
-    uint32_t l = lens[s];
+    const uint32_t l = lens[s];
     if (l) atomicAdd(&cnt[l], 1u);
   }
   __syncthreads();
-  int left = 1, maxl = 0, over = 0;
-  uint32_t c[16];
-  c[0] = 0;
-#pragma unroll
-  for (int l = 1; l < 16; ++l) {
-    c[l] = rfl(cnt[l]);
-    left <<= 1;
-    left -= (int)c[l];
-    if (c[l]) maxl = l;
-    if (left < 0) over = 1;
+  if (lane == 0) {
+    int left = 1, maxl = 0, over = 0;
+    uint32_t o = 0, code = 0, prev = 0;
+    for (int l = 1; l < 16; ++l) {
+      const uint32_t c = cnt[l];
+      left = (left << 1) - (int)c;
+      if (c) maxl = l;
+      if (left < 0) over = 1;
+      L.offs[l] = o;
+      o += c;
+      code = (code + prev) << 1;
+      L.firstc[l] = code;
+      prev = c;
+    }
+    uint32_t st = 0;
+    if (over) st = 1;
+    else if (maxl == 0) st = mode == 2 ? 1 : 2;
+    else if (left > 0 && (mode == 2 || maxl != 1)) st = 1;
+    L.bt_status = st;
   }
   for (int i = lane; i < (1 << root); i += 64) tab[i] = kBadEntry;
-  if (over) return 1;
-  if (maxl == 0) {
-    __syncthreads();
-    return mode == 2 ? 1 : 0;
-  }
-  if (left > 0 && (mode == 2 || maxl != 1)) return 1;
-  if (lane == 0) {
-    uint32_t o = 0, code = 0;
-#pragma unroll
-    for (int l = 1; l < 16; ++l) {
-      L.offs[l] = o;
-      o += c[l];
-      code = (code + c[l - 1]) << 1;
-      L.firstc[l] = code;
-    }
-  }
   __syncthreads();
-  uint32_t base[16];
-#pragma unroll
-  for (int l = 0; l < 16; ++l) base[l] = 0;
+  const uint32_t st = rfl(L.bt_status);
+  if (st == 1) return 1;
+  if (st == 2) return 0;  // no codes: all-invalid table
   const uint64_t ltmask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int c0 = 0; c0 < nsym; c0 += 64) {
-    int s = c0 + (int)lane;
-    uint32_t l = s < nsym ? lens[s] : 0;
+    const int s = c0 + (int)lane;
+    const uint32_t l = s < nsym ? lens[s] : 0;
     uint32_t rank = 0;
-#pragma unroll
-    for (int q = 1; q < 16; ++q) {
-      uint64_t m = __ballot(l == (uint32_t)q);
-      if (l == (uint32_t)q) rank = base[q] + (uint32_t)__popcll(m & ltmask);
-      base[q] += (uint32_t)__popcll(m);
+    for (uint32_t q = 1; q < 16; ++q) {
+      const uint64_t m = __ballot(l == q);
+      if (m == 0) continue;
+      if (l == q) rank = L.base[q] + (uint32_t)__popcll(m & ltmask);
+      if (lane == 0) L.base[q] += (uint32_t)__popcll(m);
     }
     if (l) {
       sorted[L.offs[l] + rank] = (uint16_t)s;
-      uint32_t code = L.firstc[l] + rank;
-      uint32_t rev = __brev(code) >> (32 - l);
+      const uint32_t code = L.firstc[l] + rank;
+      const uint32_t rev = __brev(code) >> (32 - l);
       if ((int)l <= root) {
-        uint32_t e = make_entry(mode, (uint32_t)s, l);
+        const uint32_t e = make_entry(mode, (uint32_t)s, l);
         for (uint32_t i = rev; i < (1u << root); i += (1u << l)) tab[i] = e;
       } else {
         tab[rev & ((1u << root) - 1)] = kLongEntry;
@@ -269,6 +281,30 @@ __device__ int build_table(HuffLds& L, const uint8_t* lens, int nsym, int root, 
   }
   __syncthreads();
   return 0;
+}
+
+// Fold two consecutive literals into one litlen entry when both codes fit in
+// the 10-bit index (the common case for quality/sequence bytes).
+__device__ __attribute__((noinline)) void pair_literals(HuffLds& L) {
+  const uint32_t lane = lane_id();
+  uint32_t v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t i = lane + 64u * j;
+    const uint32_t e1 = L.lit[i];
+    v[j] = e1;
+    const uint32_t l1 = (e1 >> 16) & 31;
+    if (e1 < kKindLit && l1 < (uint32_t)kLitRoot) {
+      const uint32_t e2 = L.lit[i >> l1];
+      const uint32_t l2 = (e2 >> 16) & 31;
+      if (e2 < kKindLit && l2 + l1 <= (uint32_t)kLitRoot)
+        v[j] = ((l1 + l2) << 16) | (2u << 24) | (e1 & 0xffu) | ((e2 & 0xffu) << 8);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16; ++j) L.lit[lane + 64u * j] = v[j];
+  __syncthreads();
 }
 
 // puff-style canonical decode for codes longer than the table root (rare).
@@ -290,27 +326,18 @@ __device__ uint32_t slow_decode(uint64_t bits, const uint32_t* cnt, const uint16
   return kBadEntry;
 }
 
-struct BitState {
-  uint64_t buf;
-  uint32_t cnt;
-  uint32_t rd;     // next dword (relative to the 16-aligned chunk base) to pull
-  uint32_t chunk;  // chunk index currently being read (rd / 256)
-};
-
-// Wave-cooperative ring maintenance: chunk c of the block's compressed data is
-// the 1 KiB at abase + 1024 c; ring half (c & 1) holds it.
-__device__ __forceinline__ void ring_store(HuffLds& L, uint32_t half, uint4 v) {
-  reinterpret_cast<uint4*>(L.ring)[half * 64 + lane_id()] = v;
-}
-__device__ __forceinline__ uint4 ring_load(const uint8_t* file, uint64_t abase, uint32_t c) {
-  return *reinterpret_cast<const uint4*>(file + abase + 1024ull * c + 16ull * lane_id());
+// LDS-DMA one 1 KiB chunk of compressed input into ring half (c & 1).
+__device__ __forceinline__ void ring_dma(HuffLds& L, const uint8_t* file, uint64_t abase, uint32_t c) {
+  __builtin_amdgcn_global_load_lds(
+      (const __attribute__((address_space(1))) void*)(file + abase + 1024ull * c + 16ull * lane_id()),
+      (__attribute__((address_space(3))) void*)(L.ring + 256u * (c & 1u)), 16, 0, 0);
 }
 
 __global__ __launch_bounds__(64) void k_inflate_huff(const uint8_t* __restrict__ file,
                                                      const BlockInfo* __restrict__ blocks, uint32_t b0,
                                                      uint64_t chunk_ustart, uint32_t* __restrict__ tokens,
                                                      HuffOut* __restrict__ hout) {
-  __shared__ HuffLds L;
+  __shared__ __attribute__((aligned(16))) HuffLds L;
   const uint32_t bi = b0 + blockIdx.x;
   const uint32_t lane = lane_id();
   const BlockInfo blk = blocks[bi];
@@ -326,92 +353,75 @@ __global__ __launch_bounds__(64) void k_inflate_huff(const uint8_t* __restrict__
   const uint32_t lead = (uint32_t)(sbyte - abase);  // junk bytes before cdata
   const uint64_t end_bits = 8ull * (lead + clen);
 
-  // prime the ring: chunks 0, 1 resident; chunk 2 in flight
-  ring_store(L, 0, ring_load(file, abase, 0));
-  ring_store(L, 1, ring_load(file, abase, 1));
-  uint4 pf = ring_load(file, abase, 2);
+  // prime the ring: chunks 0 and 1 resident
+  ring_dma(L, file, abase, 0);
+  ring_dma(L, file, abase, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  BitState bs;
-  bs.buf = 0;
-  bs.cnt = 0;
-  bs.rd = lead >> 2;
-  bs.chunk = 0;
+  uint64_t buf = 0;
+  uint32_t cnt = 0;
+  uint32_t rd = lead >> 2;  // ring dword index of `nextw` (relative to abase/4)
   int err = kOk;
+  const uint32_t end_bits32 = (uint32_t)end_bits;  // < 2^20: 32-bit, scalar compares
+  uint32_t nextw = L.ring[rd & 511];  // prefetched next input dword (VGPR; read at use)
 
-#define REFILL()                                                         \
-  do {                                                                   \
-    while (bs.cnt <= 32) {                                               \
-      uint32_t w = rfl(L.ring[bs.rd & 511]);                             \
-      bs.buf |= (uint64_t)w << bs.cnt;                                   \
-      bs.cnt += 32;                                                      \
-      bs.rd++;                                                           \
-      if ((bs.rd & 255) == 0) {                                          \
-        /* entered chunk c = rd/256: half (c+1)&1 is free for c+1 */     \
-        uint32_t c = bs.rd >> 8;                                         \
-        ring_store(L, (c + 1) & 1, pf);                                  \
-        pf = ring_load(file, abase, c + 2);                              \
-        bs.chunk = c;                                                    \
-        if (32ull * bs.rd - bs.cnt > end_bits + 64) { err = kErrFormat; } \
-      }                                                                  \
-    }                                                                    \
+  // one 32-bit refill from the prefetched dword, then prefetch the next one.
+  // Entering chunk c (rd % 256 == 0): chunk c was DMA'd one chunk ago ->
+  // wait for it, then DMA chunk c+1 into the half chunk c-1 just freed.
+#define REFILL1()                                                       \
+  do {                                                                  \
+    buf |= (uint64_t)rfl(nextw) << cnt;                                 \
+    cnt += 32;                                                          \
+    ++rd;                                                               \
+    if ((rd & 255) == 0) {                                              \
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                  \
+      ring_dma(L, file, abase, (rd >> 8) + 1);                          \
+      if (32u * rd - cnt > end_bits32 + 64u) err = kErrFormat;          \
+    }                                                                   \
+    nextw = L.ring[rd & 511];                                           \
   } while (0)
-#define CONSUME(n)   \
-  do {               \
-    bs.buf >>= (n);  \
-    bs.cnt -= (n);   \
+#define ENSURE()              \
+  do {                        \
+    if (cnt <= 32) REFILL1(); \
+  } while (0)
+#define CONSUME(n) \
+  do {             \
+    buf >>= (n);   \
+    cnt -= (n);    \
   } while (0)
 
-  REFILL();
+  REFILL1();
+  REFILL1();
   CONSUME(8 * (lead & 3));
 
-  uint32_t outpos = 0, ntok = 0, tokv = 0, lacc = 0, lnum = 0;
-
-#define EMIT(t)                                                                       \
-  do {                                                                                \
-    tokv = (lane == (ntok & 63)) ? (uint32_t)(t) : tokv;                            \
-    if ((ntok & 63) == 63) tok_out[(ntok & ~63u) + lane] = tokv;                      \
-    ntok++;                                                                           \
-  } while (0)
-#define FLUSH_LITS()                        \
-  do {                                      \
-    if (lnum) {                             \
-      EMIT(lacc | (lnum << 24));            \
-      lacc = 0;                             \
-      lnum = 0;                             \
-    }                                       \
-  } while (0)
-#define LITERAL(b)                         \
-  do {                                     \
-    lacc |= (uint32_t)(b) << (8 * lnum);   \
-    lnum++;                                \
-    outpos++;                              \
-    if (lnum == 3) {                       \
-      EMIT(lacc | (3u << 24));             \
-      lacc = 0;                            \
-      lnum = 0;                            \
-    }                                      \
+  uint32_t outpos = 0, ntok = 0, tokv = 0;
+#define EMIT(t)                                                   \
+  do {                                                            \
+    tokv = (lane == (ntok & 63)) ? (uint32_t)(t) : tokv;          \
+    if ((ntok & 63) == 63) tok_out[(ntok & ~63u) + lane] = tokv;  \
+    ntok++;                                                       \
   } while (0)
 
   uint32_t final_blk = 0;
   while (!final_blk && outpos < isize && err == kOk) {
-    REFILL();
-    uint32_t hdr = (uint32_t)bs.buf & 7;
+    ENSURE();
+    const uint32_t hdr = (uint32_t)buf & 7;
     CONSUME(3);
     final_blk = hdr & 1;
-    uint32_t type = hdr >> 1;
+    const uint32_t type = hdr >> 1;
     if (type == 0) {  // stored
-      uint32_t drop = bs.cnt & 7;
-      CONSUME(drop);
-      REFILL();
-      uint32_t len = (uint32_t)bs.buf & 0xffff, nlen = (uint32_t)(bs.buf >> 16) & 0xffff;
+      CONSUME(cnt & 7);
+      ENSURE();
+      if (cnt < 32) REFILL1();
+      const uint32_t len = (uint32_t)buf & 0xffff, nlen = (uint32_t)(buf >> 16) & 0xffff;
       CONSUME(32);
       if (len != (~nlen & 0xffffu)) { err = kErrIO; break; }
       for (uint32_t j = 0; j < len && outpos < isize && err == kOk; ++j) {
-        REFILL();
-        uint32_t b = (uint32_t)bs.buf & 255;
+        ENSURE();
+        EMIT((1u << 24) | ((uint32_t)buf & 255));
         CONSUME(8);
-        LITERAL(b);
+        outpos++;
       }
       continue;
     } else if (type == 1) {  // fixed Huffman
@@ -421,51 +431,53 @@ __global__ __launch_bounds__(64) void k_inflate_huff(const uint8_t* __restrict__
         L.lens[s] = l;
       }
       __syncthreads();
-      if (build_table(L, L.lens, 288, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit) ||
-          build_table(L, L.lens + 288, 32, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist)) {
+      if (rfl(build_table(L, L.lens, 288, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit)) ||
+          rfl(build_table(L, L.lens + 288, 32, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist))) {
         err = kErrIO;
         break;
       }
+      pair_literals(L);
     } else if (type == 2) {  // dynamic Huffman
-      REFILL();
-      uint32_t hlit = ((uint32_t)bs.buf & 31) + 257;
-      uint32_t hdist = ((uint32_t)(bs.buf >> 5) & 31) + 1;
-      uint32_t hclen = ((uint32_t)(bs.buf >> 10) & 15) + 4;
+      ENSURE();
+      const uint32_t hlit = ((uint32_t)buf & 31) + 257;
+      const uint32_t hdist = ((uint32_t)(buf >> 5) & 31) + 1;
+      const uint32_t hclen = ((uint32_t)(buf >> 10) & 15) + 4;
       CONSUME(14);
       if (hlit > 286 || hdist > 30) { err = kErrIO; break; }
       if (lane < 20) L.cl_lens[lane] = 0;
       __syncthreads();
       for (uint32_t i = 0; i < hclen; ++i) {
-        REFILL();
-        uint32_t v = (uint32_t)bs.buf & 7;
+        ENSURE();
+        const uint32_t v = (uint32_t)buf & 7;
         CONSUME(3);
         if (lane == 0) L.cl_lens[kClOrder[i]] = (uint8_t)v;
       }
       __syncthreads();
-      if (build_table(L, L.cl_lens, 19, 7, 2, L.dist, L.cnt_dist, L.sort_dist)) { err = kErrIO; break; }
+      if (rfl(build_table(L, L.cl_lens, 19, 7, 2, L.dist, L.cnt_dist, L.sort_dist))) { err = kErrIO; break; }
       const uint32_t ntot = hlit + hdist;
       uint32_t i = 0, last = 0;
       while (i < ntot) {
-        REFILL();
+        ENSURE();
         if (err != kOk) break;
-        uint32_t e = rfl(L.dist[(uint32_t)bs.buf & 127]);
-        if (((e >> 8) & 7) == K_BAD) { err = kErrIO; break; }
-        CONSUME(e & 15);
-        uint32_t sym = e >> 16, rep, val;
+        const uint32_t e = rfl(L.dist[(uint32_t)buf & 127]);
+        if (e >= kKindLit) { err = kErrIO; break; }
+        CONSUME((e >> 16) & 31);
+        const uint32_t sym = e & 0xffff;
+        uint32_t rep, val;
         if (sym < 16) {
           rep = 1;
           val = sym;
         } else if (sym == 16) {
           if (i == 0) { err = kErrIO; break; }
-          rep = 3 + ((uint32_t)bs.buf & 3);
+          rep = 3 + ((uint32_t)buf & 3);
           CONSUME(2);
           val = last;
         } else if (sym == 17) {
-          rep = 3 + ((uint32_t)bs.buf & 7);
+          rep = 3 + ((uint32_t)buf & 7);
           CONSUME(3);
           val = 0;
         } else {
-          rep = 11 + ((uint32_t)bs.buf & 127);
+          rep = 11 + ((uint32_t)buf & 127);
           CONSUME(7);
           val = 0;
         }
@@ -477,70 +489,85 @@ __global__ __launch_bounds__(64) void k_inflate_huff(const uint8_t* __restrict__
       if (err != kOk) break;
       __syncthreads();
       if (rfl(L.lens[256]) == 0) { err = kErrIO; break; }
-      if (build_table(L, L.lens, (int)hlit, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit) ||
-          build_table(L, L.lens + hlit, (int)hdist, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist)) {
+      if (rfl(build_table(L, L.lens, (int)hlit, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit)) ||
+          rfl(build_table(L, L.lens + hlit, (int)hdist, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist))) {
         err = kErrIO;
         break;
       }
+      pair_literals(L);
     } else {
       err = kErrIO;  // invalid block type
       break;
     }
 
-    // ---- symbol loop ----
-    while (outpos < isize) {
-      REFILL();
-      if (err != kOk) break;
-      uint32_t e = rfl(L.lit[(uint32_t)bs.buf & ((1u << kLitRoot) - 1)]);
-      uint32_t kind = (e >> 8) & 7;
-      if (kind == K_LONG) {
-        e = slow_decode(bs.buf, L.cnt_lit, L.sort_lit, 0);
-        kind = (e >> 8) & 7;
+    // ---- symbol loop: bits >= 33 after ENSURE; a literal pair takes <= 10,
+    //      a length <= 20, a distance <= 28 (ENSURE in between).  Literals run
+    //      in an inner loop with a single back-edge (no loop-carried copies).
+    if (outpos < isize && err == kOk) {
+      ENSURE();
+      uint32_t e = rfl(L.lit[(uint32_t)buf & ((1u << kLitRoot) - 1)]);
+      for (;;) {
+        while (e < kKindLit) {  // one or two literals: the entry is the token
+          CONSUME((e >> 16) & 31);
+          EMIT(e & 0x0300ffffu);
+          outpos += e >> 24;
+          if (outpos >= isize) goto block_done;
+          ENSURE();
+          e = rfl(L.lit[(uint32_t)buf & ((1u << kLitRoot) - 1)]);
+        }
+        if (err != kOk) goto block_done;
+        uint32_t kind = e >> 26;
+        if (kind == K_LONG) {
+          e = slow_decode(buf, L.cnt_lit, L.sort_lit, 0);
+          kind = e >> 26;
+          if (kind == K_LIT) continue;  // re-enters the literal loop with the decoded entry
+        }
+        if (kind == K_LEN) {
+          CONSUME((e >> 16) & 31);
+          const uint32_t ex = (e >> 9) & 15;
+          const uint32_t len = (e & 511) + ((uint32_t)buf & ((1u << ex) - 1));
+          CONSUME(ex);
+          ENSURE();
+          uint32_t d = rfl(L.dist[(uint32_t)buf & ((1u << kDistRoot) - 1)]);
+          if ((d >> 26) == K_LONG) d = slow_decode(buf, L.cnt_dist, L.sort_dist, 1);
+          if (d >= kKindLit) { err = kErrIO; goto block_done; }  // invalid distance code
+          CONSUME((d >> 16) & 31);
+          const uint32_t dx = (d >> 21) & 15;
+          const uint32_t dist = (d & 0x7fff) + ((uint32_t)buf & ((1u << dx) - 1));
+          CONSUME(dx);
+          if (dist > outpos) { err = kErrIO; goto block_done; }  // invalid distance too far back
+          EMIT(0x80000000u | ((dist - 1) << 16) | len);
+          outpos += len;
+          if (outpos >= isize) goto block_done;
+          ENSURE();
+          e = rfl(L.lit[(uint32_t)buf & ((1u << kLitRoot) - 1)]);
+          continue;
+        }
+        if (kind == K_EOB) {
+          CONSUME((e >> 16) & 31);
+          break;
+        }
+        err = kErrIO;  // invalid literal/length code
+        break;
       }
-      CONSUME(e & 15);
-      if (kind == K_LIT) {
-        LITERAL(e >> 16);
-        continue;
-      }
-      if (kind == K_LEN) {
-        uint32_t ex = (e >> 4) & 15;
-        uint32_t len = (e >> 16) + ((uint32_t)bs.buf & ((1u << ex) - 1));
-        CONSUME(ex);
-        REFILL();
-        uint32_t d = rfl(L.dist[(uint32_t)bs.buf & ((1u << kDistRoot) - 1)]);
-        if (((d >> 8) & 7) == K_LONG) d = slow_decode(bs.buf, L.cnt_dist, L.sort_dist, 1);
-        if (((d >> 8) & 7) != K_LIT) { err = kErrIO; break; }
-        CONSUME(d & 15);
-        uint32_t dx = (d >> 4) & 15;
-        uint32_t dist = (d >> 16) + ((uint32_t)bs.buf & ((1u << dx) - 1));
-        CONSUME(dx);
-        if (dist > outpos) { err = kErrIO; break; }  // invalid distance too far back
-        FLUSH_LITS();
-        EMIT(0x80000000u | ((dist - 1) << 16) | len);
-        outpos += len;
-        continue;
-      }
-      if (kind == K_EOB) break;
-      err = kErrIO;  // invalid literal/length code
-      break;
     }
-    if (32ull * bs.rd - bs.cnt > end_bits) err = kErrFormat;  // ran past the input
+  block_done:
+    if (32u * rd - cnt > end_bits32) err = kErrFormat;  // ran past the input
   }
-  FLUSH_LITS();
   if (ntok & 63) {
     if (lane < (ntok & 63)) tok_out[(ntok & ~63u) + lane] = tokv;
   }
   if (err == kOk && outpos < isize) err = kErrFormat;  // "Did not inflate expected amount"
-  if (err == kOk && 32ull * bs.rd - bs.cnt > end_bits) err = kErrFormat;
+  if (err == kOk && 32u * rd - cnt > end_bits32) err = kErrFormat;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA in flight at exit
   if (lane == 0) {
     hout[bi].ntok = ntok;
     hout[bi].status = err;
   }
-#undef REFILL
+#undef REFILL1
+#undef ENSURE
 #undef CONSUME
 #undef EMIT
-#undef FLUSH_LITS
-#undef LITERAL
 }
 
 // ---------------------------------------------------------------------------
