@@ -571,9 +571,22 @@ __global__ __launch_bounds__(64) void k_inflate_huff(const uint8_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-// Inflate phase B: tokens -> bytes, one 256-thread workgroup per BGZF block
+// Inflate phase B: tokens -> bytes, one 1024-thread workgroup per BGZF block
 // ---------------------------------------------------------------------------
-constexpr int kLzThreads = 256;
+// Every output position p gets a u16 entry in an LDS map: 0xFF00|byte for a
+// literal, else the position its byte is copied from (p - dist, strictly
+// smaller; for an overlapping match this is the periodic extension, so every
+// match is expanded in one parallel step).  Bytes are then resolved by
+// following entries back to a literal and writing the result in place (path
+// compression); positions are visited in increasing order so chains are
+// short (measured on BAM data: mean depth 7.5, max ~40 without compression).
+// The map needs ISIZE <= 65280 (positions below the 0xFF00 tag space: the
+// BGZF maximum htsjdk/bgzip write); larger blocks take the dependency-round
+// path over a byte image in the same LDS.
+constexpr int kLzThreads = 1024;
+constexpr int kLzWaves = kLzThreads / 64;
+constexpr uint32_t kMapMax = 65280;
+constexpr uint32_t kLitTag = 0xFF00u;
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const uint32_t lane = lane_id();
@@ -588,12 +601,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 // exclusive scan over the workgroup; returns the prefix, *total = sum
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
   const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
-  uint32_t inc = wave_incl_scan(v);
+  const uint32_t inc = wave_incl_scan(v);
   if (lane == 63) scratch[wid] = inc;
   __syncthreads();
-  uint32_t w0 = scratch[0], w1 = scratch[1], w2 = scratch[2], w3 = scratch[3];
-  uint32_t off = (wid > 0 ? w0 : 0) + (wid > 1 ? w1 : 0) + (wid > 2 ? w2 : 0);
-  *total = w0 + w1 + w2 + w3;
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kLzWaves; ++w) {
+    const uint32_t x = scratch[w];
+    off += (uint32_t)w < wid ? x : 0u;
+    tot += x;
+  }
+  *total = tot;
   __syncthreads();
   return off + inc - v;
 }
@@ -604,31 +622,24 @@ __device__ __forceinline__ uint32_t block_min(uint32_t v, uint32_t* scratch) {
   for (int d = 32; d > 0; d >>= 1) v = min(v, (uint32_t)__shfl_xor(v, d, 64));
   if (lane == 0) scratch[wid] = v;
   __syncthreads();
-  uint32_t r = min(min(scratch[0], scratch[1]), min(scratch[2], scratch[3]));
+  uint32_t r = 0xffffffffu;
+#pragma unroll
+  for (int w = 0; w < kLzWaves; ++w) r = min(r, scratch[w]);
   __syncthreads();
   return r;
 }
 
-__global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __restrict__ blocks, uint32_t b0,
-                                                             uint64_t chunk_ustart,
-                                                             const uint32_t* __restrict__ tokens,
-                                                             const HuffOut* __restrict__ hout,
-                                                             uint8_t* __restrict__ u) {
-  __shared__ __attribute__((aligned(16))) uint8_t out[kMaxIsize + 16];
-  __shared__ uint32_t scratch[8];
-  const BlockInfo blk = blocks[b0 + blockIdx.x];
-  const HuffOut ho = hout[b0 + blockIdx.x];
-  if (ho.status != kOk || blk.isize == 0) return;
-  const uint32_t isize = blk.isize;
-  const uint32_t o0 = (uint32_t)(blk.ustart & 15);
-  const uint32_t* tk = tokens + (blk.ustart - chunk_ustart);
-  const uint32_t ntok = ho.ntok;
+__device__ __forceinline__ uint32_t tok_len(uint32_t t) { return (t >> 31) ? (t & 0xffffu) : ((t >> 24) & 3u); }
+
+// Rare path (ISIZE > 65280): byte image, matches resolve in dependency rounds.
+__device__ void lz77_rounds(uint8_t* out, uint32_t* scratch, const uint32_t* tk, uint32_t ntok, uint32_t isize,
+                            uint32_t o0) {
   uint32_t P = 0;
   for (uint32_t c = 0; c < ntok; c += kLzThreads) {
     const uint32_t i = c + threadIdx.x;
     const uint32_t t = i < ntok ? tk[i] : 0u;
     const bool ismatch = (t >> 31) != 0;
-    const uint32_t len = ismatch ? (t & 0xffffu) : ((t >> 24) & 3u);
+    const uint32_t len = i < ntok ? tok_len(t) : 0u;
     uint32_t total;
     const uint32_t pos = P + block_excl_scan(len, scratch, &total);
     P += total;
@@ -640,33 +651,106 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
     bool pending = ismatch && pos < isize;
     __syncthreads();
     for (;;) {
-      uint32_t first = block_min(pending ? pos : 0xffffffffu, scratch);
+      const uint32_t first = block_min(pending ? pos : 0xffffffffu, scratch);
       if (first == 0xffffffffu) break;
-      if (pending) {
-        uint32_t need_end = pos - dist + min(len, dist);
-        if (pos == first || need_end <= first) {
-          uint32_t n = min(len, isize - pos);
-          uint8_t* dst = out + o0 + pos;
-          for (uint32_t k = 0; k < n; ++k) dst[k] = dst[(int)k - (int)dist];
-          pending = false;
-        }
+      if (pending && (pos == first || pos - dist + min(len, dist) <= first)) {
+        const uint32_t n = min(len, isize - pos);
+        uint8_t* dst = out + o0 + pos;
+        for (uint32_t k = 0; k < n; ++k) dst[k] = dst[(int)k - (int)dist];
+        pending = false;
       }
       __syncthreads();
     }
   }
   __syncthreads();
-  // write back: 16 B aligned segments of global memory
+}
+
+__global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __restrict__ blocks, uint32_t b0,
+                                                             uint64_t chunk_ustart,
+                                                             const uint32_t* __restrict__ tokens,
+                                                             const HuffOut* __restrict__ hout,
+                                                             uint8_t* __restrict__ u) {
+  // map index = o0 + position, so 16-byte output segments read 32 B-aligned LDS
+  __shared__ __attribute__((aligned(16))) uint16_t map[kMapMax + 32];
+  __shared__ uint32_t scratch[kLzWaves];
+  const BlockInfo blk = blocks[b0 + blockIdx.x];
+  const HuffOut ho = hout[b0 + blockIdx.x];
+  if (ho.status != kOk || blk.isize == 0) return;
+  const uint32_t isize = blk.isize;
+  const uint32_t o0 = (uint32_t)(blk.ustart & 15);
+  const uint32_t* tk = tokens + (blk.ustart - chunk_ustart);
+  const uint32_t ntok = ho.ntok;
+  const uint32_t tid = threadIdx.x;
   const uint64_t g0 = blk.ustart & ~15ull;
   const uint64_t gend = blk.ustart + isize;
   const uint32_t nseg = (uint32_t)((gend - g0 + 15) >> 4);
-  for (uint32_t s = threadIdx.x; s < nseg; s += kLzThreads) {
+
+  if (isize > kMapMax) {  // uniform per workgroup
+    uint8_t* img = reinterpret_cast<uint8_t*>(map);
+    lz77_rounds(img, scratch, tk, ntok, isize, o0);
+    for (uint32_t s = tid; s < nseg; s += kLzThreads) {
+      const uint64_t ga = g0 + 16ull * s;
+      if (ga >= blk.ustart && ga + 16 <= gend) {
+        *reinterpret_cast<uint4*>(u + ga) = *reinterpret_cast<const uint4*>(img + 16 * s);
+      } else {
+        for (int j = 0; j < 16; ++j) {
+          const uint64_t g = ga + j;
+          if (g >= blk.ustart && g < gend) u[g] = img[16 * s + j];
+        }
+      }
+    }
+    return;
+  }
+
+  // 1. contiguous token range per thread; output position by block scan
+  const uint32_t K = (ntok + kLzThreads - 1) / kLzThreads;
+  const uint32_t t0 = min(tid * K, ntok), t1 = min(t0 + K, ntok);
+  uint32_t nbytes = 0;
+  for (uint32_t i = t0; i < t1; ++i) nbytes += tok_len(tk[i]);
+  uint32_t total;
+  uint32_t p = block_excl_scan(nbytes, scratch, &total);
+
+  // 2. expand tokens into the map (the last token may run past ISIZE: clamp)
+  uint16_t* m = map + o0;
+  for (uint32_t i = t0; i < t1 && p < isize; ++i) {
+    const uint32_t t = tk[i];
+    if (t >> 31) {
+      const uint32_t n = min(t & 0xffffu, isize - p);
+      const uint32_t src = p - (((t >> 16) & 0x7fffu) + 1);  // dist <= p: checked in phase A
+      for (uint32_t j = 0; j < n; ++j) m[p + j] = (uint16_t)(src + j);
+      p += n;
+    } else {
+      m[p] = (uint16_t)(kLitTag | (t & 0xffu));
+      if (((t >> 24) & 3u) == 2u && p + 1 < isize) m[p + 1] = (uint16_t)(kLitTag | ((t >> 8) & 0xffu));
+      p += (t >> 24) & 3u;
+    }
+  }
+  __syncthreads();
+
+  // 3. resolve, increasing positions first; results written back in place
+  for (uint32_t q = tid; q < isize; q += kLzThreads) {
+    uint32_t v = m[q];
+    while (v < kLitTag) v = m[v];
+    m[q] = (uint16_t)v;
+  }
+  __syncthreads();
+
+  // 4. 16 B stores; low bytes of 16 entries packed with v_perm
+  for (uint32_t s = tid; s < nseg; s += kLzThreads) {
     const uint64_t ga = g0 + 16ull * s;
     if (ga >= blk.ustart && ga + 16 <= gend) {
-      *reinterpret_cast<uint4*>(u + ga) = *reinterpret_cast<const uint4*>(out + 16 * s);
+      const uint4 e0 = *reinterpret_cast<const uint4*>(map + 16 * s);
+      const uint4 e1 = *reinterpret_cast<const uint4*>(map + 16 * s + 8);
+      uint4 o;
+      o.x = __builtin_amdgcn_perm(e0.y, e0.x, 0x06040200u);
+      o.y = __builtin_amdgcn_perm(e0.w, e0.z, 0x06040200u);
+      o.z = __builtin_amdgcn_perm(e1.y, e1.x, 0x06040200u);
+      o.w = __builtin_amdgcn_perm(e1.w, e1.z, 0x06040200u);
+      *reinterpret_cast<uint4*>(u + ga) = o;
     } else {
       for (int j = 0; j < 16; ++j) {
-        uint64_t g = ga + j;
-        if (g >= blk.ustart && g < gend) u[g] = out[16 * s + j];
+        const uint64_t g = ga + j;
+        if (g >= blk.ustart && g < gend) u[g] = (uint8_t)map[16 * s + j];
       }
     }
   }

@@ -118,6 +118,8 @@ SYNTH = [
     dict(n_records=40, mode="long"),                    # records span many blocks
     dict(n_records=2000, block_payload=4096),           # small blocks, many straddles
     dict(n_records=500, block_payload=65536 - 1024, level=6),
+    dict(n_records=3000, block_payload=65536, level=6),  # ISIZE 65536: phase-B round path
+    dict(n_records=3000, block_payload=65280, level=1),  # ISIZE at the map limit
 ]
 
 
