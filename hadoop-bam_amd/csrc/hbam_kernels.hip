@@ -149,20 +149,46 @@ __global__ void k_block_ustart(BlockInfo* __restrict__ blocks, uint32_t n, const
 // ---------------------------------------------------------------------------
 // Inflate phase A: Huffman decode, one wavefront per BGZF block
 // ---------------------------------------------------------------------------
+// A DEFLATE block's symbol stream is decoded by all 64 lanes at once: lane l
+// starts at a guessed bit position B0 + l*S and decodes its slice up to the
+// first symbol boundary at or past the next slice (its "exit").  Huffman
+// streams self-synchronise, so a lane that started off a boundary soon falls
+// onto the true path; sync passes re-decode a slice from its predecessor's
+// exit until every start is a true boundary (usually one pass).  A last pass
+// re-decodes each slice from its true start and writes tokens at
+// wave-scanned offsets.  Block headers, dynamic-table decoding and the
+// end-of-output lookahead are wave-uniform scalar code.
+//
+// Semantics follow zlib's inflate() as driven by [htsjdk] BlockGunzipper
+// (one call, all input, ISIZE bytes of output space):
+//   * a field whose bits are not all inside the block's CDATA stops decoding
+//     ("Did not inflate expected amount" = kErrFormat unless output is full);
+//   * invalid codes / distances -> DataFormatException (kErrIO);
+//   * once output is exactly full at a symbol boundary, zlib still decodes the
+//     next litlen code (and a whole length/distance pair, or the next block
+//     header after an end-of-block) before it notices there is no room: those
+//     can still raise errors -> the scalar lookahead below.
+//
 // Table entries (u32):
 //   litlen  [15:0] payload  [20:16] bits to consume  [25:24] literal count  [28:26] kind
 //           kind 0 LIT : payload = 1 or 2 literal bytes; (e & 0x0300ffff) IS the token
 //           kind 1 LEN : payload [8:0] base (3..258), [12:9] extra bits
-//           kind 2 EOB, 3 LONG (code longer than the root: canonical slow path), 4 BAD
-//   dist    [14:0] base  [20:16] bits  [24:21] extra  [28:26] kind (0 ok, 3 LONG, 4 BAD)
+//           kind 2 EOB, 3 LONG (payload = sub-table base), 4 BAD, 5 SLOW (canonical decode)
+//   dist    [14:0] base  [20:16] bits  [24:21] extra  [28:26] kind (0 ok, 3 LONG, 4 BAD, 5 SLOW)
 //   codes   [15:0] symbol [20:16] bits (code-length alphabet, root 7: always direct)
+// Codes longer than the root index a fixed-size sub-table by the next bits;
+// sub-table entries carry the full code length.
 // Tokens (u32): literal  bit31=0, [25:24] count (1..2), [15:0] bytes
 //               match    bit31=1, [30:16] dist-1, [15:0] length
 constexpr int kLitRoot = 10;
-constexpr int kDistRoot = 8;
-enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_LONG = 3, K_BAD = 4 };
+constexpr int kDistRoot = 9;
+constexpr int kLitSubBits = 15 - kLitRoot;
+constexpr int kDistSubBits = 15 - kDistRoot;
+constexpr int kLitSubMax = 16;
+constexpr int kDistSubMax = 4;
+enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_LONG = 3, K_BAD = 4, K_SLOW = 5 };
 constexpr uint32_t kBadEntry = K_BAD << 26;
-constexpr uint32_t kLongEntry = K_LONG << 26;
+constexpr uint32_t kLongMark = (K_LONG << 26) | 0xffffu;
 constexpr uint32_t kKindLit = 1u << 26;  // e < kKindLit  <=>  literal entry
 
 __constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
@@ -177,9 +203,10 @@ __constant__ uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2,  3,  3,  4,  4,  
 __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 struct HuffLds {
-  uint32_t ring[512];             // 2 x 1 KiB compressed-input ring (LDS-DMA target, 16 B aligned)
-  uint32_t lit[1 << kLitRoot];    // litlen fast table (with literal pairs)
-  uint32_t dist[1 << kDistRoot];  // distance fast table (also the code-length table)
+  uint32_t lit[1 << kLitRoot];                      // litlen root table (with literal pairs)
+  uint32_t litsub[kLitSubMax << kLitSubBits];       // litlen sub-tables
+  uint32_t dist[1 << kDistRoot];                    // distance root table (also the code-length table)
+  uint32_t distsub[kDistSubMax << kDistSubBits];    // distance sub-tables
   uint32_t cnt_lit[16];
   uint32_t cnt_dist[16];
   uint32_t offs[16];
@@ -188,6 +215,7 @@ struct HuffLds {
   uint32_t bt_status;
   uint16_t sort_lit[288];
   uint16_t sort_dist[32];
+  uint16_t rev_of[320];
   uint8_t lens[320];
   uint8_t cl_lens[20];
 };
@@ -216,10 +244,11 @@ __device__ __forceinline__ uint32_t make_entry(int mode, uint32_t s, uint32_t le
 // (DISTS) or error (CODES).  Returns 0 on success.  Per-length state lives in
 // LDS (not in unrolled SGPR arrays) to keep the decode loop's registers free.
 // Callers must rfl() the result: a call's return value is divergent to the
-// compiler, and one divergent branch here turns the whole decode state into
-// VGPRs with exec-masked control flow (measured: ~5x the instructions).
+// compiler, and one divergent branch at the call site turns the whole decode
+// state into VGPRs with exec-masked control flow.
 __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* lens, int nsym, int root, int mode,
-                                                     uint32_t* tab, uint32_t* cnt, uint16_t* sorted) {
+                                                     uint32_t* tab, uint32_t* cnt, uint16_t* sorted, uint32_t* sub,
+                                                     int subbits, int submax) {
   const uint32_t lane = lane_id();
   if (lane < 16) {
     cnt[lane] = 0;
@@ -256,7 +285,9 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
   const uint32_t st = rfl(L.bt_status);
   if (st == 1) return 1;
   if (st == 2) return 0;  // no codes: all-invalid table
+  const uint32_t rmask = (1u << root) - 1;
   const uint64_t ltmask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  bool any_long = false;
   for (int c0 = 0; c0 < nsym; c0 += 64) {
     const int s = c0 + (int)lane;
     const uint32_t l = s < nsym ? lens[s] : 0;
@@ -271,11 +302,42 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
       sorted[L.offs[l] + rank] = (uint16_t)s;
       const uint32_t code = L.firstc[l] + rank;
       const uint32_t rev = __brev(code) >> (32 - l);
+      L.rev_of[s] = (uint16_t)rev;
       if ((int)l <= root) {
         const uint32_t e = make_entry(mode, (uint32_t)s, l);
         for (uint32_t i = rev; i < (1u << root); i += (1u << l)) tab[i] = e;
       } else {
-        tab[rev & ((1u << root) - 1)] = kLongEntry;
+        tab[rev & rmask] = kLongMark;
+        any_long = true;
+      }
+    }
+  }
+  __syncthreads();
+  if (__ballot(any_long) == 0) return 0;
+  // one fixed-size sub-table per long-code prefix, numbered in index order
+  uint32_t nsub = 0;
+  for (int c0 = 0; c0 < (1 << root); c0 += 64) {
+    const uint32_t i = c0 + lane;
+    const bool mk = tab[i] == kLongMark;
+    const uint64_t m = __ballot(mk);
+    if (mk) {
+      const uint32_t idx = nsub + (uint32_t)__popcll(m & ltmask);
+      tab[i] = idx < (uint32_t)submax ? ((K_LONG << 26) | (idx << subbits)) : (K_SLOW << 26);
+    }
+    nsub += (uint32_t)__popcll(m);
+  }
+  const uint32_t nsub_used = min(nsub, (uint32_t)submax);
+  for (uint32_t i = lane; i < (nsub_used << subbits); i += 64) sub[i] = kBadEntry;
+  __syncthreads();
+  for (int s = lane; s < nsym; s += 64) {
+    const uint32_t l = lens[s];
+    if ((int)l > root) {
+      const uint32_t rev = L.rev_of[s];
+      const uint32_t e = tab[rev & rmask];
+      if ((e >> 26) == K_LONG) {
+        const uint32_t b = e & 0xffffu;
+        const uint32_t ent = make_entry(mode, (uint32_t)s, l);
+        for (uint32_t k = rev >> root; k < (1u << subbits); k += 1u << (l - root)) sub[b + k] = ent;
       }
     }
   }
@@ -307,15 +369,16 @@ __device__ __attribute__((noinline)) void pair_literals(HuffLds& L) {
   __syncthreads();
 }
 
-// puff-style canonical decode for codes longer than the table root (rare).
-__device__ uint32_t slow_decode(uint64_t bits, const uint32_t* cnt, const uint16_t* sorted, int mode) {
+// puff-style canonical decode (sub-table overflow, split literal pairs: rare).
+template <bool UNIFORM>
+__device__ uint32_t canon_decode(uint64_t bits, const uint32_t* cnt, const uint16_t* sorted, int mode) {
   int code = 0, first = 0, index = 0;
   for (int len = 1; len < 16; ++len) {
     code |= (int)(bits & 1);
     bits >>= 1;
-    int count = (int)rfl(cnt[len]);
+    const int count = UNIFORM ? (int)rfl(cnt[len]) : (int)cnt[len];
     if (code - count < first) {
-      uint32_t s = rfl(sorted[index + (code - first)]);
+      const uint32_t s = UNIFORM ? rfl(sorted[index + (code - first)]) : sorted[index + (code - first)];
       return make_entry(mode, s, (uint32_t)len);
     }
     index += count;
@@ -326,11 +389,137 @@ __device__ uint32_t slow_decode(uint64_t bits, const uint32_t* cnt, const uint16
   return kBadEntry;
 }
 
-// LDS-DMA one 1 KiB chunk of compressed input into ring half (c & 1).
-__device__ __forceinline__ void ring_dma(HuffLds& L, const uint8_t* file, uint64_t abase, uint32_t c) {
-  __builtin_amdgcn_global_load_lds(
-      (const __attribute__((address_space(1))) void*)(file + abase + 1024ull * c + 16ull * lane_id()),
-      (__attribute__((address_space(3))) void*)(L.ring + 256u * (c & 1u)), 16, 0, 0);
+template <bool UNIFORM>
+__device__ __forceinline__ uint32_t lit_lookup(const HuffLds& L, uint64_t b) {
+  uint32_t e = L.lit[(uint32_t)b & ((1u << kLitRoot) - 1)];
+  if (UNIFORM) e = rfl(e);
+  const uint32_t k = e >> 26;
+  if (k == K_LONG) {
+    e = L.litsub[(e & 0xffffu) + ((uint32_t)(b >> kLitRoot) & ((1u << kLitSubBits) - 1))];
+    if (UNIFORM) e = rfl(e);
+  } else if (k == K_SLOW) {
+    e = canon_decode<UNIFORM>(b, L.cnt_lit, L.sort_lit, 0);
+  }
+  return e;
+}
+template <bool UNIFORM>
+__device__ __forceinline__ uint32_t dist_lookup(const HuffLds& L, uint64_t b) {
+  uint32_t d = L.dist[(uint32_t)b & ((1u << kDistRoot) - 1)];
+  if (UNIFORM) d = rfl(d);
+  const uint32_t k = d >> 26;
+  if (k == K_LONG) {
+    d = L.distsub[(d & 0xffffu) + ((uint32_t)(b >> kDistRoot) & ((1u << kDistSubBits) - 1))];
+    if (UNIFORM) d = rfl(d);
+  } else if (k == K_SLOW) {
+    d = canon_decode<UNIFORM>(b, L.cnt_dist, L.sort_dist, 1);
+  }
+  return d;
+}
+
+// lane_decode exit events
+enum : uint32_t { EV_STOP = 0, EV_EOB = 1, EV_INPUT = 2, EV_ERR = 3, EV_FULLX = 4, EV_FULLO = 5 };
+
+// Decode from bit `a` while the position is below `stop` (bit positions are
+// relative to the 16 B-aligned word base W; E = end of CDATA).  Returns the
+// event that ended the walk; x = position reached, nt/nb = tokens/bytes
+// decoded.  EMIT additionally writes tokens to tok[0..nt) and applies the
+// output-space rules with the output position of the first token = out0.
+template <bool EMIT>
+__device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t* __restrict__ W, uint32_t a,
+                                                uint32_t stop, uint32_t E, uint32_t& x, uint32_t& nt, uint32_t& nb,
+                                                uint32_t* __restrict__ tok, uint32_t out0, uint32_t isize) {
+  uint32_t wd = a >> 5;
+  uint64_t buf = (((uint64_t)W[wd + 1] << 32) | W[wd]) >> (a & 31);
+  uint32_t cnt = 64 - (a & 31);
+  wd += 2;
+  uint32_t nx = W[wd];
+  uint32_t pos = a, ev = EV_STOP;
+  nt = 0;
+  nb = 0;
+#define LREFILL()                        \
+  do {                                   \
+    if (cnt <= 32) {                     \
+      buf |= (uint64_t)nx << cnt;        \
+      cnt += 32;                         \
+      ++wd;                              \
+      nx = W[wd];                        \
+    }                                    \
+  } while (0)
+#define LCONSUME(n)  \
+  do {               \
+    buf >>= (n);     \
+    cnt -= (n);      \
+    pos += (n);      \
+  } while (0)
+  while (pos < stop) {
+    if (EMIT && out0 + nb >= isize) {
+      ev = (out0 + nb == isize) ? EV_FULLX : EV_FULLO;
+      break;
+    }
+    LREFILL();
+    uint32_t e = lit_lookup<false>(L, buf);
+    uint32_t n1 = (e >> 16) & 31;
+    uint32_t t, len;
+    if (e < kKindLit) {
+      if (pos + n1 > E) {  // a pair may straddle the end: decode the first literal alone
+        if ((e >> 24) == 2u) {
+          e = canon_decode<false>(buf, L.cnt_lit, L.sort_lit, 0);
+          n1 = (e >> 16) & 31;
+        }
+        if (pos + n1 > E) { ev = EV_INPUT; break; }
+      }
+      t = e & 0x0300ffffu;
+      len = e >> 24;
+      LCONSUME(n1);
+    } else {
+      const uint32_t k = e >> 26;
+      if (k == K_LEN) {
+        const uint32_t ex = (e >> 9) & 15;
+        if (pos + n1 + ex > E) { ev = EV_INPUT; break; }
+        len = (e & 511) + ((uint32_t)(buf >> n1) & ((1u << ex) - 1));
+        LCONSUME(n1 + ex);
+        LREFILL();
+        const uint32_t d = dist_lookup<false>(L, buf);
+        const uint32_t dn = (d >> 16) & 31;
+        if (d >= kKindLit) {  // invalid distance code
+          ev = (pos + max(dn, 1u) > E) ? EV_INPUT : EV_ERR;
+          break;
+        }
+        const uint32_t dx = (d >> 21) & 15;
+        if (pos + dn + dx > E) { ev = EV_INPUT; break; }
+        const uint32_t dist = (d & 0x7fff) + ((uint32_t)(buf >> dn) & ((1u << dx) - 1));
+        LCONSUME(dn + dx);
+        if (EMIT && dist > out0 + nb) { ev = EV_ERR; break; }  // invalid distance too far back
+        t = 0x80000000u | ((dist - 1) << 16) | len;
+      } else if (k == K_EOB) {
+        if (pos + n1 > E) { ev = EV_INPUT; break; }
+        LCONSUME(n1);
+        ev = EV_EOB;
+        break;
+      } else {  // invalid literal/length code
+        ev = (pos + max(n1, 1u) > E) ? EV_INPUT : EV_ERR;
+        break;
+      }
+    }
+    if (EMIT) tok[nt] = t;
+    ++nt;
+    nb += len;
+  }
+#undef LREFILL
+#undef LCONSUME
+  x = pos;
+  return ev;
+}
+
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v) {
+  const uint32_t lane = lane_id();
+  uint32_t s = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(s, d, 64);
+    if (lane >= (uint32_t)d) s += t;
+  }
+  return s - v;
 }
 
 __global__ __launch_bounds__(64) void k_inflate_huff(const uint8_t* __restrict__ file,
@@ -347,227 +536,265 @@ __global__ __launch_bounds__(64) void k_inflate_huff(const uint8_t* __restrict__
     return;
   }
   uint32_t* tok_out = tokens + (blk.ustart - chunk_ustart);
-  const uint64_t sbyte = blk.coff + 18;             // cdata start
-  const uint32_t clen = blk.csize - 26;             // cdata length
+  const uint64_t sbyte = blk.coff + 18;  // cdata start
   const uint64_t abase = sbyte & ~15ull;
-  const uint32_t lead = (uint32_t)(sbyte - abase);  // junk bytes before cdata
-  const uint64_t end_bits = 8ull * (lead + clen);
+  const uint32_t* __restrict__ W = reinterpret_cast<const uint32_t*>(file + abase);
+  const uint32_t E = 8u * ((uint32_t)(sbyte - abase) + (blk.csize - 26));  // end of CDATA (bits from W)
 
-  // prime the ring: chunks 0 and 1 resident
-  ring_dma(L, file, abase, 0);
-  ring_dma(L, file, abase, 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // wave-uniform bit reader (block headers, code lengths, lookahead)
+  uint64_t sbuf;
+  uint32_t scnt, swd;
+#define SSEEK(p)                                                   \
+  do {                                                             \
+    const uint32_t p_ = (p);                                       \
+    swd = p_ >> 5;                                                 \
+    sbuf = (((uint64_t)rfl(W[swd + 1]) << 32) | rfl(W[swd])) >> (p_ & 31); \
+    scnt = 64 - (p_ & 31);                                         \
+    swd += 2;                                                      \
+  } while (0)
+#define SFILL()                                \
+  do {                                         \
+    if (scnt <= 32) {                          \
+      sbuf |= (uint64_t)rfl(W[swd]) << scnt;   \
+      scnt += 32;                              \
+      ++swd;                                   \
+    }                                          \
+  } while (0)
+#define SPOS() (32u * swd - scnt)
+#define SCONSUME(n) \
+  do {              \
+    sbuf >>= (n);   \
+    scnt -= (n);    \
+  } while (0)
 
-  uint64_t buf = 0;
-  uint32_t cnt = 0;
-  uint32_t rd = lead >> 2;  // ring dword index of `nextw` (relative to abase/4)
+  SSEEK(8u * (uint32_t)(sbyte - abase));
+  uint32_t outpos = 0, ntok = 0;
   int err = kOk;
-  const uint32_t end_bits32 = (uint32_t)end_bits;  // < 2^20: 32-bit, scalar compares
-  uint32_t nextw = L.ring[rd & 511];  // prefetched next input dword (VGPR; read at use)
-
-  // one 32-bit refill from the prefetched dword, then prefetch the next one.
-  // Entering chunk c (rd % 256 == 0): chunk c was DMA'd one chunk ago ->
-  // wait for it, then DMA chunk c+1 into the half chunk c-1 just freed.
-#define REFILL1()                                                       \
-  do {                                                                  \
-    buf |= (uint64_t)rfl(nextw) << cnt;                                 \
-    cnt += 32;                                                          \
-    ++rd;                                                               \
-    if ((rd & 255) == 0) {                                              \
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                  \
-      ring_dma(L, file, abase, (rd >> 8) + 1);                          \
-      if (32u * rd - cnt > end_bits32 + 64u) err = kErrFormat;          \
-    }                                                                   \
-    nextw = L.ring[rd & 511];                                           \
-  } while (0)
-#define ENSURE()              \
-  do {                        \
-    if (cnt <= 32) REFILL1(); \
-  } while (0)
-#define CONSUME(n) \
-  do {             \
-    buf >>= (n);   \
-    cnt -= (n);    \
-  } while (0)
-
-  REFILL1();
-  REFILL1();
-  CONSUME(8 * (lead & 3));
-
-  uint32_t outpos = 0, ntok = 0, tokv = 0;
-#define EMIT(t)                                                   \
-  do {                                                            \
-    tokv = (lane == (ntok & 63)) ? (uint32_t)(t) : tokv;          \
-    if ((ntok & 63) == 63) tok_out[(ntok & ~63u) + lane] = tokv;  \
-    ntok++;                                                       \
-  } while (0)
-
-  uint32_t final_blk = 0;
-  while (!final_blk && outpos < isize && err == kOk) {
-    ENSURE();
-    const uint32_t hdr = (uint32_t)buf & 7;
-    CONSUME(3);
-    final_blk = hdr & 1;
+  bool look = false;  // output exactly full: zlib's lookahead
+  while (err == kOk) {
+    SFILL();
+    if (SPOS() + 3 > E) { if (!look) err = kErrFormat; break; }
+    const uint32_t hdr = (uint32_t)sbuf & 7;
+    SCONSUME(3);
+    const bool final_blk = hdr & 1;
     const uint32_t type = hdr >> 1;
     if (type == 0) {  // stored
-      CONSUME(cnt & 7);
-      ENSURE();
-      if (cnt < 32) REFILL1();
-      const uint32_t len = (uint32_t)buf & 0xffff, nlen = (uint32_t)(buf >> 16) & 0xffff;
-      CONSUME(32);
+      SCONSUME((8u - (SPOS() & 7u)) & 7u);  // to the byte boundary
+      SFILL();
+      if (SPOS() + 32 > E) { if (!look) err = kErrFormat; break; }
+      const uint32_t len = (uint32_t)sbuf & 0xffff, nlen = (uint32_t)(sbuf >> 16) & 0xffff;
+      SCONSUME(32);
       if (len != (~nlen & 0xffffu)) { err = kErrIO; break; }
-      for (uint32_t j = 0; j < len && outpos < isize && err == kOk; ++j) {
-        ENSURE();
-        EMIT((1u << 24) | ((uint32_t)buf & 255));
-        CONSUME(8);
-        outpos++;
+      const uint32_t p = SPOS();  // byte aligned
+      if (look) {
+        if (len != 0) break;  // COPY with no room: zlib stops here
+        if (final_blk) break;
+        continue;
       }
+      const uint32_t n = min(min(len, isize - outpos), (E - p) >> 3);
+      const uint8_t* src = reinterpret_cast<const uint8_t*>(W) + (p >> 3);
+      for (uint32_t j = lane; j < n; j += 64) tok_out[ntok + j] = (1u << 24) | src[j];
+      ntok += n;
+      outpos += n;
+      SSEEK(p + 8 * n);
+      if (n < len) {
+        if (outpos < isize) err = kErrFormat;  // ran out of input
+        break;
+      }
+      if (final_blk) {
+        if (outpos < isize) err = kErrFormat;
+        break;
+      }
+      if (outpos == isize) look = true;
       continue;
-    } else if (type == 1) {  // fixed Huffman
+    }
+    if (type == 3) { err = kErrIO; break; }
+    if (type == 1) {  // fixed Huffman
       for (int s = lane; s < 320; s += 64) {
         uint8_t l;
         if (s < 144) l = 8; else if (s < 256) l = 9; else if (s < 280) l = 7; else if (s < 288) l = 8; else l = 5;
         L.lens[s] = l;
       }
       __syncthreads();
-      if (rfl(build_table(L, L.lens, 288, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit)) ||
-          rfl(build_table(L, L.lens + 288, 32, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist))) {
+      if (rfl(build_table(L, L.lens, 288, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit, L.litsub, kLitSubBits,
+                          kLitSubMax)) ||
+          rfl(build_table(L, L.lens + 288, 32, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist, L.distsub,
+                          kDistSubBits, kDistSubMax))) {
         err = kErrIO;
         break;
       }
       pair_literals(L);
-    } else if (type == 2) {  // dynamic Huffman
-      ENSURE();
-      const uint32_t hlit = ((uint32_t)buf & 31) + 257;
-      const uint32_t hdist = ((uint32_t)(buf >> 5) & 31) + 1;
-      const uint32_t hclen = ((uint32_t)(buf >> 10) & 15) + 4;
-      CONSUME(14);
+    } else {  // dynamic Huffman
+      SFILL();
+      if (SPOS() + 14 > E) { if (!look) err = kErrFormat; break; }
+      const uint32_t hlit = ((uint32_t)sbuf & 31) + 257;
+      const uint32_t hdist = ((uint32_t)(sbuf >> 5) & 31) + 1;
+      const uint32_t hclen = ((uint32_t)(sbuf >> 10) & 15) + 4;
+      SCONSUME(14);
       if (hlit > 286 || hdist > 30) { err = kErrIO; break; }
+      if (SPOS() + 3 * hclen > E) { if (!look) err = kErrFormat; break; }
       if (lane < 20) L.cl_lens[lane] = 0;
       __syncthreads();
       for (uint32_t i = 0; i < hclen; ++i) {
-        ENSURE();
-        const uint32_t v = (uint32_t)buf & 7;
-        CONSUME(3);
+        SFILL();
+        const uint32_t v = (uint32_t)sbuf & 7;
+        SCONSUME(3);
         if (lane == 0) L.cl_lens[kClOrder[i]] = (uint8_t)v;
       }
       __syncthreads();
-      if (rfl(build_table(L, L.cl_lens, 19, 7, 2, L.dist, L.cnt_dist, L.sort_dist))) { err = kErrIO; break; }
+      if (rfl(build_table(L, L.cl_lens, 19, 7, 2, L.dist, L.cnt_dist, L.sort_dist, nullptr, 0, 0))) {
+        err = kErrIO;
+        break;
+      }
       const uint32_t ntot = hlit + hdist;
       uint32_t i = 0, last = 0;
+      bool stop = false;
       while (i < ntot) {
-        ENSURE();
-        if (err != kOk) break;
-        const uint32_t e = rfl(L.dist[(uint32_t)buf & 127]);
-        if (e >= kKindLit) { err = kErrIO; break; }
-        CONSUME((e >> 16) & 31);
+        SFILL();
+        const uint32_t e = rfl(L.dist[(uint32_t)sbuf & 127]);
+        const uint32_t nbits = (e >> 16) & 31;
+        if (SPOS() + nbits > E) { stop = true; break; }
         const uint32_t sym = e & 0xffff;
-        uint32_t rep, val;
+        uint32_t rep, val, xb = 0;
         if (sym < 16) {
           rep = 1;
           val = sym;
         } else if (sym == 16) {
-          if (i == 0) { err = kErrIO; break; }
-          rep = 3 + ((uint32_t)buf & 3);
-          CONSUME(2);
+          xb = 2;
+          rep = 3 + ((uint32_t)(sbuf >> nbits) & 3);
           val = last;
         } else if (sym == 17) {
-          rep = 3 + ((uint32_t)buf & 7);
-          CONSUME(3);
+          xb = 3;
+          rep = 3 + ((uint32_t)(sbuf >> nbits) & 7);
           val = 0;
         } else {
-          rep = 11 + ((uint32_t)buf & 127);
-          CONSUME(7);
+          xb = 7;
+          rep = 11 + ((uint32_t)(sbuf >> nbits) & 127);
           val = 0;
         }
+        if (SPOS() + nbits + xb > E) { stop = true; break; }
+        if (sym == 16 && i == 0) { err = kErrIO; break; }  // repeat with no previous length
+        SCONSUME(nbits + xb);
         if (i + rep > ntot) { err = kErrIO; break; }
         for (uint32_t j = lane; j < rep; j += 64) L.lens[i + j] = (uint8_t)val;
         i += rep;
         last = val;
       }
       if (err != kOk) break;
+      if (stop) { if (!look) err = kErrFormat; break; }
       __syncthreads();
       if (rfl(L.lens[256]) == 0) { err = kErrIO; break; }
-      if (rfl(build_table(L, L.lens, (int)hlit, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit)) ||
-          rfl(build_table(L, L.lens + hlit, (int)hdist, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist))) {
+      if (rfl(build_table(L, L.lens, (int)hlit, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit, L.litsub,
+                          kLitSubBits, kLitSubMax)) ||
+          rfl(build_table(L, L.lens + hlit, (int)hdist, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist,
+                          L.distsub, kDistSubBits, kDistSubMax))) {
         err = kErrIO;
         break;
       }
       pair_literals(L);
-    } else {
-      err = kErrIO;  // invalid block type
-      break;
     }
 
-    // ---- symbol loop: bits >= 33 after ENSURE; a literal pair takes <= 10,
-    //      a length <= 20, a distance <= 28 (ENSURE in between).  Literals run
-    //      in an inner loop with a single back-edge (no loop-carried copies).
-    if (outpos < isize && err == kOk) {
-      ENSURE();
-      uint32_t e = rfl(L.lit[(uint32_t)buf & ((1u << kLitRoot) - 1)]);
-      for (;;) {
-        while (e < kKindLit) {  // one or two literals: the entry is the token
-          CONSUME((e >> 16) & 31);
-          EMIT(e & 0x0300ffffu);
-          outpos += e >> 24;
-          if (outpos >= isize) goto block_done;
-          ENSURE();
-          e = rfl(L.lit[(uint32_t)buf & ((1u << kLitRoot) - 1)]);
+    if (!look) {
+      // ---- all-lane decode of this block's symbols
+      const uint32_t B0 = SPOS();
+      const uint32_t R = E > B0 ? E - B0 : 0u;
+      const uint32_t S = (R + 63) >> 6;
+      uint32_t a = min(B0 + lane * S, E);
+      const uint32_t stop = lane == 63 ? E : min(B0 + (lane + 1) * S, E);
+      uint32_t x, nt, nb;
+      uint32_t ev = lane_decode<false>(L, W, a, stop, E, x, nt, nb, nullptr, 0, 0);
+      for (;;) {  // sync: restart each slice from its predecessor's exit
+        const uint32_t px = __shfl_up(x, 1, 64);
+        const uint32_t pev = __shfl_up(ev, 1, 64);
+        const bool need = lane > 0 && pev == EV_STOP && px != a;
+        if (__ballot(need) == 0) break;
+        if (need) {
+          a = px;
+          ev = lane_decode<false>(L, W, a, stop, E, x, nt, nb, nullptr, 0, 0);
         }
-        if (err != kOk) goto block_done;
-        uint32_t kind = e >> 26;
-        if (kind == K_LONG) {
-          e = slow_decode(buf, L.cnt_lit, L.sort_lit, 0);
-          kind = e >> 26;
-          if (kind == K_LIT) continue;  // re-enters the literal loop with the decoded entry
-        }
-        if (kind == K_LEN) {
-          CONSUME((e >> 16) & 31);
-          const uint32_t ex = (e >> 9) & 15;
-          const uint32_t len = (e & 511) + ((uint32_t)buf & ((1u << ex) - 1));
-          CONSUME(ex);
-          ENSURE();
-          uint32_t d = rfl(L.dist[(uint32_t)buf & ((1u << kDistRoot) - 1)]);
-          if ((d >> 26) == K_LONG) d = slow_decode(buf, L.cnt_dist, L.sort_dist, 1);
-          if (d >= kKindLit) { err = kErrIO; goto block_done; }  // invalid distance code
-          CONSUME((d >> 16) & 31);
-          const uint32_t dx = (d >> 21) & 15;
-          const uint32_t dist = (d & 0x7fff) + ((uint32_t)buf & ((1u << dx) - 1));
-          CONSUME(dx);
-          if (dist > outpos) { err = kErrIO; goto block_done; }  // invalid distance too far back
-          EMIT(0x80000000u | ((dist - 1) << 16) | len);
-          outpos += len;
-          if (outpos >= isize) goto block_done;
-          ENSURE();
-          e = rfl(L.lit[(uint32_t)buf & ((1u << kLitRoot) - 1)]);
-          continue;
-        }
-        if (kind == K_EOB) {
-          CONSUME((e >> 16) & 31);
-          break;
-        }
-        err = kErrIO;  // invalid literal/length code
+      }
+      const uint64_t evm = __ballot(ev != EV_STOP);
+      const uint32_t lend = evm ? (uint32_t)__ffsll((unsigned long long)evm) - 1 : 63u;
+      const bool valid = lane <= lend;
+      const uint32_t toff = wave_excl_sum(valid ? nt : 0u);
+      const uint32_t boff = wave_excl_sum(valid ? nb : 0u);
+      uint32_t x3 = a, nt3 = 0, nb3 = 0, ev3 = EV_STOP;
+      if (valid)
+        ev3 = lane_decode<true>(L, W, a, stop, E, x3, nt3, nb3, tok_out + ntok + toff, outpos + boff, isize);
+      const uint64_t m3 = __ballot(valid && ev3 != EV_STOP);
+      const uint32_t f = m3 ? (uint32_t)__ffsll((unsigned long long)m3) - 1 : lend;
+      const uint32_t fev = __shfl(ev3, f, 64);
+      const uint32_t ftok = __shfl(toff + nt3, f, 64);
+      const uint32_t fbytes = __shfl(boff + nb3, f, 64);
+      const uint32_t fx = __shfl(x3, f, 64);
+      ntok = rfl(ntok + ftok);
+      outpos = rfl(outpos + fbytes);
+      const uint32_t fe = rfl(fev), fxs = rfl(fx);
+      if (m3 == 0) {  // walked to the end of CDATA without an end-of-block
+        if (outpos < isize) err = kErrFormat;
+        else if (outpos == isize) { look = true; SSEEK(fxs); }
+        else break;
+        if (err != kOk || fxs >= E) break;
+      } else if (fe == EV_EOB) {
+        SSEEK(fxs);
+        if (final_blk) { err = kErrFormat; break; }  // EOB before ISIZE bytes
+        continue;
+      } else if (fe == EV_FULLX) {
+        look = true;
+        SSEEK(fxs);
+      } else if (fe == EV_FULLO) {
+        break;
+      } else {
+        err = fe == EV_ERR ? kErrIO : kErrFormat;
         break;
       }
     }
-  block_done:
-    if (32u * rd - cnt > end_bits32) err = kErrFormat;  // ran past the input
-  }
-  if (ntok & 63) {
-    if (lane < (ntok & 63)) tok_out[(ntok & ~63u) + lane] = tokv;
+    // ---- lookahead (output exactly full): decode on until a symbol needs room
+    bool next_hdr = false;
+    for (;;) {
+      SFILL();
+      const uint32_t p = SPOS();
+      const uint32_t e = lit_lookup<true>(L, sbuf);
+      const uint32_t n1 = (e >> 16) & 31;
+      if (e < kKindLit) break;  // literal: no room (a pair's first code is checked by n1 >= its length)
+      const uint32_t k = e >> 26;
+      if (k == K_LEN) {
+        const uint32_t ex = (e >> 9) & 15;
+        if (p + n1 + ex > E) break;
+        SCONSUME(n1 + ex);
+        SFILL();
+        const uint32_t d = dist_lookup<true>(L, sbuf);
+        const uint32_t dn = (d >> 16) & 31;
+        if (d >= kKindLit) {
+          if (SPOS() + max(dn, 1u) <= E) err = kErrIO;
+          break;
+        }
+        const uint32_t dx = (d >> 21) & 15;
+        if (SPOS() + dn + dx > E) break;
+        const uint32_t dist = (d & 0x7fff) + ((uint32_t)(sbuf >> dn) & ((1u << dx) - 1));
+        if (dist > outpos) err = kErrIO;
+        break;
+      }
+      if (k == K_EOB) {
+        if (p + n1 > E) break;
+        SCONSUME(n1);
+        next_hdr = !final_blk;
+        break;
+      }
+      if (p + max(n1, 1u) <= E) err = kErrIO;  // invalid literal/length code
+      break;
+    }
+    if (!next_hdr) break;
   }
   if (err == kOk && outpos < isize) err = kErrFormat;  // "Did not inflate expected amount"
-  if (err == kOk && 32u * rd - cnt > end_bits32) err = kErrFormat;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA in flight at exit
   if (lane == 0) {
     hout[bi].ntok = ntok;
     hout[bi].status = err;
   }
-#undef REFILL1
-#undef ENSURE
-#undef CONSUME
-#undef EMIT
+#undef SSEEK
+#undef SFILL
+#undef SPOS
+#undef SCONSUME
 }
 
 // ---------------------------------------------------------------------------
