@@ -57,6 +57,26 @@ def cpu_baseline(data, info, seconds):
                       f"oracle/hbam_oracle.c (system zlib) single thread, {dt:.1f} s"}
 
 
+def pmc_traffic(kernels):
+    """HBM bytes per launch of `kernels` (summed) from the newest committed
+    rocprofv3 PMC summary (profiles/*/summary.json, written by
+    profiles/collect.sh + summarize.py: FETCH_SIZE x1024 x2 gfx950 correction,
+    WRITE_SIZE x1024).  None when no summary is committed."""
+    import glob
+    best = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "summary.json")))
+    if not best:
+        return None, None
+    try:
+        ks = json.load(open(best[-1]))["kernels"]
+        tot = 0.0
+        for k in kernels:
+            e = ks[k]
+            tot += e["main_fetch_bytes_corrected"] + e["main_write_bytes"]
+        return int(tot), os.path.relpath(best[-1], ROOT)
+    except (KeyError, ValueError, OSError):
+        return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,11 +143,15 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = u_all * args.steps / elapsed / 1e9
 
-    # dominant kernel pair: inflate (phase A huff + phase B lz77), HIP events on the pipeline stream
-    infl_ms = sum(s["ms_huff"] + s["ms_lz77"] for s in stats) / len(stats)
-    huff_ms = sum(s["ms_huff"] for s in stats) / len(stats)
-    alg_bytes = info["compressed"] + info["uncompressed"]  # C read + U written per launch pair
+    # dominant kernel pair: inflate (phase A huff + phase B lz77), launched as
+    # pairs over chunks of BGZF blocks; HIP events on the pipeline stream.
+    n_launch = max(1, st["inflate_launches"])
+    infl_ms = sum(s_["ms_huff"] + s_["ms_lz77"] for s_ in stats) / len(stats) / n_launch
+    huff_ms = sum(s_["ms_huff"] for s_ in stats) / len(stats) / n_launch
+    lz_ms = sum(s_["ms_lz77"] for s_ in stats) / len(stats) / n_launch
+    alg_bytes = (info["compressed"] + info["uncompressed"]) / n_launch  # C read + U written per launch pair
     achieved = alg_bytes / (infl_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(("hbam::k_inflate_huff", "hbam::k_inflate_lz77"))
     out = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -146,13 +170,16 @@ def main():
                    "uncompressed_bytes_per_gpu": info["uncompressed"], "bgzf_blocks_per_gpu": info["blocks"],
                    "parallelism": f"bgzf-shard x{world}"},
         "records_per_s": round(n_all * args.steps / elapsed, 1),
+        "link_fallbacks": int(sum(s_["link_fallbacks"] for s_ in stats)),
         "stages_ms": {k: round(st[k], 3) for k in ("ms_locate", "ms_inflate", "ms_huff", "ms_lz77", "ms_chain",
                                                     "ms_decode", "ms_total")},
-        "roofline": {"bound": "hbm", "kernel": "k_inflate_huff+k_inflate_lz77",
+        "roofline": {"bound": "hbm", "kernel": "k_inflate_huff+k_inflate_lz77 (one launch pair)",
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                     "avg_launch_ms": round(infl_ms, 3), "huff_ms": round(huff_ms, 3),
-                     "alg_bytes_per_launch": alg_bytes},
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     "launches_per_pass": n_launch, "avg_launch_ms": round(infl_ms, 3),
+                     "huff_avg_launch_ms": round(huff_ms, 3), "lz77_avg_launch_ms": round(lz_ms, 3),
+                     "alg_bytes_per_launch": int(alg_bytes)},
         "cpu_baseline": None,
     }
     if rank == 0 and not args.no_cpu_baseline:

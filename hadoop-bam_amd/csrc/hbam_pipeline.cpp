@@ -165,8 +165,12 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force) {
   bool any = false;
   while (b < b1) {
     if (!force && inflated_[b]) { ++b; continue; }
+    // even chunks (a short last chunk would pay a whole wave tail for few blocks)
+    const uint32_t left = b1 - b;
+    const uint32_t nchunks = (left + kInflateChunkBlocks - 1) / kInflateChunkBlocks;
+    const uint32_t per = (left + nchunks - 1) / nchunks;
     uint32_t e = b;
-    while (e < b1 && e - b < kInflateChunkBlocks && (force || !inflated_[e])) ++e;
+    while (e < b1 && e - b < per && (force || !inflated_[e])) ++e;
     const uint64_t cu = hblocks_[b].ustart;
     const uint64_t uend = hblocks_[e - 1].ustart + hblocks_[e - 1].isize;
     HIPCHK(tokens_.reserve(std::max<uint64_t>(uend - cu, 64)));
@@ -186,6 +190,7 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force) {
       HIPCHK(launch_inflate(fbase, dblocks_.p, b, e - b, cu, tokens_.p, hout_.p, du_.p, stream_));
     }
     for (uint32_t k = b; k < e; ++k) inflated_[k] = 1;
+    ++inflate_launches_;
     any = true;
     b = e;
   }

@@ -101,6 +101,7 @@ class Pipeline {
   int32_t n_ref() const { return n_ref_; }
 
   uint64_t link_fallbacks() const { return link_fallbacks_; }
+  uint64_t inflate_launches() const { return inflate_launches_; }
   StageTimes times;
   bool timing = false;  // record per-stage HIP event times
 
@@ -122,6 +123,7 @@ class Pipeline {
   uint32_t ndead_ = 0;
   int32_t n_ref_ = 0;
   uint64_t link_fallbacks_ = 0;
+  uint64_t inflate_launches_ = 0;  // phase A/B launch pairs so far
 
   DevBuf<uint8_t> du_;
   std::vector<uint8_t> inflated_;  // per block flag

@@ -151,6 +151,8 @@ typedef struct hbam_gpu_stats {
   uint64_t key_xor, voff_sum; /* order-independent digests of the keys / voffs */
   float ms_locate, ms_inflate, ms_huff, ms_lz77, ms_chain, ms_decode, ms_total;
   int32_t status;
+  int32_t link_fallbacks;     /* record-chain spans that took the exact serial link */
+  int32_t inflate_launches;   /* phase A + B launch pairs of this run */
   int32_t reserved;
 } hbam_gpu_stats;
 

@@ -1,0 +1,140 @@
+#!/usr/bin/env python3
+"""Summarise one rocprofv3 collection (profiles/collect.sh) into JSON.
+
+Input dir layout: <dir>/trace/**/run_kernel_stats.csv (kernel trace --stats),
+<dir>/{fetch,write,sq}/**/run_counter_collection.csv (one PMC pass each).
+
+Per kernel: calls, average duration (ns) and, from the PMC passes, average
+FETCH_SIZE / WRITE_SIZE per dispatch converted to bytes.  "main_*" fields
+average only the full-size dispatches of a kernel (grid >= half its largest
+grid): the pipeline also launches tiny instances (header read), which would
+otherwise skew a per-launch figure.  Corrections follow
+/opt/skills/guides/MI355X_MICROARCH.md "HBM [CDNA4]": FETCH_SIZE/WRITE_SIZE are
+kilobytes (counter_defs.yaml), and on gfx950 FETCH_SIZE reports half the bytes
+of a wide coalesced streaming read, so it is doubled ("fetch_bytes_corrected").
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def _find(d, name):
+    hits = glob.glob(os.path.join(d, "**", name), recursive=True)
+    return hits[0] if hits else None
+
+
+def _col(row, *cands):
+    for c in cands:
+        if c in row:
+            return row[c]
+    for k in row:
+        for c in cands:
+            if k.lower() == c.lower():
+                return row[k]
+    raise KeyError(cands)
+
+
+def short(name):
+    n = name.split("(")[0]
+    if "rocprim" in n:
+        return "rocprim:" + ("scan" if "scan" in name else "sort" if "sort" in name else "other")
+    return n.replace("void ", "").strip()
+
+
+def kernel_stats(d):
+    p = _find(os.path.join(d, "trace"), "*kernel_stats.csv")
+    out = {}
+    if not p:
+        return out
+    for r in csv.DictReader(open(p)):
+        name = short(_col(r, "Name", "KernelName"))
+        calls = int(_col(r, "Calls"))
+        tot = float(_col(r, "TotalDurationNs"))
+        e = out.setdefault(name, {"calls": 0, "total_ns": 0.0})
+        e["calls"] += calls
+        e["total_ns"] += tot
+    for e in out.values():
+        e["avg_ns"] = e["total_ns"] / max(e["calls"], 1)
+    return out
+
+
+def main_dispatch_durations(d):
+    p = _find(os.path.join(d, "trace"), "*kernel_trace.csv")
+    out = {}
+    if not p:
+        return out
+    rows = defaultdict(list)
+    for r in csv.DictReader(open(p)):
+        g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        rows[short(r["Kernel_Name"])].append((g, int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    for k, v in rows.items():
+        gmax = max(g for g, _ in v)
+        main = [t for g, t in v if 2 * g >= gmax]
+        out[k] = {"main_calls": len(main), "main_avg_ns": sum(main) / len(main), "main_grid": gmax}
+    return out
+
+
+def counters(d, sub):
+    p = _find(os.path.join(d, sub), "*counter_collection.csv")
+    agg = defaultdict(lambda: defaultdict(list))
+    if not p:
+        return {}
+    per_dispatch = defaultdict(float)
+    names = {}
+    grid = {}
+    for r in csv.DictReader(open(p)):
+        k = short(_col(r, "Kernel_Name", "KernelName"))
+        cn = _col(r, "Counter_Name", "CounterName")
+        v = float(_col(r, "Counter_Value", "CounterValue"))
+        disp = _col(r, "Dispatch_Id", "DispatchId", "Correlation_Id")
+        per_dispatch[(k, cn, disp)] += v
+        names[(k, cn, disp)] = (k, cn)
+        grid[(k, cn, disp)] = int(_col(r, "Grid_Size"))
+    gmax = defaultdict(int)
+    for key, g in grid.items():
+        gmax[names[key][0]] = max(gmax[names[key][0]], g)
+    for key, v in per_dispatch.items():
+        k, cn = names[key]
+        agg[k][cn].append(v)
+        if 2 * grid[key] >= gmax[k]:
+            agg[k]["main:" + cn].append(v)
+    return {k: {cn: sum(vs) / len(vs) for cn, vs in cs.items()} for k, cs in agg.items()}
+
+
+def main():
+    d = sys.argv[1]
+    ks = kernel_stats(d)
+    for k, e in main_dispatch_durations(d).items():
+        ks.setdefault(k, {}).update(e)
+    pm = {}
+    for sub in ("fetch", "write", "sq"):
+        for k, cs in counters(d, sub).items():
+            pm.setdefault(k, {}).update(cs)
+    res = {}
+    for k in sorted(set(ks) | set(pm), key=lambda k: -ks.get(k, {}).get("total_ns", 0)):
+        e = dict(ks.get(k, {}))
+        c = pm.get(k, {})
+        for pre in ("", "main:"):
+            tag = pre.replace(":", "_")
+            if pre + "FETCH_SIZE" in c:
+                e[tag + "fetch_kb_raw"] = c[pre + "FETCH_SIZE"]
+                e[tag + "fetch_bytes_corrected"] = c[pre + "FETCH_SIZE"] * 1024 * 2
+            if pre + "WRITE_SIZE" in c:
+                e[tag + "write_kb_raw"] = c[pre + "WRITE_SIZE"]
+                e[tag + "write_bytes"] = c[pre + "WRITE_SIZE"] * 1024
+        for cn, v in c.items():
+            if cn.startswith("SQ_"):
+                e[cn] = v
+        if "SQ_LDS_BANK_CONFLICT" in c and c.get("SQ_INSTS_LDS"):
+            e["lds_bank_conflict_per_lds_inst"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_INSTS_LDS"]
+        if c.get("SQ_ACTIVE_INST_VALU") is not None and c.get("SQ_WAVE_CYCLES"):
+            e["valu_active_frac_of_wave_cycles"] = c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"]
+        res[k] = e
+    print(json.dumps({"kernels": res}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
