@@ -44,6 +44,15 @@ struct HuffOut {
   int32_t status;
 };
 
+// Phase-A table prebuild (k_huff_tables -> k_inflate_huff), per block of a chunk.
+constexpr uint32_t kHuffTableImage = 11008;  // bytes of the LDS table image
+struct HuffTableInfo {
+  uint32_t status;     // 0: tables + B0 valid; else decode the block's headers inline
+  uint32_t B0;         // bit of the first symbol (relative to the 16 B-aligned cdata base)
+  uint32_t final_blk;  // BFINAL of the first DEFLATE block
+  uint32_t pad;
+};
+
 // Record-chain transition rules.
 enum ChainMode : int {
   kReader = 0,  // [htsjdk] BAMRecordCodec.decode (BAMRecordReader path)

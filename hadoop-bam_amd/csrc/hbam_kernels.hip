@@ -21,6 +21,7 @@
 //   sbi_emit       .splitting-bai entries (SplittingBAMIndexer.java:262-287)
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "hbam_device.h"
@@ -147,17 +148,22 @@ __global__ void k_block_ustart(BlockInfo* __restrict__ blocks, uint32_t n, const
 }
 
 // ---------------------------------------------------------------------------
-// Inflate phase A: Huffman decode, one wavefront per BGZF block
+// Inflate phase A: Huffman decode, one 256-thread workgroup per BGZF block
 // ---------------------------------------------------------------------------
-// A DEFLATE block's symbol stream is decoded by all 64 lanes at once: lane l
-// starts at a guessed bit position B0 + l*S and decodes its slice up to the
-// first symbol boundary at or past the next slice (its "exit").  Huffman
-// streams self-synchronise, so a lane that started off a boundary soon falls
-// onto the true path; sync passes re-decode a slice from its predecessor's
-// exit until every start is a true boundary (usually one pass).  A last pass
-// re-decodes each slice from its true start and writes tokens at
-// wave-scanned offsets.  Block headers, dynamic-table decoding and the
-// end-of-output lookahead are wave-uniform scalar code.
+// The block's compressed bytes are staged in LDS (dynamic shared memory sized
+// per launch to the largest block of the chunk) by coalesced 16 B loads; the
+// Huffman tables (~11 KiB) sit next to them.  Wave 0 parses block headers,
+// decodes code lengths and builds the tables (wave-uniform scalar code, the
+// other waves wait at a barrier).  A DEFLATE block's symbol stream is then
+// decoded by all 256 lanes at once: lane l starts at a guessed bit position
+// B0 + l*S and decodes its slice up to the first symbol boundary at or past
+// the next slice (its "exit").  Huffman streams self-synchronise, so a lane
+// that started off a boundary soon falls onto the true path.  A sync pass
+// re-decodes each slice from its predecessor's exit only until it lands on one
+// of the first kMergePts boundaries its speculative walk recorded (the walks
+// share every symbol from there on), so it costs a few symbols per lane.  A
+// last pass re-decodes each slice from its true start and writes tokens at
+// workgroup-scanned offsets, four at a time (16 B stores).
 //
 // Semantics follow zlib's inflate() as driven by [htsjdk] BlockGunzipper
 // (one call, all input, ISIZE bytes of output space):
@@ -180,15 +186,31 @@ __global__ void k_block_ustart(BlockInfo* __restrict__ blocks, uint32_t n, const
 // sub-table entries carry the full code length.
 // Tokens (u32): literal  bit31=0, [25:24] count (1..2), [15:0] bytes
 //               match    bit31=1, [30:16] dist-1, [15:0] length
+#ifndef HBAM_HUFF_THREADS
+#define HBAM_HUFF_THREADS 256
+#endif
+constexpr int kHuffThreads = HBAM_HUFF_THREADS;
+constexpr int kHuffWaves = kHuffThreads / 64;
+
+// Wave-local ordering of LDS traffic (code run by one wave only).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 constexpr int kLitRoot = 10;
 constexpr int kDistRoot = 9;
-constexpr int kLitSubBits = 15 - kLitRoot;
-constexpr int kDistSubBits = 15 - kDistRoot;
-constexpr int kLitSubMax = 16;
-constexpr int kDistSubMax = 4;
+// Variable-size sub-tables (as zlib's inflate_table): the root entry of a
+// long-code prefix holds the sub-table base and its index width (= the longest
+// code under that prefix - root).  A complete litlen code with a 10-bit root
+// needs at most 310 sub entries (zlib ENOUGH_LENS 1334 - 1024); the distance
+// code with a 9-bit root fits the same capacity.  Prefixes that would not fit
+// fall back to K_SLOW (canonical decode), which valid streams never reach.
+constexpr int kLitSubCap = 512;
+constexpr int kDistSubCap = 512;
 enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_LONG = 3, K_BAD = 4, K_SLOW = 5 };
 constexpr uint32_t kBadEntry = K_BAD << 26;
-constexpr uint32_t kLongMark = (K_LONG << 26) | 0xffffu;
+constexpr uint32_t kLongTag = 0xF0000000u;  // build-time mark: kLongTag | (max len - root)
 constexpr uint32_t kKindLit = 1u << 26;  // e < kKindLit  <=>  literal entry
 
 __constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
@@ -202,23 +224,30 @@ __constant__ uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2,  3,  3,  4,  4,  
                                        6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
+// LDS tables of one DEFLATE block.  The leading kTableImage bytes (lit ..
+// sort_dist) are everything the symbol decode reads; k_huff_tables writes
+// exactly that image to HBM and k_inflate_huff copies it back.
 struct HuffLds {
   uint32_t lit[1 << kLitRoot];                      // litlen root table (with literal pairs)
-  uint32_t litsub[kLitSubMax << kLitSubBits];       // litlen sub-tables
+  uint32_t litsub[kLitSubCap];                      // litlen sub-tables
   uint32_t dist[1 << kDistRoot];                    // distance root table (also the code-length table)
-  uint32_t distsub[kDistSubMax << kDistSubBits];    // distance sub-tables
+  uint32_t distsub[kDistSubCap];                    // distance sub-tables
   uint32_t cnt_lit[16];
   uint32_t cnt_dist[16];
+  uint16_t sort_lit[288];
+  uint16_t sort_dist[32];
+  // ---- build scratch
   uint32_t offs[16];
   uint32_t firstc[16];
   uint32_t base[16];
   uint32_t bt_status;
-  uint16_t sort_lit[288];
-  uint16_t sort_dist[32];
   uint16_t rev_of[320];
   uint8_t lens[320];
   uint8_t cl_lens[20];
 };
+constexpr uint32_t kTableImage = offsetof(HuffLds, offs);
+static_assert(kTableImage % 16 == 0, "table image is copied in 16 B units");
+static_assert(kTableImage == kHuffTableImage, "hbam_device.h kHuffTableImage must match HuffLds");
 
 // mode 0 litlen, 1 distance, 2 code-length codes
 __device__ __forceinline__ uint32_t make_entry(int mode, uint32_t s, uint32_t len) {
@@ -238,7 +267,8 @@ __device__ __forceinline__ uint32_t make_entry(int mode, uint32_t s, uint32_t le
   return (len << 16) | s;
 }
 
-// Canonical Huffman table build, all 64 lanes of the wave.  Validity follows
+// Canonical Huffman table build by ONE wave (wave 0 of the workgroup; the
+// other waves wait at the caller's barrier).  Validity follows
 // zlib inflate_table: over-subscribed -> error; incomplete -> error unless
 // the only code has length 1 (LENS/DISTS); no codes -> all-invalid table
 // (DISTS) or error (CODES).  Returns 0 on success.  Per-length state lives in
@@ -248,18 +278,18 @@ __device__ __forceinline__ uint32_t make_entry(int mode, uint32_t s, uint32_t le
 // state into VGPRs with exec-masked control flow.
 __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* lens, int nsym, int root, int mode,
                                                      uint32_t* tab, uint32_t* cnt, uint16_t* sorted, uint32_t* sub,
-                                                     int subbits, int submax) {
+                                                     int subcap) {
   const uint32_t lane = lane_id();
   if (lane < 16) {
     cnt[lane] = 0;
     L.base[lane] = 0;
   }
-  __syncthreads();
+  wave_sync();
   for (int s = lane; s < nsym; s += 64) {
     const uint32_t l = lens[s];
     if (l) atomicAdd(&cnt[l], 1u);
   }
-  __syncthreads();
+  wave_sync();
   if (lane == 0) {
     int left = 1, maxl = 0, over = 0;
     uint32_t o = 0, code = 0, prev = 0;
@@ -281,7 +311,7 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
     L.bt_status = st;
   }
   for (int i = lane; i < (1 << root); i += 64) tab[i] = kBadEntry;
-  __syncthreads();
+  wave_sync();
   const uint32_t st = rfl(L.bt_status);
   if (st == 1) return 1;
   if (st == 2) return 0;  // no codes: all-invalid table
@@ -307,41 +337,47 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
         const uint32_t e = make_entry(mode, (uint32_t)s, l);
         for (uint32_t i = rev; i < (1u << root); i += (1u << l)) tab[i] = e;
       } else {
-        tab[rev & rmask] = kLongMark;
+        atomicMax(&tab[rev & rmask], kLongTag | (l - (uint32_t)root));  // widest sub-table under the prefix
         any_long = true;
       }
     }
   }
-  __syncthreads();
+  wave_sync();
   if (__ballot(any_long) == 0) return 0;
-  // one fixed-size sub-table per long-code prefix, numbered in index order
-  uint32_t nsub = 0;
+  // sub-table bases: exclusive scan of the sub-table sizes in root-index order
+  uint32_t used = 0;
   for (int c0 = 0; c0 < (1 << root); c0 += 64) {
     const uint32_t i = c0 + lane;
-    const bool mk = tab[i] == kLongMark;
-    const uint64_t m = __ballot(mk);
-    if (mk) {
-      const uint32_t idx = nsub + (uint32_t)__popcll(m & ltmask);
-      tab[i] = idx < (uint32_t)submax ? ((K_LONG << 26) | (idx << subbits)) : (K_SLOW << 26);
+    const uint32_t t = tab[i];
+    const bool mk = t >= kLongTag;
+    const uint32_t bits = t & 15u;
+    const uint32_t sz = mk ? (1u << bits) : 0u;
+    uint32_t inc = sz;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t v = __shfl_up(inc, d, 64);
+      if (lane >= (uint32_t)d) inc += v;
     }
-    nsub += (uint32_t)__popcll(m);
+    const uint32_t base = used + inc - sz;
+    if (mk) tab[i] = base + sz <= (uint32_t)subcap ? ((K_LONG << 26) | (bits << 16) | base) : (K_SLOW << 26);
+    used += (uint32_t)__shfl(inc, 63, 64);
   }
-  const uint32_t nsub_used = min(nsub, (uint32_t)submax);
-  for (uint32_t i = lane; i < (nsub_used << subbits); i += 64) sub[i] = kBadEntry;
-  __syncthreads();
+  const uint32_t nused = min(used, (uint32_t)subcap);
+  for (uint32_t i = lane; i < nused; i += 64) sub[i] = kBadEntry;
+  wave_sync();
   for (int s = lane; s < nsym; s += 64) {
     const uint32_t l = lens[s];
     if ((int)l > root) {
       const uint32_t rev = L.rev_of[s];
       const uint32_t e = tab[rev & rmask];
       if ((e >> 26) == K_LONG) {
-        const uint32_t b = e & 0xffffu;
+        const uint32_t b = e & 0xffffu, sb = (e >> 16) & 15u;
         const uint32_t ent = make_entry(mode, (uint32_t)s, l);
-        for (uint32_t k = rev >> root; k < (1u << subbits); k += 1u << (l - root)) sub[b + k] = ent;
+        for (uint32_t k = rev >> root; k < (1u << sb); k += 1u << (l - root)) sub[b + k] = ent;
       }
     }
   }
-  __syncthreads();
+  wave_sync();
   return 0;
 }
 
@@ -363,10 +399,10 @@ __device__ __attribute__((noinline)) void pair_literals(HuffLds& L) {
         v[j] = ((l1 + l2) << 16) | (2u << 24) | (e1 & 0xffu) | ((e2 & 0xffu) << 8);
     }
   }
-  __syncthreads();
+  wave_sync();
 #pragma unroll
   for (int j = 0; j < 16; ++j) L.lit[lane + 64u * j] = v[j];
-  __syncthreads();
+  wave_sync();
 }
 
 // puff-style canonical decode (sub-table overflow, split literal pairs: rare).
@@ -395,7 +431,7 @@ __device__ __forceinline__ uint32_t lit_lookup(const HuffLds& L, uint64_t b) {
   if (UNIFORM) e = rfl(e);
   const uint32_t k = e >> 26;
   if (k == K_LONG) {
-    e = L.litsub[(e & 0xffffu) + ((uint32_t)(b >> kLitRoot) & ((1u << kLitSubBits) - 1))];
+    e = L.litsub[(e & 0xffffu) + ((uint32_t)(b >> kLitRoot) & ((1u << ((e >> 16) & 15u)) - 1))];
     if (UNIFORM) e = rfl(e);
   } else if (k == K_SLOW) {
     e = canon_decode<UNIFORM>(b, L.cnt_lit, L.sort_lit, 0);
@@ -408,7 +444,7 @@ __device__ __forceinline__ uint32_t dist_lookup(const HuffLds& L, uint64_t b) {
   if (UNIFORM) d = rfl(d);
   const uint32_t k = d >> 26;
   if (k == K_LONG) {
-    d = L.distsub[(d & 0xffffu) + ((uint32_t)(b >> kDistRoot) & ((1u << kDistSubBits) - 1))];
+    d = L.distsub[(d & 0xffffu) + ((uint32_t)(b >> kDistRoot) & ((1u << ((d >> 16) & 15u)) - 1))];
     if (UNIFORM) d = rfl(d);
   } else if (k == K_SLOW) {
     d = canon_decode<UNIFORM>(b, L.cnt_dist, L.sort_dist, 1);
@@ -416,26 +452,54 @@ __device__ __forceinline__ uint32_t dist_lookup(const HuffLds& L, uint64_t b) {
   return d;
 }
 
-// lane_decode exit events
-enum : uint32_t { EV_STOP = 0, EV_EOB = 1, EV_INPUT = 2, EV_ERR = 3, EV_FULLX = 4, EV_FULLO = 5 };
+// lane_decode exit events (EV_MERGE: the sync walk reached a boundary of the
+// lane's speculative walk)
+enum : uint32_t { EV_STOP = 0, EV_EOB = 1, EV_INPUT = 2, EV_ERR = 3, EV_FULLX = 4, EV_FULLO = 5, EV_MERGE = 6 };
+enum { LD_SPEC = 0, LD_SYNC = 1, LD_EMIT = 2 };
+
+// Boundaries of a lane's speculative walk: p[k] = bit position after symbol
+// kMergeFirst << k, b[k] = output bytes decoded up to there (~0u = not reached).
+#ifndef HBAM_MERGE_FIRST
+#define HBAM_MERGE_FIRST 4
+#endif
+constexpr uint32_t kMergeFirst = HBAM_MERGE_FIRST;  // power of two
+struct MergePts {
+  uint32_t p0, p1, p2, p3;
+  uint32_t b0, b1, b2, b3;
+};
+
+// 16 B token store with 4 B alignment (global memory; unaligned mode).
+struct __attribute__((packed, aligned(4))) Tok4 {
+  uint32_t a, b, c, d;
+};
 
 // Decode from bit `a` while the position is below `stop` (bit positions are
-// relative to the 16 B-aligned word base W; E = end of CDATA).  Returns the
+// relative to the 16 B-aligned LDS image W; E = end of CDATA).  Returns the
 // event that ended the walk; x = position reached, nt/nb = tokens/bytes
-// decoded.  EMIT additionally writes tokens to tok[0..nt) and applies the
-// output-space rules with the output position of the first token = out0.
-template <bool EMIT>
+// decoded.
+//   LD_SPEC records the first boundaries in mp;
+//   LD_SYNC stops with EV_MERGE (mj = index) when it reaches one of them;
+//   LD_EMIT writes tokens to tok[0..nt) and applies the output-space rules with
+//           the output position of the first token = out0.
+template <int MODE>
 __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t* __restrict__ W, uint32_t a,
                                                 uint32_t stop, uint32_t E, uint32_t& x, uint32_t& nt, uint32_t& nb,
-                                                uint32_t* __restrict__ tok, uint32_t out0, uint32_t isize) {
+                                                MergePts& mp, uint32_t& mj, uint32_t* __restrict__ tok,
+                                                uint32_t out0, uint32_t isize) {
+  constexpr bool EMIT = MODE == LD_EMIT;
   uint32_t wd = a >> 5;
   uint64_t buf = (((uint64_t)W[wd + 1] << 32) | W[wd]) >> (a & 31);
   uint32_t cnt = 64 - (a & 31);
   wd += 2;
   uint32_t nx = W[wd];
   uint32_t pos = a, ev = EV_STOP;
+  uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, fill = 0;  // EMIT: pending tokens
   nt = 0;
   nb = 0;
+  if (MODE == LD_SPEC) {
+    mp.p0 = mp.p1 = mp.p2 = mp.p3 = ~0u;
+    mp.b0 = mp.b1 = mp.b2 = mp.b3 = ~0u;
+  }
 #define LREFILL()                        \
   do {                                   \
     if (cnt <= 32) {                     \
@@ -452,6 +516,14 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
     pos += (n);      \
   } while (0)
   while (pos < stop) {
+    if (MODE == LD_SYNC) {
+      const bool h0 = pos == mp.p0, h1 = pos == mp.p1, h2 = pos == mp.p2, h3 = pos == mp.p3;
+      if (h0 | h1 | h2 | h3) {
+        mj = h0 ? 0u : h1 ? 1u : h2 ? 2u : 3u;
+        ev = EV_MERGE;
+        break;
+      }
+    }
     if (EMIT && out0 + nb >= isize) {
       ev = (out0 + nb == isize) ? EV_FULLX : EV_FULLO;
       break;
@@ -501,300 +573,558 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
         break;
       }
     }
-    if (EMIT) tok[nt] = t;
+    if (EMIT) {
+      q0 = fill == 0 ? t : q0;
+      q1 = fill == 1 ? t : q1;
+      q2 = fill == 2 ? t : q2;
+      q3 = t;
+      if (++fill == 4) {
+        *reinterpret_cast<Tok4*>(tok + nt - 3) = Tok4{q0, q1, q2, q3};
+        fill = 0;
+      }
+    }
     ++nt;
     nb += len;
+    if (MODE == LD_SPEC && (nt & (nt - 1)) == 0 && nt >= kMergeFirst && nt <= 8 * kMergeFirst) {
+      // boundaries after symbols F, 2F, 4F, 8F: the speculative walk has
+      // usually joined the true path by the later ones
+      mp.p0 = nt == kMergeFirst ? pos : mp.p0;
+      mp.b0 = nt == kMergeFirst ? nb : mp.b0;
+      mp.p1 = nt == 2 * kMergeFirst ? pos : mp.p1;
+      mp.b1 = nt == 2 * kMergeFirst ? nb : mp.b1;
+      mp.p2 = nt == 4 * kMergeFirst ? pos : mp.p2;
+      mp.b2 = nt == 4 * kMergeFirst ? nb : mp.b2;
+      mp.p3 = nt == 8 * kMergeFirst ? pos : mp.p3;
+      mp.b3 = nt == 8 * kMergeFirst ? nb : mp.b3;
+    }
   }
 #undef LREFILL
 #undef LCONSUME
+  if (EMIT && fill) {  // the 1..3 tokens not yet stored
+    uint32_t* p = tok + nt - fill;
+    p[0] = q0;
+    if (fill > 1) p[1] = q1;
+    if (fill > 2) p[2] = q2;
+  }
   x = pos;
   return ev;
 }
 
-__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v) {
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const uint32_t lane = lane_id();
-  uint32_t s = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t t = __shfl_up(s, d, 64);
-    if (lane >= (uint32_t)d) s += t;
+    const uint32_t t = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d) v += t;
   }
-  return s - v;
+  return v;
 }
 
-__global__ __launch_bounds__(64) void k_inflate_huff(const uint8_t* __restrict__ file,
-                                                     const BlockInfo* __restrict__ blocks, uint32_t b0,
-                                                     uint64_t chunk_ustart, uint32_t* __restrict__ tokens,
-                                                     HuffOut* __restrict__ hout) {
-  __shared__ __attribute__((aligned(16))) HuffLds L;
-  const uint32_t bi = b0 + blockIdx.x;
+// Workgroup-wide helpers for the phase-A workgroup (all threads call them in
+// uniform control flow; each ends with a barrier so `red` can be reused).
+__device__ __forceinline__ uint32_t wg_any(bool p, uint32_t* red) {
+  const uint32_t w = threadIdx.x >> 6;
+  const uint64_t b = __ballot(p);
+  if (lane_id() == 0) red[w] = b != 0;
+  __syncthreads();
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < kHuffWaves; ++i) r |= red[i];
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ uint32_t wg_min(uint32_t v, uint32_t* red) {
+  const uint32_t w = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v = min(v, (uint32_t)__shfl_xor(v, d, 64));
+  if (lane_id() == 0) red[w] = v;
+  __syncthreads();
+  uint32_t r = 0xffffffffu;
+#pragma unroll
+  for (int i = 0; i < kHuffWaves; ++i) r = min(r, red[i]);
+  __syncthreads();
+  return r;
+}
+// exclusive scans of (u, v) over the workgroup
+__device__ __forceinline__ void wg_excl_scan2(uint32_t u, uint32_t v, uint32_t* red, uint32_t& eu, uint32_t& ev) {
+  const uint32_t w = threadIdx.x >> 6;
+  const uint32_t iu = wave_incl_scan(u), iv = wave_incl_scan(v);
+  if (lane_id() == 63) {
+    red[w] = iu;
+    red[kHuffWaves + w] = iv;
+  }
+  __syncthreads();
+  uint32_t ou = 0, ov = 0;
+#pragma unroll
+  for (int i = 0; i < kHuffWaves; ++i) {
+    ou += (uint32_t)i < w ? red[i] : 0u;
+    ov += (uint32_t)i < w ? red[kHuffWaves + i] : 0u;
+  }
+  __syncthreads();
+  eu = ou + iu - u;
+  ev = ov + iv - v;
+}
+
+// Wave-uniform bit reader over a 16 B-aligned LDS image (block headers, code
+// lengths, lookahead).  Values are readfirstlane'd so the state stays in SGPRs.
+struct SReader {
+  const uint32_t* W;
+  uint64_t buf;
+  uint32_t cnt, wd;
+  __device__ __forceinline__ void seek(uint32_t p) {
+    wd = p >> 5;
+    buf = (((uint64_t)rfl(W[wd + 1]) << 32) | rfl(W[wd])) >> (p & 31);
+    cnt = 64 - (p & 31);
+    wd += 2;
+  }
+  __device__ __forceinline__ void fill() {
+    if (cnt <= 32) {
+      buf |= (uint64_t)rfl(W[wd]) << cnt;
+      cnt += 32;
+      ++wd;
+    }
+  }
+  __device__ __forceinline__ uint32_t pos() const { return 32u * wd - cnt; }
+  __device__ __forceinline__ void consume(uint32_t n) {
+    buf >>= n;
+    cnt -= n;
+  }
+};
+
+// Dynamic-Huffman block header after BTYPE: code-length code, code lengths,
+// litlen / distance tables (+ literal pairing).  Run by one wave.  Returns
+// DH_OK, DH_TRUNC (a field does not fit before bit E) or kErrIO
+// (DataFormatException: bad counts, over/under-subscribed codes, a repeat with
+// no previous length, no end-of-block code).
+enum : int { DH_OK = 0, DH_TRUNC = -1 };
+__device__ __forceinline__ int dyn_header(HuffLds& L, SReader& R, uint32_t E) {
   const uint32_t lane = lane_id();
+  R.fill();
+  if (R.pos() + 14 > E) return DH_TRUNC;
+  const uint32_t hlit = ((uint32_t)R.buf & 31) + 257;
+  const uint32_t hdist = ((uint32_t)(R.buf >> 5) & 31) + 1;
+  const uint32_t hclen = ((uint32_t)(R.buf >> 10) & 15) + 4;
+  R.consume(14);
+  if (hlit > 286 || hdist > 30) return kErrIO;
+  if (R.pos() + 3 * hclen > E) return DH_TRUNC;
+  if (lane < 20) L.cl_lens[lane] = 0;
+  wave_sync();
+  for (uint32_t i = 0; i < hclen; ++i) {
+    R.fill();
+    const uint32_t v = (uint32_t)R.buf & 7;
+    R.consume(3);
+    if (lane == 0) L.cl_lens[kClOrder[i]] = (uint8_t)v;
+  }
+  wave_sync();
+  if (rfl(build_table(L, L.cl_lens, 19, 7, 2, L.dist, L.cnt_dist, L.sort_dist, nullptr, 0))) return kErrIO;
+  const uint32_t ntot = hlit + hdist;
+  uint32_t i = 0, last = 0;
+  while (i < ntot) {
+    R.fill();
+    const uint32_t e = rfl(L.dist[(uint32_t)R.buf & 127]);
+    const uint32_t nbits = (e >> 16) & 31;
+    if (R.pos() + nbits > E) return DH_TRUNC;
+    const uint32_t sym = e & 0xffff;
+    uint32_t rep, val, xb = 0;
+    if (sym < 16) {
+      rep = 1;
+      val = sym;
+    } else if (sym == 16) {
+      xb = 2;
+      rep = 3 + ((uint32_t)(R.buf >> nbits) & 3);
+      val = last;
+    } else if (sym == 17) {
+      xb = 3;
+      rep = 3 + ((uint32_t)(R.buf >> nbits) & 7);
+      val = 0;
+    } else {
+      xb = 7;
+      rep = 11 + ((uint32_t)(R.buf >> nbits) & 127);
+      val = 0;
+    }
+    if (R.pos() + nbits + xb > E) return DH_TRUNC;
+    if (sym == 16 && i == 0) return kErrIO;  // repeat with no previous length
+    R.consume(nbits + xb);
+    if (i + rep > ntot) return kErrIO;
+    for (uint32_t j = lane; j < rep; j += 64) L.lens[i + j] = (uint8_t)val;
+    i += rep;
+    last = val;
+  }
+  wave_sync();
+  if (rfl(L.lens[256]) == 0) return kErrIO;
+  if (rfl(build_table(L, L.lens, (int)hlit, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit, L.litsub, kLitSubCap)) ||
+      rfl(build_table(L, L.lens + hlit, (int)hdist, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist, L.distsub,
+                      kDistSubCap)))
+    return kErrIO;
+  pair_literals(L);
+  return DH_OK;
+}
+
+// First DEFLATE block of every BGZF block: header + tables built ahead of the
+// decode kernel, one wave per block at high occupancy, so the serial header
+// work of one block overlaps the others instead of idling a decode workgroup.
+// status 0: tables[blockIdx.x] holds the table image and the symbols start at
+// bit B0; anything else (stored / fixed block, malformed or long header) is
+// left to k_inflate_huff's inline path, which owns the error semantics.
+constexpr uint32_t kTabStageBytes = 1024;
+__global__ __launch_bounds__(64) void k_huff_tables(const uint8_t* __restrict__ file,
+                                                    const BlockInfo* __restrict__ blocks, uint32_t b0,
+                                                    uint8_t* __restrict__ tables,
+                                                    HuffTableInfo* __restrict__ tinfo) {
+  __shared__ __attribute__((aligned(16))) HuffLds L;
+  __shared__ __attribute__((aligned(16))) uint4 s_in[kTabStageBytes / 16 + 1];
+  const uint32_t lane = lane_id();
+  const uint32_t bi = b0 + blockIdx.x;
+  const BlockInfo blk = blocks[bi];
+  HuffTableInfo ti{1u, 0u, 0u, 0u};
+  if (blk.isize != 0) {
+    const uint64_t sbyte = blk.coff + 18;
+    const uint64_t abase = sbyte & ~15ull;
+    const uint32_t nreal = min((uint32_t)((blk.coff + blk.csize - abase + 15) >> 4), kTabStageBytes / 16);
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(file + abase);
+    for (uint32_t i = lane; i <= nreal; i += 64) s_in[i] = src[i];  // +1 pad chunk (file is padded)
+    wave_sync();
+    SReader R;
+    R.W = reinterpret_cast<const uint32_t*>(s_in);
+    const uint32_t Ereal = 8u * ((uint32_t)(sbyte - abase) + (blk.csize - 26));
+    const uint32_t E = min(Ereal, 128u * nreal);
+    R.seek(8u * (uint32_t)(sbyte - abase));
+    R.fill();
+    if (R.pos() + 3 <= E && (((uint32_t)R.buf >> 1) & 3u) == 2u) {
+      const uint32_t fin = (uint32_t)R.buf & 1u;
+      R.consume(3);
+      if (dyn_header(L, R, E) == DH_OK) {
+        wave_sync();
+        uint4* __restrict__ dst = reinterpret_cast<uint4*>(tables + (uint64_t)blockIdx.x * kTableImage);
+        const uint4* img = reinterpret_cast<const uint4*>(&L);
+        for (uint32_t i = lane; i < kTableImage / 16; i += 64) dst[i] = img[i];
+        ti = HuffTableInfo{0u, R.pos(), fin, 0u};
+      }
+    }
+  }
+  if (lane == 0) tinfo[blockIdx.x] = ti;
+}
+
+// Control block: wave 0 -> workgroup (pass parameters) and back (results).
+struct HuffCtl {
+  uint32_t act;                 // kActDecode / kActDone
+  uint32_t B0, out0, tok0;      // all-lane pass: first symbol bit, output / token position
+  uint32_t fe, fx, ftok, fbytes, m3any;  // its result
+  uint32_t xx[kHuffWaves], xe[kHuffWaves];  // exit / event of each wave's last lane
+  uint32_t red[2 * kHuffWaves];
+};
+enum : uint32_t { kActDecode = 1, kActDone = 2 };
+constexpr uint32_t kHuffLdsBytes = (sizeof(HuffLds) + 15) & ~15u;
+constexpr uint32_t kHuffCtlBytes = (sizeof(HuffCtl) + 15) & ~15u;
+constexpr uint32_t kHuffStaticBytes = kHuffLdsBytes + kHuffCtlBytes;
+
+__global__ __launch_bounds__(kHuffThreads) void k_inflate_huff(const uint8_t* __restrict__ file,
+                                                               const BlockInfo* __restrict__ blocks, uint32_t b0,
+                                                               uint64_t chunk_ustart, uint32_t* __restrict__ tokens,
+                                                               HuffOut* __restrict__ hout,
+                                                               const uint8_t* __restrict__ tables,
+                                                               const HuffTableInfo* __restrict__ tinfo,
+                                                               uint64_t* __restrict__ prof) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  // optional per-block cycle profile (prof != nullptr; thread 0's clock):
+  // [0] staging [1] wave-0 headers/tables/lookahead [2] spec pass (to the first
+  // exchange) [3] sync [4] end scan [5] emit [6] result hand-back
+  // [7] of [1]: dynamic litlen/dist table builds + literal pairing
+  // [8] all-lane passes [9] sync iterations [10] total
+  uint64_t pacc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t pt = prof ? clock64() : 0, pt0 = pt;
+#define PROF_T(i)                           \
+  do {                                      \
+    if (prof && threadIdx.x == 0) {         \
+      const uint64_t n_ = clock64();        \
+      pacc[i] += n_ - pt;                   \
+      pt = n_;                              \
+    }                                       \
+  } while (0)
+  HuffLds& L = *reinterpret_cast<HuffLds*>(smem);
+  HuffCtl& C = *reinterpret_cast<HuffCtl*>(smem + kHuffLdsBytes);
+  uint4* s_in = reinterpret_cast<uint4*>(smem + kHuffStaticBytes);
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const uint32_t bi = b0 + blockIdx.x;
   const BlockInfo blk = blocks[bi];
   const uint32_t isize = blk.isize;
   if (isize == 0) {  // inflate(buf,off,0) returns 0 without reading: nothing to validate
-    if (lane == 0) { hout[bi].ntok = 0; hout[bi].status = kOk; }
+    if (tid == 0) { hout[bi].ntok = 0; hout[bi].status = kOk; }
     return;
   }
   uint32_t* tok_out = tokens + (blk.ustart - chunk_ustart);
   const uint64_t sbyte = blk.coff + 18;  // cdata start
   const uint64_t abase = sbyte & ~15ull;
-  const uint32_t* __restrict__ W = reinterpret_cast<const uint32_t*>(file + abase);
+  const HuffTableInfo ti = tinfo[blockIdx.x];
+  {  // stage the block (+16 B of zero-padded file) and its prebuilt tables in LDS
+    const uint32_t nq = (uint32_t)((blk.coff + blk.csize - abase + 15) >> 4) + 1;
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(file + abase);
+    for (uint32_t i = tid; i < nq; i += kHuffThreads) s_in[i] = src[i];
+    if (ti.status == 0) {
+      const uint4* __restrict__ tsrc = reinterpret_cast<const uint4*>(tables + (uint64_t)blockIdx.x * kTableImage);
+      uint4* tdst = reinterpret_cast<uint4*>(&L);
+      for (uint32_t i = tid; i < kTableImage / 16; i += kHuffThreads) tdst[i] = tsrc[i];
+    }
+  }
+  __syncthreads();
+  PROF_T(0);
+  const uint32_t* __restrict__ W = reinterpret_cast<const uint32_t*>(s_in);
   const uint32_t E = 8u * ((uint32_t)(sbyte - abase) + (blk.csize - 26));  // end of CDATA (bits from W)
 
-  // wave-uniform bit reader (block headers, code lengths, lookahead)
-  uint64_t sbuf;
-  uint32_t scnt, swd;
-#define SSEEK(p)                                                   \
-  do {                                                             \
-    const uint32_t p_ = (p);                                       \
-    swd = p_ >> 5;                                                 \
-    sbuf = (((uint64_t)rfl(W[swd + 1]) << 32) | rfl(W[swd])) >> (p_ & 31); \
-    scnt = 64 - (p_ & 31);                                         \
-    swd += 2;                                                      \
-  } while (0)
-#define SFILL()                                \
-  do {                                         \
-    if (scnt <= 32) {                          \
-      sbuf |= (uint64_t)rfl(W[swd]) << scnt;   \
-      scnt += 32;                              \
-      ++swd;                                   \
-    }                                          \
-  } while (0)
-#define SPOS() (32u * swd - scnt)
-#define SCONSUME(n) \
-  do {              \
-    sbuf >>= (n);   \
-    scnt -= (n);    \
-  } while (0)
+  SReader R;  // wave 0's reader
+  R.W = W;
+  R.buf = 0;
+  R.cnt = R.wd = 0;
 
-  SSEEK(8u * (uint32_t)(sbyte - abase));
   uint32_t outpos = 0, ntok = 0;
   int err = kOk;
-  bool look = false;  // output exactly full: zlib's lookahead
-  while (err == kOk) {
-    SFILL();
-    if (SPOS() + 3 > E) { if (!look) err = kErrFormat; break; }
-    const uint32_t hdr = (uint32_t)sbuf & 7;
-    SCONSUME(3);
-    const bool final_blk = hdr & 1;
-    const uint32_t type = hdr >> 1;
-    if (type == 0) {  // stored
-      SCONSUME((8u - (SPOS() & 7u)) & 7u);  // to the byte boundary
-      SFILL();
-      if (SPOS() + 32 > E) { if (!look) err = kErrFormat; break; }
-      const uint32_t len = (uint32_t)sbuf & 0xffff, nlen = (uint32_t)(sbuf >> 16) & 0xffff;
-      SCONSUME(32);
-      if (len != (~nlen & 0xffffu)) { err = kErrIO; break; }
-      const uint32_t p = SPOS();  // byte aligned
-      if (look) {
-        if (len != 0) break;  // COPY with no room: zlib stops here
-        if (final_blk) break;
-        continue;
-      }
-      const uint32_t n = min(min(len, isize - outpos), (E - p) >> 3);
-      const uint8_t* src = reinterpret_cast<const uint8_t*>(W) + (p >> 3);
-      for (uint32_t j = lane; j < n; j += 64) tok_out[ntok + j] = (1u << 24) | src[j];
-      ntok += n;
-      outpos += n;
-      SSEEK(p + 8 * n);
-      if (n < len) {
-        if (outpos < isize) err = kErrFormat;  // ran out of input
-        break;
-      }
-      if (final_blk) {
-        if (outpos < isize) err = kErrFormat;
-        break;
-      }
-      if (outpos == isize) look = true;
-      continue;
-    }
-    if (type == 3) { err = kErrIO; break; }
-    if (type == 1) {  // fixed Huffman
-      for (int s = lane; s < 320; s += 64) {
-        uint8_t l;
-        if (s < 144) l = 8; else if (s < 256) l = 9; else if (s < 280) l = 7; else if (s < 288) l = 8; else l = 5;
-        L.lens[s] = l;
-      }
-      __syncthreads();
-      if (rfl(build_table(L, L.lens, 288, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit, L.litsub, kLitSubBits,
-                          kLitSubMax)) ||
-          rfl(build_table(L, L.lens + 288, 32, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist, L.distsub,
-                          kDistSubBits, kDistSubMax))) {
-        err = kErrIO;
-        break;
-      }
-      pair_literals(L);
-    } else {  // dynamic Huffman
-      SFILL();
-      if (SPOS() + 14 > E) { if (!look) err = kErrFormat; break; }
-      const uint32_t hlit = ((uint32_t)sbuf & 31) + 257;
-      const uint32_t hdist = ((uint32_t)(sbuf >> 5) & 31) + 1;
-      const uint32_t hclen = ((uint32_t)(sbuf >> 10) & 15) + 4;
-      SCONSUME(14);
-      if (hlit > 286 || hdist > 30) { err = kErrIO; break; }
-      if (SPOS() + 3 * hclen > E) { if (!look) err = kErrFormat; break; }
-      if (lane < 20) L.cl_lens[lane] = 0;
-      __syncthreads();
-      for (uint32_t i = 0; i < hclen; ++i) {
-        SFILL();
-        const uint32_t v = (uint32_t)sbuf & 7;
-        SCONSUME(3);
-        if (lane == 0) L.cl_lens[kClOrder[i]] = (uint8_t)v;
-      }
-      __syncthreads();
-      if (rfl(build_table(L, L.cl_lens, 19, 7, 2, L.dist, L.cnt_dist, L.sort_dist, nullptr, 0, 0))) {
-        err = kErrIO;
-        break;
-      }
-      const uint32_t ntot = hlit + hdist;
-      uint32_t i = 0, last = 0;
-      bool stop = false;
-      while (i < ntot) {
-        SFILL();
-        const uint32_t e = rfl(L.dist[(uint32_t)sbuf & 127]);
-        const uint32_t nbits = (e >> 16) & 31;
-        if (SPOS() + nbits > E) { stop = true; break; }
-        const uint32_t sym = e & 0xffff;
-        uint32_t rep, val, xb = 0;
-        if (sym < 16) {
-          rep = 1;
-          val = sym;
-        } else if (sym == 16) {
-          xb = 2;
-          rep = 3 + ((uint32_t)(sbuf >> nbits) & 3);
-          val = last;
-        } else if (sym == 17) {
-          xb = 3;
-          rep = 3 + ((uint32_t)(sbuf >> nbits) & 7);
-          val = 0;
-        } else {
-          xb = 7;
-          rep = 11 + ((uint32_t)(sbuf >> nbits) & 127);
-          val = 0;
-        }
-        if (SPOS() + nbits + xb > E) { stop = true; break; }
-        if (sym == 16 && i == 0) { err = kErrIO; break; }  // repeat with no previous length
-        SCONSUME(nbits + xb);
-        if (i + rep > ntot) { err = kErrIO; break; }
-        for (uint32_t j = lane; j < rep; j += 64) L.lens[i + j] = (uint8_t)val;
-        i += rep;
-        last = val;
-      }
-      if (err != kOk) break;
-      if (stop) { if (!look) err = kErrFormat; break; }
-      __syncthreads();
-      if (rfl(L.lens[256]) == 0) { err = kErrIO; break; }
-      if (rfl(build_table(L, L.lens, (int)hlit, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit, L.litsub,
-                          kLitSubBits, kLitSubMax)) ||
-          rfl(build_table(L, L.lens + hlit, (int)hdist, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist,
-                          L.distsub, kDistSubBits, kDistSubMax))) {
-        err = kErrIO;
-        break;
-      }
-      pair_literals(L);
-    }
+  bool look = false;       // output exactly full: zlib's lookahead
+  bool final_blk = false;  // BFINAL of the current DEFLATE block
+  bool resume = false;     // an all-lane pass result waits in C
+  bool pre = ti.status == 0;  // first DEFLATE block's header + tables come from k_huff_tables
 
-    if (!look) {
-      // ---- all-lane decode of this block's symbols
-      const uint32_t B0 = SPOS();
-      const uint32_t R = E > B0 ? E - B0 : 0u;
-      const uint32_t S = (R + 63) >> 6;
-      uint32_t a = min(B0 + lane * S, E);
-      const uint32_t stop = lane == 63 ? E : min(B0 + (lane + 1) * S, E);
-      uint32_t x, nt, nb;
-      uint32_t ev = lane_decode<false>(L, W, a, stop, E, x, nt, nb, nullptr, 0, 0);
-      for (;;) {  // sync: restart each slice from its predecessor's exit
-        const uint32_t px = __shfl_up(x, 1, 64);
-        const uint32_t pev = __shfl_up(ev, 1, 64);
-        const bool need = lane > 0 && pev == EV_STOP && px != a;
-        if (__ballot(need) == 0) break;
-        if (need) {
-          a = px;
-          ev = lane_decode<false>(L, W, a, stop, E, x, nt, nb, nullptr, 0, 0);
-        }
-      }
-      const uint64_t evm = __ballot(ev != EV_STOP);
-      const uint32_t lend = evm ? (uint32_t)__ffsll((unsigned long long)evm) - 1 : 63u;
-      const bool valid = lane <= lend;
-      const uint32_t toff = wave_excl_sum(valid ? nt : 0u);
-      const uint32_t boff = wave_excl_sum(valid ? nb : 0u);
-      uint32_t x3 = a, nt3 = 0, nb3 = 0, ev3 = EV_STOP;
-      if (valid)
-        ev3 = lane_decode<true>(L, W, a, stop, E, x3, nt3, nb3, tok_out + ntok + toff, outpos + boff, isize);
-      const uint64_t m3 = __ballot(valid && ev3 != EV_STOP);
-      const uint32_t f = m3 ? (uint32_t)__ffsll((unsigned long long)m3) - 1 : lend;
-      const uint32_t fev = __shfl(ev3, f, 64);
-      const uint32_t ftok = __shfl(toff + nt3, f, 64);
-      const uint32_t fbytes = __shfl(boff + nb3, f, 64);
-      const uint32_t fx = __shfl(x3, f, 64);
-      ntok = rfl(ntok + ftok);
-      outpos = rfl(outpos + fbytes);
-      const uint32_t fe = rfl(fev), fxs = rfl(fx);
-      if (m3 == 0) {  // walked to the end of CDATA without an end-of-block
-        if (outpos < isize) err = kErrFormat;
-        else if (outpos == isize) { look = true; SSEEK(fxs); }
-        else break;
-        if (err != kOk || fxs >= E) break;
-      } else if (fe == EV_EOB) {
-        SSEEK(fxs);
-        if (final_blk) { err = kErrFormat; break; }  // EOB before ISIZE bytes
-        continue;
-      } else if (fe == EV_FULLX) {
-        look = true;
-        SSEEK(fxs);
-      } else if (fe == EV_FULLO) {
-        break;
-      } else {
-        err = fe == EV_ERR ? kErrIO : kErrFormat;
-        break;
-      }
-    }
-    // ---- lookahead (output exactly full): decode on until a symbol needs room
-    bool next_hdr = false;
+  // zlib's lookahead once the output is exactly full: decode on until a
+  // symbol needs room; returns true when it ends at a (non-final) EOB so the
+  // next block header must be examined too.
+  auto lookahead = [&]() -> bool {
     for (;;) {
-      SFILL();
-      const uint32_t p = SPOS();
-      const uint32_t e = lit_lookup<true>(L, sbuf);
+      R.fill();
+      const uint32_t p = R.pos();
+      const uint32_t e = lit_lookup<true>(L, R.buf);
       const uint32_t n1 = (e >> 16) & 31;
-      if (e < kKindLit) break;  // literal: no room (a pair's first code is checked by n1 >= its length)
+      if (e < kKindLit) return false;  // literal: no room (a pair's first code is checked by n1 >= its length)
       const uint32_t k = e >> 26;
       if (k == K_LEN) {
         const uint32_t ex = (e >> 9) & 15;
-        if (p + n1 + ex > E) break;
-        SCONSUME(n1 + ex);
-        SFILL();
-        const uint32_t d = dist_lookup<true>(L, sbuf);
+        if (p + n1 + ex > E) return false;
+        R.consume(n1 + ex);
+        R.fill();
+        const uint32_t d = dist_lookup<true>(L, R.buf);
         const uint32_t dn = (d >> 16) & 31;
         if (d >= kKindLit) {
-          if (SPOS() + max(dn, 1u) <= E) err = kErrIO;
-          break;
+          if (R.pos() + max(dn, 1u) <= E) err = kErrIO;
+          return false;
         }
         const uint32_t dx = (d >> 21) & 15;
-        if (SPOS() + dn + dx > E) break;
-        const uint32_t dist = (d & 0x7fff) + ((uint32_t)(sbuf >> dn) & ((1u << dx) - 1));
+        if (R.pos() + dn + dx > E) return false;
+        const uint32_t dist = (d & 0x7fff) + ((uint32_t)(R.buf >> dn) & ((1u << dx) - 1));
         if (dist > outpos) err = kErrIO;
-        break;
+        return false;
       }
       if (k == K_EOB) {
-        if (p + n1 > E) break;
-        SCONSUME(n1);
-        next_hdr = !final_blk;
-        break;
+        if (p + n1 > E) return false;
+        R.consume(n1);
+        return !final_blk;
       }
       if (p + max(n1, 1u) <= E) err = kErrIO;  // invalid literal/length code
-      break;
+      return false;
     }
-    if (!next_hdr) break;
+  };
+
+  if (wave == 0) R.seek(8u * (uint32_t)(sbyte - abase));
+  for (;;) {
+    if (wave == 0) {
+      uint32_t act = kActDone;
+      for (;;) {  // wave-uniform: advance to the next all-lane pass or to the end
+        bool do_look = false;
+        if (resume) {  // ---- result of the all-lane pass
+          resume = false;
+          const uint32_t fe = rfl(C.fe), fxs = rfl(C.fx), m3any = rfl(C.m3any);
+          ntok = rfl(ntok + C.ftok);
+          outpos = rfl(outpos + C.fbytes);
+          if (!m3any) {  // walked to the end of CDATA without an end-of-block
+            if (outpos < isize) err = kErrFormat;
+            else if (outpos == isize) { look = true; R.seek(fxs); }
+            else break;
+            if (err != kOk || fxs >= E) break;
+            do_look = true;
+          } else if (fe == EV_EOB) {
+            R.seek(fxs);
+            if (final_blk) { err = kErrFormat; break; }  // EOB before ISIZE bytes
+            continue;
+          } else if (fe == EV_FULLX) {
+            look = true;
+            R.seek(fxs);
+            do_look = true;
+          } else if (fe == EV_FULLO) {
+            break;
+          } else {
+            err = fe == EV_ERR ? kErrIO : kErrFormat;
+            break;
+          }
+        } else if (pre) {  // ---- first DEFLATE block: prebuilt tables already in LDS
+          pre = false;
+          final_blk = ti.final_blk != 0;
+          R.seek(ti.B0);
+          if (lane == 0) {
+            C.B0 = ti.B0;
+            C.out0 = 0;
+            C.tok0 = 0;
+          }
+          act = kActDecode;
+          resume = true;
+          break;
+        } else {  // ---- next DEFLATE block header
+          if (err != kOk) break;
+          R.fill();
+          if (R.pos() + 3 > E) { if (!look) err = kErrFormat; break; }
+          const uint32_t hdr = (uint32_t)R.buf & 7;
+          R.consume(3);
+          final_blk = hdr & 1;
+          const uint32_t type = hdr >> 1;
+          if (type == 0) {  // stored
+            R.consume((8u - (R.pos() & 7u)) & 7u);  // to the byte boundary
+            R.fill();
+            if (R.pos() + 32 > E) { if (!look) err = kErrFormat; break; }
+            const uint32_t len = (uint32_t)R.buf & 0xffff, nlen = (uint32_t)(R.buf >> 16) & 0xffff;
+            R.consume(32);
+            if (len != (~nlen & 0xffffu)) { err = kErrIO; break; }
+            const uint32_t p = R.pos();  // byte aligned
+            if (look) {
+              if (len != 0) break;  // COPY with no room: zlib stops here
+              if (final_blk) break;
+              continue;
+            }
+            const uint32_t n = min(min(len, isize - outpos), (E - p) >> 3);
+            const uint8_t* src = reinterpret_cast<const uint8_t*>(W) + (p >> 3);
+            for (uint32_t j = lane; j < n; j += 64) tok_out[ntok + j] = (1u << 24) | src[j];
+            ntok += n;
+            outpos += n;
+            R.seek(p + 8 * n);
+            if (n < len) {
+              if (outpos < isize) err = kErrFormat;  // ran out of input
+              break;
+            }
+            if (final_blk) {
+              if (outpos < isize) err = kErrFormat;
+              break;
+            }
+            if (outpos == isize) look = true;
+            continue;
+          }
+          if (type == 3) { err = kErrIO; break; }
+          if (type == 1) {  // fixed Huffman
+            for (int s = lane; s < 320; s += 64) {
+              uint8_t l;
+              if (s < 144) l = 8; else if (s < 256) l = 9; else if (s < 280) l = 7; else if (s < 288) l = 8; else l = 5;
+              L.lens[s] = l;
+            }
+            wave_sync();
+            if (rfl(build_table(L, L.lens, 288, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit, L.litsub, kLitSubCap)) ||
+                rfl(build_table(L, L.lens + 288, 32, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist, L.distsub,
+                                kDistSubCap))) {
+              err = kErrIO;
+              break;
+            }
+            pair_literals(L);
+          } else {  // dynamic Huffman
+            const uint64_t tb0 = prof ? clock64() : 0;
+            const int dh = dyn_header(L, R, E);
+            if (prof && threadIdx.x == 0) pacc[7] += clock64() - tb0;
+            if (dh == DH_TRUNC) { if (!look) err = kErrFormat; break; }
+            if (dh != DH_OK) { err = kErrIO; break; }
+          }
+          if (!look) {  // hand the symbol stream to the workgroup
+            if (lane == 0) {
+              C.B0 = R.pos();
+              C.out0 = outpos;
+              C.tok0 = ntok;
+            }
+            act = kActDecode;
+            resume = true;
+            break;
+          }
+          do_look = true;
+        }
+        if (do_look) {
+          if (!lookahead()) break;
+        }
+      }
+      if (lane == 0) C.act = act;
+    }
+    PROF_T(1);
+    __syncthreads();
+    if (C.act != kActDecode) break;
+    if (prof) pacc[8]++;
+
+    // ---- all-lane decode of this DEFLATE block's symbols
+    const uint32_t B0 = C.B0, out0 = C.out0, tok0 = C.tok0;
+    const uint32_t R = E > B0 ? E - B0 : 0u;
+    const uint32_t S = (R + kHuffThreads - 1) / kHuffThreads;
+    uint32_t a = min(B0 + tid * S, E);
+    const uint32_t stop = tid == kHuffThreads - 1 ? E : min(B0 + (tid + 1) * S, E);
+    MergePts mp;
+    uint32_t mj = 0, x, nt, nb;
+    uint32_t ev = lane_decode<LD_SPEC>(L, W, a, stop, E, x, nt, nb, mp, mj, nullptr, 0, 0);
+    const uint32_t sx = x, snt = nt, snb = nb, sev = ev;
+    bool first_x = true;
+    for (;;) {  // sync: restart each slice from its predecessor's exit
+      if (lane == 63) {
+        C.xx[wave] = x;
+        C.xe[wave] = ev;
+      }
+      __syncthreads();
+      if (first_x) PROF_T(2);
+      first_x = false;
+      if (prof) pacc[9]++;
+      uint32_t px = __shfl_up(x, 1, 64), pev = __shfl_up(ev, 1, 64);
+      if (lane == 0 && wave > 0) {
+        px = C.xx[wave - 1];
+        pev = C.xe[wave - 1];
+      }
+      const bool need = tid > 0 && pev == EV_STOP && px != a;
+      if (!wg_any(need, C.red)) break;
+      if (need) {
+        a = px;
+        uint32_t rx, rnt, rnb;
+        const uint32_t rev = lane_decode<LD_SYNC>(L, W, a, stop, E, rx, rnt, rnb, mp, mj, nullptr, 0, 0);
+        if (rev == EV_MERGE) {  // shares the speculative walk from boundary mj on
+          const uint32_t bj = mj == 0 ? mp.b0 : mj == 1 ? mp.b1 : mj == 2 ? mp.b2 : mp.b3;
+          x = sx;
+          ev = sev;
+          nt = rnt + snt - (kMergeFirst << mj);
+          nb = rnb + snb - bj;
+        } else {
+          x = rx;
+          ev = rev;
+          nt = rnt;
+          nb = rnb;
+        }
+      }
+    }
+    PROF_T(3);
+    const uint32_t lend0 = wg_min(ev != EV_STOP ? tid : 0xffffffffu, C.red);
+    const uint32_t lend = lend0 == 0xffffffffu ? (uint32_t)kHuffThreads - 1 : lend0;
+    const bool valid = tid <= lend;
+    uint32_t toff, boff;
+    wg_excl_scan2(valid ? nt : 0u, valid ? nb : 0u, C.red, toff, boff);
+    PROF_T(4);
+    uint32_t x3 = a, nt3 = 0, nb3 = 0, ev3 = EV_STOP;
+    if (valid)
+      ev3 = lane_decode<LD_EMIT>(L, W, a, stop, E, x3, nt3, nb3, mp, mj, tok_out + tok0 + toff, out0 + boff, isize);
+    const uint32_t m3 = wg_min((valid && ev3 != EV_STOP) ? tid : 0xffffffffu, C.red);
+    PROF_T(5);
+    const uint32_t f = m3 != 0xffffffffu ? m3 : lend;
+    if (tid == f) {
+      C.fe = ev3;
+      C.fx = x3;
+      C.ftok = toff + nt3;
+      C.fbytes = boff + nb3;
+      C.m3any = m3 != 0xffffffffu;
+    }
+    __syncthreads();
+    PROF_T(6);
   }
-  if (err == kOk && outpos < isize) err = kErrFormat;  // "Did not inflate expected amount"
-  if (lane == 0) {
+  if (tid == 0) {
+    if (err == kOk && outpos < isize) err = kErrFormat;  // "Did not inflate expected amount"
     hout[bi].ntok = ntok;
     hout[bi].status = err;
+    if (prof) {
+      pacc[10] = clock64() - pt0;
+      for (int i = 0; i < 11; ++i) prof[16ull * bi + i] = pacc[i];
+    }
   }
-#undef SSEEK
-#undef SFILL
-#undef SPOS
-#undef SCONSUME
+#undef PROF_T
 }
 
 // ---------------------------------------------------------------------------
@@ -814,16 +1144,6 @@ constexpr int kLzThreads = 1024;
 constexpr int kLzWaves = kLzThreads / 64;
 constexpr uint32_t kMapMax = 65280;
 constexpr uint32_t kLitTag = 0xFF00u;
-
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-  const uint32_t lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t t = __shfl_up(v, d, 64);
-    if (lane >= (uint32_t)d) v += t;
-  }
-  return v;
-}
 
 // exclusive scan over the workgroup; returns the prefix, *total = sum
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
@@ -1439,20 +1759,41 @@ hipError_t scan_u32_to_u64(void* tmp, size_t* tmp_bytes, const uint32_t* in, uin
   return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, in, out, (int)n, s);
 }
 
+uint64_t* g_huff_prof = nullptr;  // HBAM_HUFF_PROF: per-block cycle profile (hbam_pipeline.cpp)
+
+// max_stage = largest staged span of the chunk's blocks (huff_stage_bytes)
+static hipError_t launch_huff(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
+                              uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
+                              uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s) {
+  hipLaunchKernelGGL(k_huff_tables, dim3(nb), dim3(64), 0, s, file, blocks, b0, tables, tinfo);
+  hipError_t e0 = hipGetLastError();
+  if (e0 != hipSuccess) return e0;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_inflate_huff),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const uint32_t lds = kHuffStaticBytes + ((max_stage + 15) & ~15u);
+  hipLaunchKernelGGL(k_inflate_huff, dim3(nb), dim3(kHuffThreads), lds, s, file, blocks, b0, chunk_ustart, tokens,
+                     hout, tables, tinfo, g_huff_prof);
+  return hipGetLastError();
+}
 hipError_t launch_inflate(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                          uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint8_t* u, hipStream_t s) {
+                          uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint8_t* u, uint32_t max_stage,
+                          uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s) {
   if (nb == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_inflate_huff, dim3(nb), dim3(64), 0, s, file, blocks, b0, chunk_ustart, tokens, hout);
-  hipError_t e = hipGetLastError();
+  hipError_t e = launch_huff(file, blocks, b0, nb, chunk_ustart, tokens, hout, max_stage, tables, tinfo, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_inflate_lz77, dim3(nb), dim3(kLzThreads), 0, s, blocks, b0, chunk_ustart, tokens, hout, u);
   return hipGetLastError();
 }
 hipError_t launch_inflate_huff(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                               uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, hipStream_t s) {
+                               uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
+                               uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s) {
   if (nb == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_inflate_huff, dim3(nb), dim3(64), 0, s, file, blocks, b0, chunk_ustart, tokens, hout);
-  return hipGetLastError();
+  return launch_huff(file, blocks, b0, nb, chunk_ustart, tokens, hout, max_stage, tables, tinfo, s);
 }
 hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb, uint64_t chunk_ustart,
                                const uint32_t* tokens, const HuffOut* hout, uint8_t* u, hipStream_t s) {
@@ -1542,3 +1883,16 @@ hipError_t launch_sbi_emit(const uint64_t* voff, uint64_t n, uint32_t g, uint64_
 }
 
 }  // namespace hbam
+#ifdef HBAM_PROBE
+namespace hbam {
+__global__ void k_probe_spec(const uint32_t* W, uint32_t a, uint32_t stop, uint32_t E, uint32_t* out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  HuffLds& L = *reinterpret_cast<HuffLds*>(smem);
+  W = reinterpret_cast<const uint32_t*>(smem + sizeof(HuffLds));
+  MergePts mp;
+  uint32_t mj = 0, x, nt, nb;
+  uint32_t ev = lane_decode<LD_SPEC>(L, W, a + threadIdx.x, stop, E, x, nt, nb, mp, mj, nullptr, 0, 0);
+  out[threadIdx.x] = ev + x + nt + nb + mp.p0 + mp.p3;
+}
+}
+#endif

@@ -41,9 +41,19 @@ hipError_t sort_u64(void* tmp, size_t* tmp_bytes, uint64_t* keys_in, uint64_t* k
 hipError_t scan_u32_to_u64(void* tmp, size_t* tmp_bytes, const uint32_t* in, uint64_t* out, uint32_t n,
                            hipStream_t s);
 hipError_t launch_inflate(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                          uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint8_t* u, hipStream_t s);
+                          uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint8_t* u, uint32_t max_stage,
+                          uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s);
 hipError_t launch_inflate_huff(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                               uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, hipStream_t s);
+                               uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
+                               uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s);
+// HBAM_HUFF_PROF profile buffer (16 u64 per block) or nullptr
+extern uint64_t* g_huff_prof;
+// LDS bytes phase A stages for a block: its cdata from the 16 B-aligned start,
+// footer included, plus one 16 B pad (must match k_inflate_huff).
+inline uint32_t huff_stage_bytes(const BlockInfo& b) {
+  const uint64_t abase = (b.coff + 18) & ~15ull;
+  return (uint32_t)(((b.coff + b.csize - abase + 15) >> 4) + 1) * 16u;
+}
 hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb, uint64_t chunk_ustart,
                                const uint32_t* tokens, const HuffOut* hout, uint8_t* u, hipStream_t s);
 // stage: 0 guess, 1 serial link, 2 count, 3 emit, 4 parallel link (base = in[] scratch)

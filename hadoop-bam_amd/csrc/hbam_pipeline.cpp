@@ -2,6 +2,8 @@
 #include "hbam_pipeline.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "hbam_launch.h"
@@ -161,6 +163,15 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force) {
   const uint8_t* fbase = dfile_ - base_;
   if (timing) HIPCHK(hipEventRecord(ev_[2], stream_));
   float huff_ms = 0, lz_ms = 0;
+  // HBAM_HUFF_PROF=1: phase-A per-block cycle profile of large inflates (stderr)
+  static const bool prof_on = getenv("HBAM_HUFF_PROF") != nullptr;
+  DevBuf<uint64_t> prof;
+  const bool prof_this = prof_on && b1 - b0 >= 1024;
+  if (prof_this) {
+    HIPCHK(prof.reserve(16ull * nblk));
+    HIPCHK(hipMemsetAsync(prof.p, 0, 16ull * nblk * 8, stream_));
+    g_huff_prof = prof.p;
+  }
   uint32_t b = b0;
   bool any = false;
   while (b < b1) {
@@ -174,9 +185,14 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force) {
     const uint64_t cu = hblocks_[b].ustart;
     const uint64_t uend = hblocks_[e - 1].ustart + hblocks_[e - 1].isize;
     HIPCHK(tokens_.reserve(std::max<uint64_t>(uend - cu, 64)));
+    uint32_t max_stage = 0;
+    for (uint32_t k = b; k < e; ++k) max_stage = std::max(max_stage, huff_stage_bytes(hblocks_[k]));
+    HIPCHK(tables_.reserve((uint64_t)(e - b) * kHuffTableImage));
+    HIPCHK(tinfo_.reserve(e - b));
     if (timing) {
       HIPCHK(hipEventRecord(ev_[4], stream_));
-      HIPCHK(launch_inflate_huff(fbase, dblocks_.p, b, e - b, cu, tokens_.p, hout_.p, stream_));
+      HIPCHK(launch_inflate_huff(fbase, dblocks_.p, b, e - b, cu, tokens_.p, hout_.p, max_stage, tables_.p,
+                                 tinfo_.p, stream_));
       HIPCHK(hipEventRecord(ev_[5], stream_));
       HIPCHK(launch_inflate_lz77(dblocks_.p, b, e - b, cu, tokens_.p, hout_.p, du_.p, stream_));
       HIPCHK(hipEventRecord(ev_[6], stream_));
@@ -187,12 +203,31 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force) {
       huff_ms += a;
       lz_ms += c;
     } else {
-      HIPCHK(launch_inflate(fbase, dblocks_.p, b, e - b, cu, tokens_.p, hout_.p, du_.p, stream_));
+      HIPCHK(launch_inflate(fbase, dblocks_.p, b, e - b, cu, tokens_.p, hout_.p, du_.p, max_stage, tables_.p,
+                            tinfo_.p, stream_));
     }
     for (uint32_t k = b; k < e; ++k) inflated_[k] = 1;
     ++inflate_launches_;
     any = true;
     b = e;
+  }
+  g_huff_prof = nullptr;
+  if (prof_this && any) {
+    std::vector<uint64_t> h(16ull * nblk);
+    HIPCHK(hipMemcpy(h.data(), prof.p, h.size() * 8, hipMemcpyDeviceToHost));
+    double acc[11] = {0};
+    uint64_t n = 0;
+    for (uint32_t k = b0; k < b1; ++k) {
+      if (h[16ull * k + 10] == 0) continue;
+      ++n;
+      for (int i = 0; i < 11; ++i) acc[i] += (double)h[16ull * k + i];
+    }
+    static const char* names[11] = {"stage", "wave0_hdr", "spec", "sync", "scan", "emit", "handback", "tables",
+                                     "passes", "sync_iters", "total"};
+    fprintf(stderr, "[huff prof] %llu blocks, mean cycles per block:", (unsigned long long)n);
+    for (int i = 0; i < 11; ++i)
+      fprintf(stderr, " %s=%.0f", names[i], n ? acc[i] / n : 0.0);
+    fprintf(stderr, "\n");
   }
   if (!any) {
     times.inflate = times.huff = times.lz77 = 0;

@@ -129,6 +129,8 @@ class Pipeline {
   std::vector<uint8_t> inflated_;  // per block flag
   DevBuf<uint32_t> tokens_;
   DevBuf<HuffOut> hout_;
+  DevBuf<uint8_t> tables_;        // phase-A prebuilt table images (per chunk)
+  DevBuf<HuffTableInfo> tinfo_;
 
   // span scratch
   DevBuf<uint64_t> g_, x_, x2_, entry_, base_arr_, summary_, dead_;
