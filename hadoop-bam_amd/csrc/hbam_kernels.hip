@@ -487,11 +487,17 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
                                                 MergePts& mp, uint32_t& mj, uint32_t* __restrict__ tok,
                                                 uint32_t out0, uint32_t isize) {
   constexpr bool EMIT = MODE == LD_EMIT;
-  uint32_t wd = a >> 5;
-  uint64_t buf = (((uint64_t)W[wd + 1] << 32) | W[wd]) >> (a & 31);
-  uint32_t cnt = 64 - (a & 31);
-  wd += 2;
-  uint32_t nx = W[wd];
+  uint32_t wd, cnt, nx;
+  uint64_t buf;
+#define LSEEK(p)                                                    \
+  do {                                                              \
+    wd = (p) >> 5;                                                  \
+    buf = (((uint64_t)W[wd + 1] << 32) | W[wd]) >> ((p) & 31);      \
+    cnt = 64 - ((p) & 31);                                          \
+    wd += 2;                                                        \
+    nx = W[wd];                                                     \
+  } while (0)
+  LSEEK(a);
   uint32_t pos = a, ev = EV_STOP;
   uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, fill = 0;  // EMIT: pending tokens
   nt = 0;
@@ -515,7 +521,86 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
     cnt -= (n);      \
     pos += (n);      \
   } while (0)
-  while (pos < stop) {
+#define LCOMMIT(t_, len_)                                                                   \
+  do {                                                                                      \
+    if (EMIT) {                                                                             \
+      q0 = fill == 0 ? (t_) : q0;                                                           \
+      q1 = fill == 1 ? (t_) : q1;                                                           \
+      q2 = fill == 2 ? (t_) : q2;                                                           \
+      q3 = (t_);                                                                            \
+      if (++fill == 4) {                                                                    \
+        *reinterpret_cast<Tok4*>(tok + nt - 3) = Tok4{q0, q1, q2, q3};                      \
+        fill = 0;                                                                           \
+      }                                                                                     \
+    }                                                                                       \
+    ++nt;                                                                                   \
+    nb += (len_);                                                                           \
+    if (MODE == LD_SPEC && (nt & (nt - 1)) == 0 && nt >= kMergeFirst && nt <= 8 * kMergeFirst) { \
+      /* boundaries after symbols F, 2F, 4F, 8F: the speculative walk has */                \
+      /* usually joined the true path by the later ones */                                  \
+      mp.p0 = nt == kMergeFirst ? pos : mp.p0;                                              \
+      mp.b0 = nt == kMergeFirst ? nb : mp.b0;                                               \
+      mp.p1 = nt == 2 * kMergeFirst ? pos : mp.p1;                                          \
+      mp.b1 = nt == 2 * kMergeFirst ? nb : mp.b1;                                           \
+      mp.p2 = nt == 4 * kMergeFirst ? pos : mp.p2;                                          \
+      mp.b2 = nt == 4 * kMergeFirst ? nb : mp.b2;                                           \
+      mp.p3 = nt == 8 * kMergeFirst ? pos : mp.p3;                                          \
+      mp.b3 = nt == 8 * kMergeFirst ? nb : mp.b3;                                           \
+    }                                                                                       \
+  } while (0)
+  // Fast path: while a whole symbol (<= 15+5+15+13 = 48 bits) fits before E,
+  // no CDATA-end checks are needed; literal and length/distance symbols are
+  // decoded with selects instead of divergent branches (the wave mixes both in
+  // nearly every step).  End-of-block, invalid codes and (EMIT) distances
+  // beyond the output leave it; the slow path below re-decodes that symbol
+  // from `pos` with every zlib check.
+  const uint32_t fast_end = E >= 48 ? min(stop, E - 47) : 0u;
+  for (;;) {
+    bool merged = false;
+    while (pos < fast_end && (!EMIT || out0 + nb < isize)) {
+      if (MODE == LD_SYNC) {
+        const bool h0 = pos == mp.p0, h1 = pos == mp.p1, h2 = pos == mp.p2, h3 = pos == mp.p3;
+        if (h0 | h1 | h2 | h3) {
+          mj = h0 ? 0u : h1 ? 1u : h2 ? 2u : 3u;
+          merged = true;
+          break;
+        }
+      }
+      LREFILL();
+      uint32_t e = L.lit[(uint32_t)buf & ((1u << kLitRoot) - 1)];
+      if ((e >> 26) == K_LONG)
+        e = L.litsub[(e & 0xffffu) + ((uint32_t)(buf >> kLitRoot) & ((1u << ((e >> 16) & 15u)) - 1))];
+      const uint32_t kind = e >> 26;
+      if (kind > K_LEN) break;  // EOB, invalid or canonical-decode entry
+      const uint32_t n1 = (e >> 16) & 31;
+      const bool isl = kind == K_LEN;
+      const uint32_t ex = isl ? (e >> 9) & 15 : 0u;
+      const uint32_t len = isl ? (e & 511) + ((uint32_t)(buf >> n1) & ((1u << ex) - 1)) : (e >> 24);
+      const uint32_t c1 = n1 + ex;
+      buf >>= c1;
+      cnt -= c1;
+      LREFILL();
+      uint32_t d = L.dist[(uint32_t)buf & ((1u << kDistRoot) - 1)];
+      if ((d >> 26) == K_LONG)
+        d = L.distsub[(d & 0xffffu) + ((uint32_t)(buf >> kDistRoot) & ((1u << ((d >> 16) & 15u)) - 1))];
+      if (isl && d >= kKindLit) break;  // invalid distance code
+      const uint32_t dn = (d >> 16) & 31, dx = (d >> 21) & 15;
+      const uint32_t dist = (d & 0x7fff) + ((uint32_t)(buf >> dn) & ((1u << dx) - 1));
+      if (EMIT && isl && dist > out0 + nb) break;  // too far back: the slow path reports it
+      const uint32_t c2 = isl ? dn + dx : 0u;
+      buf >>= c2;
+      cnt -= c2;
+      pos += c1 + c2;
+      const uint32_t t = isl ? (0x80000000u | ((dist - 1) << 16) | len) : (e & 0x0300ffffu);
+      LCOMMIT(t, len);
+    }
+    if (MODE == LD_SYNC && merged) {
+      ev = EV_MERGE;
+      break;
+    }
+    // ---- slow path: one symbol with every check (or the end of the slice)
+    if (pos >= stop) break;
+    LSEEK(pos);
     if (MODE == LD_SYNC) {
       const bool h0 = pos == mp.p0, h1 = pos == mp.p1, h2 = pos == mp.p2, h3 = pos == mp.p3;
       if (h0 | h1 | h2 | h3) {
@@ -573,33 +658,12 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
         break;
       }
     }
-    if (EMIT) {
-      q0 = fill == 0 ? t : q0;
-      q1 = fill == 1 ? t : q1;
-      q2 = fill == 2 ? t : q2;
-      q3 = t;
-      if (++fill == 4) {
-        *reinterpret_cast<Tok4*>(tok + nt - 3) = Tok4{q0, q1, q2, q3};
-        fill = 0;
-      }
-    }
-    ++nt;
-    nb += len;
-    if (MODE == LD_SPEC && (nt & (nt - 1)) == 0 && nt >= kMergeFirst && nt <= 8 * kMergeFirst) {
-      // boundaries after symbols F, 2F, 4F, 8F: the speculative walk has
-      // usually joined the true path by the later ones
-      mp.p0 = nt == kMergeFirst ? pos : mp.p0;
-      mp.b0 = nt == kMergeFirst ? nb : mp.b0;
-      mp.p1 = nt == 2 * kMergeFirst ? pos : mp.p1;
-      mp.b1 = nt == 2 * kMergeFirst ? nb : mp.b1;
-      mp.p2 = nt == 4 * kMergeFirst ? pos : mp.p2;
-      mp.b2 = nt == 4 * kMergeFirst ? nb : mp.b2;
-      mp.p3 = nt == 8 * kMergeFirst ? pos : mp.p3;
-      mp.b3 = nt == 8 * kMergeFirst ? nb : mp.b3;
-    }
+    LCOMMIT(t, len);
   }
+#undef LSEEK
 #undef LREFILL
 #undef LCONSUME
+#undef LCOMMIT
   if (EMIT && fill) {  // the 1..3 tokens not yet stored
     uint32_t* p = tok + nt - fill;
     p[0] = q0;
@@ -818,7 +882,10 @@ constexpr uint32_t kHuffLdsBytes = (sizeof(HuffLds) + 15) & ~15u;
 constexpr uint32_t kHuffCtlBytes = (sizeof(HuffCtl) + 15) & ~15u;
 constexpr uint32_t kHuffStaticBytes = kHuffLdsBytes + kHuffCtlBytes;
 
-__global__ __launch_bounds__(kHuffThreads) void k_inflate_huff(const uint8_t* __restrict__ file,
+#ifndef HBAM_HUFF_WPE
+#define HBAM_HUFF_WPE 5  // waves per SIMD (VGPR cap 96; measured best on C2)
+#endif
+__global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(const uint8_t* __restrict__ file,
                                                                const BlockInfo* __restrict__ blocks, uint32_t b0,
                                                                uint64_t chunk_ustart, uint32_t* __restrict__ tokens,
                                                                HuffOut* __restrict__ hout,
