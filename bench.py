@@ -171,6 +171,7 @@ def main():
                    "parallelism": f"bgzf-shard x{world}"},
         "records_per_s": round(n_all * args.steps / elapsed, 1),
         "link_fallbacks": int(sum(s_["link_fallbacks"] for s_ in stats)),
+        "link_rewalks": int(sum(s_["link_rewalks"] for s_ in stats)),
         "stages_ms": {k: round(st[k], 3) for k in ("ms_locate", "ms_inflate", "ms_huff", "ms_lz77", "ms_chain",
                                                     "ms_decode", "ms_total")},
         "roofline": {"bound": "hbm", "kernel": "k_inflate_huff+k_inflate_lz77 (one launch pair)",

@@ -321,7 +321,7 @@ int hbam_gpu_run(hbam_gpu* g, int32_t flags, hbam_gpu_stats* st) {
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   (void)hipEventRecord(e0, p.stream());
-  const uint64_t lf0 = p.link_fallbacks(), il0 = p.inflate_launches();
+  const uint64_t lf0 = p.link_fallbacks(), il0 = p.inflate_launches(), lr0 = p.link_rewalks();
   int rc = p.locate();
   if (rc == HBAM_OK) rc = p.inflate(0, (uint32_t)p.blocks().size(), true);
   float ms_inflate = p.times.inflate, ms_huff = p.times.huff, ms_lz = p.times.lz77;
@@ -345,6 +345,7 @@ int hbam_gpu_run(hbam_gpu* g, int32_t flags, hbam_gpu_stats* st) {
   st->status = g->span.status;
   st->link_fallbacks = (int32_t)(p.link_fallbacks() - lf0);
   st->inflate_launches = (int32_t)(p.inflate_launches() - il0);
+  st->link_rewalks = (int32_t)(p.link_rewalks() - lr0);
   if (p.timing) {
     st->ms_locate = p.times.locate;
     st->ms_inflate = ms_inflate;

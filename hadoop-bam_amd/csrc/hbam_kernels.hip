@@ -1713,44 +1713,342 @@ __device__ uint64_t murmur3_dev(const uint8_t* u, uint64_t off, uint32_t len, in
   return h1;
 }
 
+// Fields + key of the record at q into slot i of the columns.
+__device__ __forceinline__ void decode_record(const uint8_t* __restrict__ u, uint64_t q, uint64_t i,
+                                              const Columns& col) {
+  const int32_t bs = (int32_t)ldu32(u, q);
+  const int32_t ref = (int32_t)ldu32(u, q + 4);
+  const int32_t pos = (int32_t)ldu32(u, q + 8);
+  const uint32_t w12 = ldu32(u, q + 12);
+  const uint32_t w16 = ldu32(u, q + 16);
+  const int32_t lseq = (int32_t)ldu32(u, q + 20);
+  const int32_t nref = (int32_t)ldu32(u, q + 24);
+  const int32_t npos = (int32_t)ldu32(u, q + 28);
+  const int32_t tlen = (int32_t)ldu32(u, q + 32);
+  const uint16_t flag = (uint16_t)(w16 >> 16);
+  col.ref_id[i] = ref;
+  col.pos[i] = pos;
+  col.l_read_name[i] = (uint8_t)w12;
+  col.mapq[i] = (uint8_t)(w12 >> 8);
+  col.bin[i] = (uint16_t)(w12 >> 16);
+  col.n_cigar[i] = (uint16_t)w16;
+  col.flag[i] = flag;
+  col.l_seq[i] = lseq;
+  col.next_ref_id[i] = nref;
+  col.next_pos[i] = npos;
+  col.tlen[i] = tlen;
+  col.rest_off[i] = q + 36;
+  col.rest_len[i] = (uint32_t)(bs - 32);
+  // BAMRecordReader.getKey (:81-121): alignmentStart = pos+1
+  const int32_t start = (int32_t)((uint32_t)pos + 1u);
+  int64_t key;
+  if (!((flag & 4) || ref < 0 || start < 0)) {
+    key = (int64_t)(((uint64_t)(int64_t)ref << 32) | (uint64_t)(int64_t)(int32_t)(start - 1));
+  } else {
+    const int32_t h = (int32_t)murmur3_dev(u, q + 36, (uint32_t)(bs - 32), 0);
+    key = (int64_t)((0x7fffffffull << 32) | (uint64_t)(int64_t)h);
+  }
+  col.key[i] = key;
+}
+
 __global__ void k_rec_decode(const uint8_t* __restrict__ u, const uint64_t* __restrict__ rec_pos, uint64_t n,
                              Columns col) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t q = rec_pos[i];
-    const int32_t bs = (int32_t)ldu32(u, q);
-    const int32_t ref = (int32_t)ldu32(u, q + 4);
-    const int32_t pos = (int32_t)ldu32(u, q + 8);
-    const uint32_t w12 = ldu32(u, q + 12);
-    const uint32_t w16 = ldu32(u, q + 16);
-    const int32_t lseq = (int32_t)ldu32(u, q + 20);
-    const int32_t nref = (int32_t)ldu32(u, q + 24);
-    const int32_t npos = (int32_t)ldu32(u, q + 28);
-    const int32_t tlen = (int32_t)ldu32(u, q + 32);
-    const uint16_t flag = (uint16_t)(w16 >> 16);
-    col.ref_id[i] = ref;
-    col.pos[i] = pos;
-    col.l_read_name[i] = (uint8_t)w12;
-    col.mapq[i] = (uint8_t)(w12 >> 8);
-    col.bin[i] = (uint16_t)(w12 >> 16);
-    col.n_cigar[i] = (uint16_t)w16;
-    col.flag[i] = flag;
-    col.l_seq[i] = lseq;
-    col.next_ref_id[i] = nref;
-    col.next_pos[i] = npos;
-    col.tlen[i] = tlen;
-    col.rest_off[i] = q + 36;
-    col.rest_len[i] = (uint32_t)(bs - 32);
-    // BAMRecordReader.getKey (:81-121): alignmentStart = pos+1
-    const int32_t start = (int32_t)((uint32_t)pos + 1u);
-    int64_t key;
-    if (!((flag & 4) || ref < 0 || start < 0)) {
-      key = (int64_t)(((uint64_t)(int64_t)ref << 32) | (uint64_t)(int64_t)(int32_t)(start - 1));
-    } else {
-      const int32_t h = (int32_t)murmur3_dev(u, q + 36, (uint32_t)(bs - 32), 0);
-      key = (int64_t)((0x7fffffffull << 32) | (uint64_t)(int64_t)h);
+       i += (uint64_t)gridDim.x * blockDim.x)
+    decode_record(u, rec_pos[i], i, col);
+}
+
+// ---------------------------------------------------------------------------
+// Record chain v2: lane-per-block walks with per-block record lists
+// ---------------------------------------------------------------------------
+//   k_rec_cand     one wave per block: first plausible record start (64
+//                  positions per step) -- where the block's guess walk begins.
+//   k_rec_walk     one lane per block: the chain from that candidate (next
+//                  candidates on failure), from the span start, or from a
+//                  forced (true) entry; every record start of the block is
+//                  listed as a u16 offset.  All walks of a span are in flight
+//                  at once, so the span costs one dependent-load chain of
+//                  ~records-per-block steps instead of a wave per block.
+//   k_rec_linkfix  max-scan link check; blocks whose list is off the chain are
+//                  re-walked from their true entry (usually zero or a few).
+//   k_rec_check    one wave per block: the reader / indexer rules of
+//                  k_rec_count for every listed record at once; the first stop
+//                  gives count, status and the bytes still to inflate.
+//   k_rec_out      one wave per block: positions, voffs and (reader) the fused
+//                  decode + key at the block's scanned base.
+template <int MODE>
+__global__ __launch_bounds__(64) void k_rec_cand(ChainEnv E, uint64_t* __restrict__ cand) {
+  const uint32_t k = E.k0 + blockIdx.x;
+  const BlockInfo b = E.blocks[k];
+  const uint64_t bend = b.ustart + b.isize;
+  const uint32_t lane = lane_id();
+  uint64_t c = kNone;
+  if (bend > E.p0 && b.ustart > E.p0 && b.ustart < E.q_end && b.isize > 0) {
+    for (uint64_t c0 = b.ustart; c0 < bend; c0 += 64) {
+      const uint64_t p = c0 + lane;
+      const uint64_t m = __ballot(p < bend && plausible(E, p));
+      if (m) {
+        c = c0 + (uint64_t)(__ffsll((long long)m) - 1);
+        break;
+      }
     }
-    col.key[i] = key;
+  }
+  if (lane == 0) cand[blockIdx.x] = c;
+}
+
+constexpr int kGuessLookahead = 4;  // plausible records required past a guess walk's exit
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_rec_walk(ChainEnv E, const uint64_t* __restrict__ cand,
+                                                  const uint64_t* __restrict__ force, uint64_t* __restrict__ g_out,
+                                                  uint64_t* __restrict__ x_out, uint32_t* __restrict__ wcnt,
+                                                  uint16_t* __restrict__ list, uint32_t* __restrict__ overflow,
+                                                  bool validate) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nb = E.k1 - E.k0;
+  if (i >= nb) return;
+  uint64_t f = kNone;  // guess
+  if (force) {
+    f = force[i];
+    if (f == kNone) return;  // keep this block's walk
+  }
+  const BlockInfo b = E.blocks[E.k0 + i];
+  const uint64_t bend = b.ustart + b.isize;
+  if (validate && f != kForceEmpty && f != kNone) {
+    // a link-round entry may itself come from a wrong walk upstream (fixed in
+    // the same round): re-walk only if the chain from it is plausible to the
+    // block end and beyond; otherwise keep the old walk for the next round
+    uint64_t q = f;
+    bool ok = true;
+    int extra = 0;
+    while (ok) {
+      if (q >= bend && (extra++ >= kGuessLookahead || q == E.e_true || q + 36 > E.e_inf)) break;
+      if (!plausible(E, q)) ok = false;
+      else q += 4 + (uint64_t)(int32_t)ldu32(E.u, q);
+    }
+    if (!ok) return;
+  }
+  uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
+  uint64_t g = kNone, x = kNone;
+  uint32_t n = 0;
+  const bool live = bend > E.p0 && b.ustart < E.q_end && b.isize > 0;
+  if (live && f != kForceEmpty) {
+    uint64_t entry = f;
+    if (f == kNone && b.ustart <= E.p0) entry = E.p0;  // the block of the span start: entry known
+    if (entry != kNone) {
+      g = entry;
+      uint64_t q = entry, nq;
+      while (q < bend) {
+        if (n < kListCap) L[n] = (uint16_t)(q - b.ustart);
+        ++n;
+        if (!chain_step<MODE>(E, q, &nq)) break;
+        q = nq;
+      }
+      x = q;
+    } else {
+      uint64_t c = cand[i];
+      while (c < bend) {  // c == kNone (no candidate): nothing to walk
+        uint64_t q = c;
+        uint32_t m = 0;
+        bool valid = true;
+        while (q < bend) {
+          if (!plausible(E, q)) { valid = false; break; }
+          if (m < kListCap) L[m] = (uint16_t)(q - b.ustart);
+          ++m;
+          q += 4 + (uint64_t)(int32_t)ldu32(E.u, q);
+        }
+        // the chain must go on plausibly past the block end for a few records
+        // (or reach the end / unreadable data): a false start one or two bytes
+        // before a true one reads a huge block_size and lands at random, and a
+        // single landing check passes too often (~1 in 2000 blocks on C2)
+        if (valid) {
+          uint64_t y = q;
+          for (int k = 0; k < kGuessLookahead; ++k) {
+            if (y == E.e_true || y + 36 > E.e_inf) break;
+            if (!plausible(E, y)) { valid = false; break; }
+            y += 4 + (uint64_t)(int32_t)ldu32(E.u, y);
+          }
+        }
+        if (valid) {
+          g = c;
+          x = q;
+          n = m;
+          break;
+        }
+        for (++c; c < bend && !plausible(E, c); ++c) {}
+      }
+    }
+  }
+  if (n > kListCap) atomicOr(overflow, 1u);
+  g_out[i] = g;
+  x_out[i] = x;
+  wcnt[i] = n;
+}
+
+// Parallel link check (in = exclusive max-scan of the guess exits).  Entries
+// where the chain enters a block; a block whose walk does not start there is
+// re-walked from it (force = entry), a stray walk in a pass-through block is
+// dropped (force = kForceEmpty).  A chain that breaks before a block is a
+// hard violation (serial link).
+__global__ void k_rec_linkfix(ChainEnv E, const uint64_t* __restrict__ g, const uint64_t* __restrict__ x,
+                              const uint64_t* __restrict__ in_scan, uint64_t* __restrict__ entry,
+                              uint64_t* __restrict__ force, uint32_t* __restrict__ counters) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nb = E.k1 - E.k0;
+  if (i >= nb) return;
+  if (i == 0) {
+    entry[0] = E.p0;
+    const BlockInfo b = E.blocks[E.k0];
+    if (x[0] < b.ustart + b.isize) atomicAdd(&counters[0], 1u);  // chain stops in the first block
+    return;
+  }
+  const BlockInfo b = E.blocks[E.k0 + i];
+  const uint64_t bend = b.ustart + b.isize;
+  const uint64_t in = in_scan[i];
+  const uint64_t gi = g[i];
+  uint64_t e = kNone;
+  if (in >= E.q_end) {
+    e = kNone;
+  } else if (in >= bend || b.isize == 0) {
+    if (gi != kNone && x[i] > in) {  // a stray walk would corrupt later in[]
+      force[i] = kForceEmpty;
+      atomicAdd(&counters[1], 1u);
+    }
+  } else if (in < b.ustart) {
+    atomicAdd(&counters[0], 1u);  // a block before stopped inside itself
+  } else {
+    e = in;
+    if (gi != in) {
+      force[i] = in;
+      atomicAdd(&counters[1], 1u);
+    }
+  }
+  entry[i] = e;
+}
+
+// force[] off the serial link's entry[]
+__global__ void k_force_from_entry(const uint64_t* __restrict__ g, const uint64_t* __restrict__ entry, uint32_t nb,
+                                   uint64_t* __restrict__ force) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb) return;
+  const uint64_t e = entry[i], gi = g[i];
+  force[i] = e == gi ? kNone : (e == kNone ? kForceEmpty : e);
+}
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, uint32_t src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, (int)src, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// The k_rec_count rules, one lane per listed record.
+template <int MODE>
+__global__ __launch_bounds__(64) void k_rec_check(ChainEnv E, const uint64_t* __restrict__ entry,
+                                                  const uint32_t* __restrict__ wcnt,
+                                                  const uint16_t* __restrict__ list, uint32_t* __restrict__ cnt,
+                                                  int32_t* __restrict__ err, unsigned long long* __restrict__ need) {
+  const uint32_t i = blockIdx.x;
+  const uint32_t lane = lane_id();
+  const uint64_t e = entry[i];
+  uint32_t count = 0;
+  int st = kOk;
+  if (e != kNone) {
+    const BlockInfo b = E.blocks[E.k0 + i];
+    const uint64_t lim = min(b.ustart + b.isize, E.q_end);
+    const uint32_t n = min(wcnt[i], kListCap);
+    const uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
+    count = n;
+    for (uint32_t r0 = 0; r0 < n; r0 += 64) {
+      const uint32_t r = r0 + lane;
+      bool stop = false, counted = false;
+      int s = kOk;
+      uint64_t nd = 0;
+      if (r < n) {
+        const uint64_t q = b.ustart + L[r];
+        const uint64_t avail = E.e_true - q;
+        if (q >= lim) {
+          stop = true;  // outside the span
+        } else if (MODE == kReader) {
+          const bool first = r == 0 && q == E.p0;  // first record follows a seek
+          if (!first && is_dead(E, q)) {
+            stop = true;  // readInt at an exhausted block + empty block: EOF
+          } else if (avail < 4) {
+            stop = true;
+          } else if (q + 4 > E.e_inf) {
+            stop = true;
+            nd = q + 4;
+          } else {
+            const int32_t bs = (int32_t)ldu32(E.u, q);
+            if (bs < 32) {
+              stop = true;
+              s = kErrFormat;
+            } else if (dead_in_record(E, q, bs) || avail - 4 < (uint64_t)bs) {
+              stop = true;
+              s = kErrTrunc;
+            } else if (q + 4 + (uint64_t)bs > E.e_inf) {
+              stop = true;
+              nd = q + 4 + (uint64_t)bs;
+            } else {
+              const int32_t ref = (int32_t)ldu32(E.u, q + 4), nref = (int32_t)ldu32(E.u, q + 24);
+              if (ref < -1 || ref >= E.n_ref || nref < -1 || nref >= E.n_ref) {
+                stop = true;
+                s = kErrArg;
+              }
+            }
+          }
+        } else {
+          if (is_dead(E, q)) {
+            stop = true;
+          } else if (avail < 4) {
+            stop = true;
+            if (avail > 0) s = kErrIO;  // "less than 4 bytes long"
+          } else if (q + 4 > E.e_inf) {
+            stop = true;
+            nd = q + 4;
+          } else {
+            const int32_t bs = (int32_t)ldu32(E.u, q);
+            if (bs > 0 && ((uint64_t)bs > avail - 4 || is_dead(E, q + 4))) {
+              stop = true;
+              counted = true;
+              s = kErrIO;  // "Skip failed"
+            }
+          }
+        }
+      }
+      const uint64_t m = __ballot(stop);
+      if (m) {
+        const uint32_t f = (uint32_t)__ffsll((long long)m) - 1;
+        count = r0 + f + (uint32_t)__shfl((int)counted, (int)f, 64);
+        st = __shfl(s, (int)f, 64);
+        const uint64_t fnd = shfl_u64(nd, f);
+        if (lane == 0 && fnd) atomicMax(need, (unsigned long long)fnd);
+        break;
+      }
+    }
+  }
+  if (lane == 0) {
+    cnt[i] = count;
+    err[i] = st;
+  }
+}
+
+template <int MODE, bool DECODE>
+__global__ __launch_bounds__(64) void k_rec_out(ChainEnv E, const uint32_t* __restrict__ cnt,
+                                                const uint64_t* __restrict__ base, const uint16_t* __restrict__ list,
+                                                uint64_t* __restrict__ rec_pos, uint64_t* __restrict__ rec_voff,
+                                                Columns col) {
+  const uint32_t i = blockIdx.x;
+  const uint32_t n = cnt[i];
+  if (n == 0) return;
+  const BlockInfo b = E.blocks[E.k0 + i];
+  const uint64_t o0 = base[i];
+  const uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
+  for (uint32_t r = lane_id(); r < n; r += 64) {
+    const uint32_t off = L[r];
+    const uint64_t q = b.ustart + off, o = o0 + r;
+    rec_pos[o] = q;
+    rec_voff[o] = (b.coff << 16) | off;
+    if (DECODE) decode_record(E.u, q, o, col);
   }
 }
 
@@ -1902,6 +2200,48 @@ hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s) 
       if (mode == kReader) hipLaunchKernelGGL(k_rec_emit<kReader>, dim3(gb), dim3(tb), 0, s, E, a.entry, a.cnt, a.base, a.rec_pos, a.rec_voff);
       else hipLaunchKernelGGL(k_rec_emit<kIndexer>, dim3(gb), dim3(tb), 0, s, E, a.entry, a.cnt, a.base, a.rec_pos, a.rec_voff);
       break;
+    case 5: {  // v2: candidates + walks
+      if (mode == kReader) {
+        hipLaunchKernelGGL(k_rec_cand<kReader>, dim3(nb), dim3(64), 0, s, E, a.cand);
+        hipLaunchKernelGGL(k_rec_walk<kReader>, dim3((nb + 255) / 256), dim3(256), 0, s, E, a.cand, nullptr, a.g,
+                           a.x, a.wcnt, a.list, a.counters + 2, false);
+      } else {
+        hipLaunchKernelGGL(k_rec_cand<kIndexer>, dim3(nb), dim3(64), 0, s, E, a.cand);
+        hipLaunchKernelGGL(k_rec_walk<kIndexer>, dim3((nb + 255) / 256), dim3(256), 0, s, E, a.cand, nullptr, a.g,
+                           a.x, a.wcnt, a.list, a.counters + 2, false);
+      }
+      break;
+    }
+    case 6: {  // v2: y, exclusive max-scan, check with re-walk requests
+      hipError_t e = hipMemsetAsync(a.force, 0xff, (size_t)nb * 8, s);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(k_rec_link_y, dim3(gb), dim3(tb), 0, s, a.g, a.x, nb, a.x2);
+      size_t sb = a.scan_bytes;
+      e = hipcub::DeviceScan::ExclusiveScan(a.scan_tmp, sb, a.x2, a.base, hipcub::Max(), (uint64_t)0, (int)nb, s);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(k_rec_linkfix, dim3(gb), dim3(tb), 0, s, E, a.g, a.x, a.base, a.entry, a.force, a.counters);
+      break;
+    }
+    case 7:    // v2: re-walk the requested blocks (entries validated)
+    case 8: {  // v2: force off the serial link's (exact) entry[], then re-walk
+      const bool validate = stage == 7;
+      if (stage == 8) hipLaunchKernelGGL(k_force_from_entry, dim3(gb), dim3(tb), 0, s, a.g, a.entry, nb, a.force);
+      if (mode == kReader)
+        hipLaunchKernelGGL(k_rec_walk<kReader>, dim3((nb + 255) / 256), dim3(256), 0, s, E, a.cand, a.force, a.g,
+                           a.x, a.wcnt, a.list, a.counters + 2, validate);
+      else
+        hipLaunchKernelGGL(k_rec_walk<kIndexer>, dim3((nb + 255) / 256), dim3(256), 0, s, E, a.cand, a.force, a.g,
+                           a.x, a.wcnt, a.list, a.counters + 2, validate);
+      break;
+    }
+    case 9:  // v2: per-record check
+      if (mode == kReader)
+        hipLaunchKernelGGL(k_rec_check<kReader>, dim3(nb), dim3(64), 0, s, E, a.entry, a.wcnt, a.list, a.cnt, a.err,
+                           a.need);
+      else
+        hipLaunchKernelGGL(k_rec_check<kIndexer>, dim3(nb), dim3(64), 0, s, E, a.entry, a.wcnt, a.list, a.cnt,
+                           a.err, a.need);
+      break;
     case 4: {  // parallel link: y, exclusive max-scan, check
       hipLaunchKernelGGL(k_rec_link_y, dim3(gb), dim3(tb), 0, s, a.g, a.x, nb, a.x2);
       size_t sb = a.scan_bytes;
@@ -1914,6 +2254,33 @@ hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s) 
     default:
       return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_rec_out(const ChainArgs& a, int mode, bool decode, const Columns& col, hipStream_t s) {
+  ChainEnv E;
+  E.u = a.u;
+  E.blocks = a.blocks;
+  E.e_inf = a.e_inf;
+  E.e_true = a.e_true;
+  E.p0 = a.p0;
+  E.q_end = a.q_end;
+  E.dead = a.dead;
+  E.ndead = a.ndead;
+  E.n_ref = a.n_ref;
+  E.k0 = a.k0;
+  E.k1 = a.k1;
+  const uint32_t nb = a.k1 - a.k0;
+  if (nb == 0) return hipSuccess;
+  if (mode == kReader && decode)
+    hipLaunchKernelGGL((k_rec_out<kReader, true>), dim3(nb), dim3(64), 0, s, E, a.cnt, a.base, a.list, a.rec_pos,
+                       a.rec_voff, col);
+  else if (mode == kReader)
+    hipLaunchKernelGGL((k_rec_out<kReader, false>), dim3(nb), dim3(64), 0, s, E, a.cnt, a.base, a.list, a.rec_pos,
+                       a.rec_voff, col);
+  else
+    hipLaunchKernelGGL((k_rec_out<kIndexer, false>), dim3(nb), dim3(64), 0, s, E, a.cnt, a.base, a.list, a.rec_pos,
+                       a.rec_voff, col);
   return hipGetLastError();
 }
 

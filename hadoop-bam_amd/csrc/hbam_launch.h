@@ -26,7 +26,15 @@ struct ChainArgs {
   unsigned long long* need;
   // outputs
   uint64_t *rec_pos, *rec_voff;
+  // chain v2 (lane-per-block walks + per-block record lists)
+  uint64_t* cand;       // first plausible record start per block
+  uint64_t* force;      // re-walk requests (kNone = keep)
+  uint32_t* wcnt;       // records listed per block
+  uint16_t* list;       // kListCap u16 offsets (from ustart) per block
+  uint32_t* counters;   // [0] hard link violations, [1] blocks to re-walk, [2] list overflow
 };
+constexpr uint32_t kListCap = 2048;              // >= 65536 / 36 + 2: every reader-mode record start
+constexpr uint64_t kForceEmpty = ~0ull - 1;      // force[]: the block holds no record start
 
 hipError_t launch_bgzf_scan(const uint8_t* file, uint64_t lo, uint64_t hi, uint64_t* cand, uint32_t cap,
                             uint32_t* count, hipStream_t s);
@@ -56,8 +64,13 @@ inline uint32_t huff_stage_bytes(const BlockInfo& b) {
 }
 hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb, uint64_t chunk_ustart,
                                const uint32_t* tokens, const HuffOut* hout, uint8_t* u, hipStream_t s);
-// stage: 0 guess, 1 serial link, 2 count, 3 emit, 4 parallel link (base = in[] scratch)
+// stage: 0 guess, 1 serial link, 2 count, 3 emit, 4 parallel link (base = in[] scratch),
+//        5 candidates + walks (v2), 6 link check with re-walk requests (v2),
+//        7 re-walk requested blocks (v2), 8 re-walk every block off entry[] (v2),
+//        9 per-record check -> cnt/err/need (v2)
 hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s);
+// chain v2 output: positions, voffs and (decode) the SoA columns, one wave per block
+hipError_t launch_rec_out(const ChainArgs& a, int mode, bool decode, const Columns& col, hipStream_t s);
 hipError_t link_scan_bytes(uint32_t nb, size_t* bytes);
 hipError_t launch_rec_decode(const uint8_t* u, const uint64_t* rec_pos, uint64_t n, const Columns& col,
                              hipStream_t s);

@@ -13,6 +13,7 @@ namespace hbam {
 namespace {
 constexpr uint32_t kInflateChunkBlocks = 16384;  // blocks per phase-A/B launch pair
 constexpr int kMaxChainIters = 64;
+constexpr int kMaxLinkFix = 4;  // re-walk rounds before the serial link
 }  // namespace
 
 Pipeline::Pipeline(int device) : device_(device) {
@@ -348,6 +349,7 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
   a.k0 = k0;
   if (timing) HIPCHK(hipEventRecord(ev_[0], stream_));
   float infl_ms = 0;
+  bool lists = true;  // chain v2 lists hold every record start (no overflow)
   for (int it = 0;; ++it) {
     if (it >= kMaxChainIters) return fail(kErrState, "record chain did not converge");
     int rc = inflate(k0, inf_end);
@@ -359,43 +361,82 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
     const uint32_t nb = k1 - k0;
     HIPCHK(g_.reserve(nb));
     HIPCHK(x_.reserve(nb));
+    HIPCHK(x2_.reserve(nb));
     HIPCHK(entry_.reserve(nb));
     HIPCHK(summary_.reserve(4));
     HIPCHK(cnt_.reserve(nb + 1));
     HIPCHK(errv_.reserve(nb + 1));
     HIPCHK(need_.reserve(1));
+    HIPCHK(rcand_.reserve(nb));
+    HIPCHK(force_.reserve(nb));
+    HIPCHK(wcnt_.reserve(nb));
+    HIPCHK(list_.reserve((uint64_t)nb * kListCap));
+    HIPCHK(base_arr_.reserve(nb + 1));
+    HIPCHK(counters_.reserve(4));
+    size_t lsb = 0;
+    HIPCHK(link_scan_bytes(nb, &lsb));
+    HIPCHK(scan_tmp_.reserve(lsb + 16));
     a.g = g_.p;
     a.x = x_.p;
+    a.x2 = x2_.p;
     a.entry = entry_.p;
     a.summary = summary_.p;
     a.cnt = cnt_.p;
     a.err = errv_.p;
     a.need = need_.p;
-    HIPCHK(hipMemsetAsync(need_.p, 0, 8, stream_));
-    HIPCHK(launch_chain(a, mode, 0, stream_));  // per-block guesses
-    // link: parallel check of the guesses, exact serial link on any violation
-    HIPCHK(x2_.reserve(nb));
-    HIPCHK(base_arr_.reserve(nb + 1));
-    size_t lsb = 0;
-    HIPCHK(link_scan_bytes(nb, &lsb));
-    HIPCHK(scan_tmp_.reserve(lsb + 16));
-    HIPCHK(hipMemsetAsync(flags_.p + 2, 0, 4, stream_));
-    a.x2 = x2_.p;
+    a.cand = rcand_.p;
+    a.force = force_.p;
+    a.wcnt = wcnt_.p;
+    a.list = list_.p;
+    a.counters = counters_.p;
     a.base = base_arr_.p;
-    a.changed = flags_.p + 2;
     a.scan_tmp = scan_tmp_.p;
     a.scan_bytes = lsb;
-    HIPCHK(launch_chain(a, mode, 4, stream_));
-    uint32_t fails = 0;
-    HIPCHK(hipMemcpyAsync(&fails, flags_.p + 2, 4, hipMemcpyDeviceToHost, stream_));
-    HIPCHK(hipStreamSynchronize(stream_));
-    link_fallbacks_ += fails ? 1 : 0;
-    if (fails) HIPCHK(launch_chain(a, mode, 1, stream_));  // exact serial link (writes entry)
+    HIPCHK(hipMemsetAsync(need_.p, 0, 8, stream_));
+    HIPCHK(hipMemsetAsync(counters_.p, 0, 16, stream_));
+    HIPCHK(launch_chain(a, mode, 5, stream_));  // candidates + lane-per-block walks
+    // link: max-scan of the walk exits; re-walk blocks that are off the chain
+    bool serial = false;
+    for (int fix = 0;; ++fix) {
+      HIPCHK(hipMemsetAsync(counters_.p, 0, 8, stream_));
+      HIPCHK(launch_chain(a, mode, 6, stream_));
+      uint32_t ctr[2] = {0, 0};
+      HIPCHK(hipMemcpyAsync(ctr, counters_.p, 8, hipMemcpyDeviceToHost, stream_));
+      HIPCHK(hipStreamSynchronize(stream_));
+      static const bool dbg = getenv("HBAM_DEBUG_LINK") != nullptr;
+      if (dbg && (ctr[0] || ctr[1])) {  // print the first flagged blocks of this round
+        std::vector<uint64_t> hg(nb), hx(nb), hin(nb), hf(nb);
+        HIPCHK(hipMemcpy(hg.data(), g_.p, nb * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(hx.data(), x_.p, nb * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(hin.data(), base_arr_.p, nb * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(hf.data(), force_.p, nb * 8, hipMemcpyDeviceToHost));
+        int shown = 0;
+        fprintf(stderr, "[link] round %d hard=%u fix=%u nb=%u\n", fix, ctr[0], ctr[1], nb);
+        for (uint32_t i = 0; i < nb && shown < 6; ++i) {
+          const BlockInfo& b = hblocks_[k0 + i];
+          const bool flagged = hf[i] != kNone || (i > 0 && hin[i] < b.ustart && hin[i] < q_end);
+          if (!flagged) continue;
+          ++shown;
+          fprintf(stderr, "  blk %u ustart=%llu bend=%llu in=%lld g=%lld x=%lld force=%lld prev_g=%lld prev_x=%lld\n", i,
+                  (unsigned long long)b.ustart, (unsigned long long)(b.ustart + b.isize), (long long)hin[i],
+                  (long long)hg[i], (long long)hx[i], (long long)hf[i], i ? (long long)hg[i - 1] : -1,
+                  i ? (long long)hx[i - 1] : -1);
+        }
+      }
+      if (ctr[0]) { serial = true; break; }
+      if (ctr[1] == 0) break;
+      if (fix == kMaxLinkFix) { serial = true; break; }
+      ++link_rewalks_;
+      HIPCHK(launch_chain(a, mode, 7, stream_));
+    }
     uint64_t sm[2] = {0, 0};
     unsigned long long need = 0;
-    if (fails) {
+    if (serial) {  // exact serial link (writes entry[] + summary), then lists off entry[]
+      ++link_fallbacks_;
+      HIPCHK(launch_chain(a, mode, 1, stream_));
+      HIPCHK(launch_chain(a, mode, 8, stream_));
       HIPCHK(hipMemcpyAsync(sm, summary_.p, 16, hipMemcpyDeviceToHost, stream_));
-    } else {  // final chain position = max of every guess exit; no stop
+    } else {  // final chain position = max of every walk exit; no stop
       uint64_t t[2] = {0, 0};
       HIPCHK(hipMemcpyAsync(&t[0], base_arr_.p + nb - 1, 8, hipMemcpyDeviceToHost, stream_));
       HIPCHK(hipMemcpyAsync(&t[1], x2_.p + nb - 1, 8, hipMemcpyDeviceToHost, stream_));
@@ -403,8 +444,11 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
       sm[0] = nb == 1 ? t[1] : std::max(t[0], t[1]);
       sm[1] = 0;
     }
+    uint32_t ovf = 0;
+    HIPCHK(hipMemcpyAsync(&ovf, counters_.p + 2, 4, hipMemcpyDeviceToHost, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
-    HIPCHK(launch_chain(a, mode, 2, stream_));  // count + validate
+    lists = ovf == 0;
+    HIPCHK(launch_chain(a, mode, lists ? 9 : 2, stream_));  // count + validate
     HIPCHK(hipMemcpyAsync(&need, need_.p, 8, hipMemcpyDeviceToHost, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
     const uint64_t final_pos = sm[0];
@@ -460,12 +504,12 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
   a.base = base_arr_.p;
   a.rec_pos = rec_pos_.p;
   a.rec_voff = rec_voff_.p;
-  HIPCHK(launch_chain(a, mode, 3, stream_));
-  if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
   out->n = total;
   out->rec_pos = rec_pos_.p;
   out->rec_voff = rec_voff_.p;
-  if (decode && mode == kReader) {
+  const bool dec = decode && mode == kReader;
+  Columns c{};
+  if (dec) {
     // SoA backing store: 8-byte columns first, then 4, 2, 1 (alignment)
     const uint64_t n = std::max<uint64_t>(total, 1);
     const uint64_t per = 8 * 2 + 4 * 7 + 2 * 3 + 1 * 2;
@@ -479,7 +523,6 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
       p += (bytes + 15) & ~15ull;
       return r;
     };
-    Columns& c = out->col;
     c.key = reinterpret_cast<int64_t*>(take(8 * n));
     c.rest_off = reinterpret_cast<uint64_t*>(take(8 * n));
     c.voff = rec_voff_.p;
@@ -495,16 +538,24 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
     c.flag = reinterpret_cast<uint16_t*>(take(2 * n));
     c.l_read_name = take(n);
     c.mapq = take(n);
-    HIPCHK(launch_rec_decode(du_.p, rec_pos_.p, total, c, stream_));
+    out->col = c;
+  }
+  if (lists) {  // positions + voffs (+ fused decode) straight off the per-block lists
+    if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
+    HIPCHK(launch_rec_out(a, mode, dec, c, stream_));
+  } else {      // a block listed more starts than kListCap: per-block walks
+    HIPCHK(launch_chain(a, mode, 3, stream_));
+    if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
+    if (dec) HIPCHK(launch_rec_decode(du_.p, rec_pos_.p, total, c, stream_));
   }
   if (timing) HIPCHK(hipEventRecord(ev_[2], stream_));
   HIPCHK(hipStreamSynchronize(stream_));
   if (timing) {
-    float all = 0, dec = 0;
+    float all = 0, dcd = 0;
     (void)hipEventElapsedTime(&all, ev_[0], ev_[1]);
-    (void)hipEventElapsedTime(&dec, ev_[1], ev_[2]);
+    (void)hipEventElapsedTime(&dcd, ev_[1], ev_[2]);
     times.chain = all - infl_ms;
-    times.decode = dec;
+    times.decode = dcd;
     times.inflate = infl_ms;
   }
   return kOk;

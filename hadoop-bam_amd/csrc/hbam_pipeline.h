@@ -101,6 +101,7 @@ class Pipeline {
   int32_t n_ref() const { return n_ref_; }
 
   uint64_t link_fallbacks() const { return link_fallbacks_; }
+  uint64_t link_rewalks() const { return link_rewalks_; }
   uint64_t inflate_launches() const { return inflate_launches_; }
   StageTimes times;
   bool timing = false;  // record per-stage HIP event times
@@ -123,6 +124,7 @@ class Pipeline {
   uint32_t ndead_ = 0;
   int32_t n_ref_ = 0;
   uint64_t link_fallbacks_ = 0;
+  uint64_t link_rewalks_ = 0;      // re-walk rounds of the parallel link
   uint64_t inflate_launches_ = 0;  // phase A/B launch pairs so far
 
   DevBuf<uint8_t> du_;
@@ -139,6 +141,9 @@ class Pipeline {
   DevBuf<int32_t> errv_;
   DevBuf<unsigned long long> need_;
   DevBuf<uint64_t> rec_pos_, rec_voff_;
+  DevBuf<uint64_t> rcand_, force_;  // chain v2
+  DevBuf<uint32_t> wcnt_, counters_;
+  DevBuf<uint16_t> list_;
   DevBuf<uint8_t> scan_tmp_;
   DevBuf<uint8_t> cols_;  // SoA backing store
   uint64_t cols_cap_ = 0;

@@ -153,7 +153,7 @@ typedef struct hbam_gpu_stats {
   int32_t status;
   int32_t link_fallbacks;     /* record-chain spans that took the exact serial link */
   int32_t inflate_launches;   /* phase A + B launch pairs of this run */
-  int32_t reserved;
+  int32_t link_rewalks;       /* parallel-link re-walk rounds of this run */
 } hbam_gpu_stats;
 
 int hbam_gpu_create(int32_t device, hbam_gpu **out);
