@@ -1283,10 +1283,23 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
                                                              uint64_t chunk_ustart,
                                                              const uint32_t* __restrict__ tokens,
                                                              const HuffOut* __restrict__ hout,
-                                                             uint8_t* __restrict__ u) {
+                                                             uint8_t* __restrict__ u,
+                                                             uint64_t* __restrict__ prof) {
   // map index = o0 + position, so 16-byte output segments read 32 B-aligned LDS
   __shared__ __attribute__((aligned(16))) uint16_t map[kMapMax + 32];
   __shared__ uint32_t scratch[kLzWaves];
+  // optional cycle profile (thread 0): [0] token scan [2] map fill
+  // [3] resolve [4] store [5] total ([1] unused)
+  uint64_t pacc[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t pt = prof ? clock64() : 0, pt0 = pt;
+#define LZ_T(i)                             \
+  do {                                      \
+    if (prof && threadIdx.x == 0) {         \
+      const uint64_t n_ = clock64();        \
+      pacc[i] += n_ - pt;                   \
+      pt = n_;                              \
+    }                                       \
+  } while (0)
   const BlockInfo blk = blocks[b0 + blockIdx.x];
   const HuffOut ho = hout[b0 + blockIdx.x];
   if (ho.status != kOk || blk.isize == 0) return;
@@ -1323,6 +1336,7 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
   for (uint32_t i = t0; i < t1; ++i) nbytes += tok_len(tk[i]);
   uint32_t total;
   uint32_t p = block_excl_scan(nbytes, scratch, &total);
+  LZ_T(0);
 
   // 2. expand tokens into the map (the last token may run past ISIZE: clamp)
   uint16_t* m = map + o0;
@@ -1340,6 +1354,7 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
     }
   }
   __syncthreads();
+  LZ_T(2);
 
   // 3. resolve, increasing positions first; results written back in place
   for (uint32_t q = tid; q < isize; q += kLzThreads) {
@@ -1348,6 +1363,7 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
     m[q] = (uint16_t)v;
   }
   __syncthreads();
+  LZ_T(3);
 
   // 4. 16 B stores; low bytes of 16 entries packed with v_perm
   for (uint32_t s = tid; s < nseg; s += kLzThreads) {
@@ -1368,6 +1384,12 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
       }
     }
   }
+  LZ_T(4);
+  if (prof && tid == 0) {
+    pacc[5] = clock64() - pt0;
+    for (int i = 0; i < 6; ++i) prof[8ull * (b0 + blockIdx.x) + i] = pacc[i];
+  }
+#undef LZ_T
 }
 
 // ---------------------------------------------------------------------------
@@ -2124,7 +2146,8 @@ hipError_t scan_u32_to_u64(void* tmp, size_t* tmp_bytes, const uint32_t* in, uin
   return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, in, out, (int)n, s);
 }
 
-uint64_t* g_huff_prof = nullptr;  // HBAM_HUFF_PROF: per-block cycle profile (hbam_pipeline.cpp)
+uint64_t* g_huff_prof = nullptr;
+uint64_t* g_lz_prof = nullptr;  // HBAM_HUFF_PROF: phase-B per-block cycle profile (8 u64 per block)  // HBAM_HUFF_PROF: per-block cycle profile (hbam_pipeline.cpp)
 
 // max_stage = largest staged span of the chunk's blocks (huff_stage_bytes)
 static hipError_t launch_huff(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
@@ -2151,7 +2174,8 @@ hipError_t launch_inflate(const uint8_t* file, const BlockInfo* blocks, uint32_t
   if (nb == 0) return hipSuccess;
   hipError_t e = launch_huff(file, blocks, b0, nb, chunk_ustart, tokens, hout, max_stage, tables, tinfo, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_inflate_lz77, dim3(nb), dim3(kLzThreads), 0, s, blocks, b0, chunk_ustart, tokens, hout, u);
+  hipLaunchKernelGGL(k_inflate_lz77, dim3(nb), dim3(kLzThreads), 0, s, blocks, b0, chunk_ustart, tokens, hout, u,
+                     g_lz_prof);
   return hipGetLastError();
 }
 hipError_t launch_inflate_huff(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
@@ -2163,7 +2187,8 @@ hipError_t launch_inflate_huff(const uint8_t* file, const BlockInfo* blocks, uin
 hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb, uint64_t chunk_ustart,
                                const uint32_t* tokens, const HuffOut* hout, uint8_t* u, hipStream_t s) {
   if (nb == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_inflate_lz77, dim3(nb), dim3(kLzThreads), 0, s, blocks, b0, chunk_ustart, tokens, hout, u);
+  hipLaunchKernelGGL(k_inflate_lz77, dim3(nb), dim3(kLzThreads), 0, s, blocks, b0, chunk_ustart, tokens, hout, u,
+                     g_lz_prof);
   return hipGetLastError();
 }
 

@@ -56,6 +56,7 @@ hipError_t launch_inflate_huff(const uint8_t* file, const BlockInfo* blocks, uin
                                uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s);
 // HBAM_HUFF_PROF profile buffer (16 u64 per block) or nullptr
 extern uint64_t* g_huff_prof;
+extern uint64_t* g_lz_prof;
 // LDS bytes phase A stages for a block: its cdata from the 16 B-aligned start,
 // footer included, plus one 16 B pad (must match k_inflate_huff).
 inline uint32_t huff_stage_bytes(const BlockInfo& b) {

@@ -168,10 +168,14 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force) {
   static const bool prof_on = getenv("HBAM_HUFF_PROF") != nullptr;
   DevBuf<uint64_t> prof;
   const bool prof_this = prof_on && b1 - b0 >= 1024;
+  DevBuf<uint64_t> lzprof;
   if (prof_this) {
     HIPCHK(prof.reserve(16ull * nblk));
     HIPCHK(hipMemsetAsync(prof.p, 0, 16ull * nblk * 8, stream_));
     g_huff_prof = prof.p;
+    HIPCHK(lzprof.reserve(8ull * nblk));
+    HIPCHK(hipMemsetAsync(lzprof.p, 0, 8ull * nblk * 8, stream_));
+    g_lz_prof = lzprof.p;
   }
   uint32_t b = b0;
   bool any = false;
@@ -213,7 +217,21 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force) {
     b = e;
   }
   g_huff_prof = nullptr;
+  g_lz_prof = nullptr;
   if (prof_this && any) {
+    std::vector<uint64_t> hl(8ull * nblk);
+    HIPCHK(hipMemcpy(hl.data(), lzprof.p, hl.size() * 8, hipMemcpyDeviceToHost));
+    double la[6] = {0};
+    uint64_t ln = 0;
+    for (uint32_t k = b0; k < b1; ++k) {
+      if (hl[8ull * k + 5] == 0) continue;
+      ++ln;
+      for (int i = 0; i < 6; ++i) la[i] += (double)hl[8ull * k + i];
+    }
+    static const char* lnames[6] = {"scan", "-", "fill", "resolve", "store", "total"};
+    fprintf(stderr, "[lz77 prof] %llu blocks, mean cycles per block:", (unsigned long long)ln);
+    for (int i = 0; i < 6; ++i) fprintf(stderr, " %s=%.0f", lnames[i], ln ? la[i] / ln : 0.0);
+    fprintf(stderr, "\n");
     std::vector<uint64_t> h(16ull * nblk);
     HIPCHK(hipMemcpy(h.data(), prof.p, h.size() * 8, hipMemcpyDeviceToHost));
     double acc[11] = {0};
