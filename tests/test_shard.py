@@ -1,0 +1,116 @@
+"""Multi-process sharded read (hbam.shard) on CPU with gloo.
+
+Each rank stands in the oracle as its shard decoder (test infrastructure), so
+these tests pin the host logic of the multi-GPU path: byte splits, the
+BAMSplitGuesser-based virtual splits, the empty-split merge of
+BAMInputFormat.java:497-513, global ordinals and the gathered .splitting-bai.
+The GPU decoder behind the same logic is covered by test_gpu_shard.py.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import orc
+from hbam import shard, synth
+
+
+class OracleDecoder:
+    def __init__(self, data):
+        self.s = orc.Stream(data)
+
+    def guess_record_starts(self, begs, ends):
+        return [self.s.guess_record_start(b, e) for b, e in zip(begs, ends)]
+
+    def decode_span(self, vs, ve):
+        rc, r = self.s.decode_span(vs, ve)
+        assert rc == 0
+        return r
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, path, outdir, granularity, use_gpu):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    data = open(path, "rb").read()
+    if use_gpu:
+        import hbam
+        dec = hbam.BamFile(data, device=0)
+        first = dec.header()["first_record_voff"]
+    else:
+        dec = OracleDecoder(data)
+        first = dec.s.first_record_voff
+
+    def all_gather(obj):
+        out = [None] * world
+        dist.all_gather_object(out, obj)
+        return out
+
+    rd = shard.ShardedBamReader(dec, len(data), first, rank, world, all_gather)
+    recs, base, total, sbi = rd.run(granularity)
+    keys = recs["key"] if recs is not None else np.zeros(0, np.int64)
+    voffs = recs["voff"] if recs is not None else np.zeros(0, np.uint64)
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), key=keys, voff=voffs, base=base, total=total,
+             sbi=np.frombuffer(sbi, np.uint8) if sbi is not None else np.zeros(0, np.uint8))
+    dist.destroy_process_group()
+
+
+def run_sharded(data, world, granularity, tmp_path, use_gpu=False):
+    path = os.path.join(tmp_path, "in.bam")
+    open(path, "wb").write(data)
+    mp.spawn(_worker, args=(world, _free_port(), path, str(tmp_path), granularity, use_gpu), nprocs=world,
+             join=True)
+    parts = [np.load(os.path.join(tmp_path, f"r{r}.npz")) for r in range(world)]
+    return parts
+
+
+def check_against_oracle(data, parts, granularity):
+    s = orc.Stream(data)
+    rc, want = s.decode_all()
+    assert rc == 0
+    keys = np.concatenate([p["key"] for p in parts])
+    voffs = np.concatenate([p["voff"] for p in parts])
+    np.testing.assert_array_equal(voffs, want["voff"])
+    np.testing.assert_array_equal(keys, want["key"])
+    bases = [int(p["base"]) for p in parts]
+    assert bases == [int(sum(len(q["voff"]) for q in parts[:r])) for r in range(len(parts))]
+    assert all(int(p["total"]) == len(want["voff"]) for p in parts)
+    assert parts[0]["sbi"].tobytes() == s.splitting_index(granularity)
+
+
+def test_file_splits_cover_the_file():
+    for size, world in ((10, 3), (1000, 8), (7, 8)):
+        sp = shard.file_splits(size, world)
+        assert len(sp) == world
+        assert sp[0][0] == 0 and sum(n for _, n in sp) == size
+        for (a, n), (b, _) in zip(sp, sp[1:]):
+            assert a + n == b
+
+
+def test_merge_empty_splits_follows_reference():
+    # BAMInputFormat.java:497-513: an empty split extends the previous one
+    got = shard.merge_empty_splits([(5, 10, False), (20, 30, True), (25, 40, True), (50, 60, False)])
+    assert got == [(5, 40), None, None, (50, 60)]
+    with pytest.raises(IOError):
+        shard.merge_empty_splits([(0, 10, True), (20, 30, False)])
+
+
+@pytest.mark.parametrize("world,g,kw", [
+    (2, 4096, dict(n_records=6000)),
+    (3, 7, dict(n_records=4000, block_payload=4096)),          # many straddling records
+    (4, 1, dict(n_records=1500, block_payload=8192, level=1)),
+    (2, 5, dict(n_records=12, mode="long")),                     # records spanning many blocks
+])
+def test_sharded_read_matches_whole_file(tmp_path, world, g, kw):
+    data, _ = synth.make_bam(**kw)
+    parts = run_sharded(data, world, g, tmp_path)
+    check_against_oracle(data, parts, g)
