@@ -53,26 +53,28 @@ __device__ __forceinline__ uint64_t ldu64(const uint8_t* base, uint64_t off) {
 // exact framing htsjdk writes and requires (XLEN==6), plus the BC subfield id
 // for selectivity.  Candidates are appended unordered, sorted, then the BSIZE
 // chain is verified; any break falls back to the serial walk (bgzf_walk).
-__global__ void k_bgzf_scan(const uint8_t* __restrict__ file, uint64_t lo, uint64_t hi,
+__global__ void k_bgzf_scan(const uint8_t* __restrict__ buf, uint64_t len, uint64_t base,
                             uint64_t* __restrict__ cand, uint32_t cap, uint32_t* __restrict__ count) {
-  const uint64_t a0 = lo & ~3ull;
-  const uint64_t nd = (hi - a0 + 3) / 4;  // dwords to inspect
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nd;
+  // buf = first byte of the loaded range (16 B aligned, zero padded past
+  // len); 16 positions per thread from one 16 B load + the next word;
+  // candidates are reported in file coordinates (base + offset)
+  const uint64_t nc = (len + 15) / 16;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nc;
        t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(file + a0) + t;
-    uint32_t w0 = w[0], w1 = w[1];
+    const uint4 v = *reinterpret_cast<const uint4*>(buf + 16 * t);
+    const uint32_t w4 = *reinterpret_cast<const uint32_t*>(buf + 16 * t + 16);
+    const uint32_t w[5] = {v.x, v.y, v.z, v.w, w4};
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      uint64_t p = a0 + 4 * t + s;
-      if (p < lo || p >= hi) continue;
-      uint32_t magic = __builtin_amdgcn_alignbyte(w1, w0, s);
+    for (int s = 0; s < 16; ++s) {
+      const uint32_t magic = __builtin_amdgcn_alignbyte(w[(s >> 2) + 1], w[s >> 2], s & 3);
       if (magic != 0x04088b1fu) continue;
-      if (p + 18 > hi) continue;
-      uint32_t xlen = ldu32(file, p + 10) & 0xffffu;
-      uint32_t sub = ldu32(file, p + 12);
+      const uint64_t p = 16 * t + s;
+      if (p + 18 > len) continue;
+      const uint32_t xlen = ldu32(buf, p + 10) & 0xffffu;
+      const uint32_t sub = ldu32(buf, p + 12);
       if (xlen != 6 || sub != 0x00024342u) continue;
-      uint32_t i = atomicAdd(count, 1u);
-      if (i < cap) cand[i] = p;
+      const uint32_t i = atomicAdd(count, 1u);
+      if (i < cap) cand[i] = base + p;
     }
   }
 }
@@ -824,6 +826,148 @@ __device__ __forceinline__ int dyn_header(HuffLds& L, SReader& R, uint32_t E) {
   return DH_OK;
 }
 
+// Dynamic header with the code-length symbols decoded by all 64 lanes of the
+// wave (k_huff_tables): lane l speculatively decodes the kClSlice bits from
+// p + l*kClSlice of a window, a sync loop restarts slices from their
+// predecessor's exit until every lane starts on a true boundary (code-length
+// codes are <= 7 bits and resynchronise within a few symbols), then a wave
+// scan of the run lengths places every lane's runs in lens[].  Valid headers
+// only: any anomaly (bad counts, a repeat with no previous length, a run past
+// HLIT+HDIST, bits beyond the staged window) returns DH_TRUNC and the decode
+// kernel parses the block inline with dyn_header (the zlib semantics).
+constexpr uint32_t kClSlice = 16;
+constexpr uint32_t kClMaxSym = kClSlice;  // a slice holds at most one symbol per bit
+struct ClLds {
+  uint16_t ent[64][kClMaxSym];  // sym | extra << 5 | bits << 12
+};
+
+__device__ __forceinline__ uint32_t peek32(const uint32_t* W, uint32_t p) {
+  return __builtin_amdgcn_alignbit(W[(p >> 5) + 1], W[p >> 5], p & 31);
+}
+
+__device__ int dyn_header_par(HuffLds& L, ClLds& C, const uint32_t* __restrict__ W, uint32_t p, uint32_t E,
+                              uint32_t* end_pos) {
+  const uint32_t lane = lane_id();
+  if (p + 14 > E) return DH_TRUNC;
+  const uint32_t h = rfl(peek32(W, p));
+  const uint32_t hlit = (h & 31) + 257, hdist = ((h >> 5) & 31) + 1, hclen = ((h >> 10) & 15) + 4;
+  if (hlit > 286 || hdist > 30) return DH_TRUNC;
+  p += 14;
+  if (p + 3 * hclen > E) return DH_TRUNC;
+  if (lane < 20) L.cl_lens[lane] = 0;
+  wave_sync();
+  if (lane < hclen) L.cl_lens[kClOrder[lane]] = (uint8_t)(peek32(W, p + 3 * lane) & 7);
+  wave_sync();
+  p += 3 * hclen;
+  if (rfl(build_table(L, L.cl_lens, 19, 7, 2, L.dist, L.cnt_dist, L.sort_dist, nullptr, 0))) return DH_TRUNC;
+  const uint32_t ntot = hlit + hdist;
+  uint32_t done = 0, prevv = 0, have_prev = 0;
+  for (;;) {  // windows of 64 * kClSlice bits
+    const uint32_t a0 = p + lane * kClSlice, stop = a0 + kClSlice;
+    uint32_t a = a0, x = a0, ns = 0;
+    auto decode_slice = [&]() {
+      x = a;
+      ns = 0;
+      while (x < stop && x + 14 <= E) {
+        const uint32_t b = peek32(W, x);
+        const uint32_t e = L.dist[b & 127];
+        const uint32_t nb = (e >> 16) & 31, sym = e & 0xffff;
+        const uint32_t xb = sym < 16 ? 0u : sym == 16 ? 2u : sym == 17 ? 3u : 7u;
+        const uint32_t ext = (b >> nb) & ((1u << xb) - 1);
+        if (ns < kClMaxSym) C.ent[lane][ns] = (uint16_t)(sym | (ext << 5) | ((nb + xb) << 12));
+        ++ns;
+        x += nb + xb;
+      }
+    };
+    decode_slice();
+    for (;;) {  // sync: restart each slice from its predecessor's exit
+      uint32_t px = __shfl_up(x, 1, 64);
+      if (lane == 0) px = a0;
+      const bool need = px != a;
+      if (__ballot(need) == 0) break;
+      if (need) {
+        a = px;
+        decode_slice();
+      }
+    }
+    // run lengths of this lane's symbols and its last defined value
+    uint32_t cnt = 0, own = 0, has = 0;
+    for (uint32_t j = 0; j < ns && j < kClMaxSym; ++j) {
+      const uint32_t en = C.ent[lane][j], sym = en & 31, ext = (en >> 5) & 127;
+      cnt += sym < 16 ? 1u : sym == 18 ? 11u + ext : 3u + ext;
+      if (sym != 16) {
+        own = sym < 16 ? sym : 0u;
+        has = 1;
+      }
+    }
+    const bool bad_lane = ns > kClMaxSym;
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t t = __shfl_up(incl, d, 64);
+      if (lane >= (uint32_t)d) incl += t;
+    }
+    const uint32_t base = done + incl - cnt;
+    const uint64_t reach = __ballot(done + incl >= ntot);
+    const uint32_t lend = reach ? (uint32_t)__ffsll((unsigned long long)reach) - 1 : 63u;
+    // value entering each lane (for repeat codes): last defined value before it
+    uint32_t v = own, hv = has;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t v2 = __shfl_up(v, d, 64), h2 = __shfl_up(hv, d, 64);
+      if (lane >= (uint32_t)d && !hv) {
+        v = v2;
+        hv = h2;
+      }
+    }
+    uint32_t in_v = __shfl_up(v, 1, 64), in_h = __shfl_up(hv, 1, 64);
+    if (lane == 0 || !in_h) {
+      in_v = prevv;
+      in_h = have_prev;
+    }
+    // write this lane's runs
+    uint32_t i = base, last = in_v, hl = in_h, xe = a;
+    bool bad = bad_lane;
+    if (lane <= lend) {
+      for (uint32_t j = 0; j < ns && j < kClMaxSym && i < ntot; ++j) {
+        const uint32_t en = C.ent[lane][j], sym = en & 31, ext = (en >> 5) & 127;
+        uint32_t val, rep;
+        if (sym < 16) { val = sym; rep = 1; }
+        else if (sym == 16) { val = last; rep = 3 + ext; bad |= !hl; }
+        else if (sym == 17) { val = 0; rep = 3 + ext; }
+        else { val = 0; rep = 11 + ext; }
+        if (i + rep > ntot) { bad = true; break; }
+        for (uint32_t k = 0; k < rep; ++k) L.lens[i + k] = (uint8_t)val;
+        i += rep;
+        last = val;
+        hl = 1;
+        xe += en >> 12;
+      }
+    }
+    if (__ballot(bad)) return DH_TRUNC;
+    if (reach) {  // this window completes the header: end = after lane lend's last used symbol
+      const uint32_t end = (uint32_t)__shfl(xe, (int)lend, 64);
+      if (end > E) return DH_TRUNC;
+      *end_pos = rfl(end);
+      break;
+    }
+    const uint32_t tot = (uint32_t)__shfl(incl, 63, 64);
+    if (tot == 0) return DH_TRUNC;  // no progress (ran past the staged window)
+    done += tot;
+    prevv = (uint32_t)__shfl(v, 63, 64);
+    have_prev = (uint32_t)__shfl(hv, 63, 64) | have_prev;
+    p = rfl((uint32_t)__shfl(x, 63, 64));
+  }
+  wave_sync();
+  if (rfl(L.lens[256]) == 0) return DH_TRUNC;
+  if (rfl(build_table(L, L.lens, (int)hlit, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit, L.litsub, kLitSubCap)) ||
+      rfl(build_table(L, L.lens + hlit, (int)hdist, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist, L.distsub,
+                      kDistSubCap)))
+    return DH_TRUNC;
+  pair_literals(L);
+  return DH_OK;
+}
+
 // First DEFLATE block of every BGZF block: header + tables built ahead of the
 // decode kernel, one wave per block at high occupancy, so the serial header
 // work of one block overlaps the others instead of idling a decode workgroup.
@@ -837,6 +981,7 @@ __global__ __launch_bounds__(64) void k_huff_tables(const uint8_t* __restrict__ 
                                                     HuffTableInfo* __restrict__ tinfo) {
   __shared__ __attribute__((aligned(16))) HuffLds L;
   __shared__ __attribute__((aligned(16))) uint4 s_in[kTabStageBytes / 16 + 1];
+  __shared__ ClLds C;
   const uint32_t lane = lane_id();
   const uint32_t bi = b0 + blockIdx.x;
   const BlockInfo blk = blocks[bi];
@@ -857,12 +1002,13 @@ __global__ __launch_bounds__(64) void k_huff_tables(const uint8_t* __restrict__ 
     if (R.pos() + 3 <= E && (((uint32_t)R.buf >> 1) & 3u) == 2u) {
       const uint32_t fin = (uint32_t)R.buf & 1u;
       R.consume(3);
-      if (dyn_header(L, R, E) == DH_OK) {
+      uint32_t b0pos = 0;
+      if (dyn_header_par(L, C, R.W, R.pos(), E, &b0pos) == DH_OK) {
         wave_sync();
         uint4* __restrict__ dst = reinterpret_cast<uint4*>(tables + (uint64_t)blockIdx.x * kTableImage);
         const uint4* img = reinterpret_cast<const uint4*>(&L);
         for (uint32_t i = lane; i < kTableImage / 16; i += 64) dst[i] = img[i];
-        ti = HuffTableInfo{0u, R.pos(), fin, 0u};
+        ti = HuffTableInfo{0u, b0pos, fin, 0u};
       }
     }
   }
@@ -1424,6 +1570,16 @@ __device__ __forceinline__ bool dead_in_record(const ChainEnv& E, uint64_t q, in
   return bs > 32 && is_dead(E, q + 36);
 }
 
+// Is any dead position within [q, q + 40] (header fields + first rest byte)?
+__device__ __forceinline__ bool dead_near(const ChainEnv& E, uint64_t q) {
+  uint32_t lo = 0, hi = E.ndead;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (E.dead[mid] < q) lo = mid + 1; else hi = mid;
+  }
+  return lo < E.ndead && E.dead[lo] <= q + 40;
+}
+
 // Necessary conditions for a record of a well-formed BAM (guess only; the
 // true chain is fixed by the link step, never by this test).
 __device__ __forceinline__ bool plausible(const ChainEnv& E, uint64_t q) {
@@ -1819,6 +1975,8 @@ __global__ __launch_bounds__(64) void k_rec_cand(ChainEnv E, uint64_t* __restric
 }
 
 constexpr int kGuessLookahead = 4;  // plausible records required past a guess walk's exit
+constexpr uint32_t kListPlausible = 0x80000000u;  // wcnt flag: the list came from a plausible() walk
+constexpr uint32_t kListCountMask = 0x7fffffffu;
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_rec_walk(ChainEnv E, const uint64_t* __restrict__ cand,
@@ -1853,6 +2011,7 @@ __global__ __launch_bounds__(256) void k_rec_walk(ChainEnv E, const uint64_t* __
   uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
   uint64_t g = kNone, x = kNone;
   uint32_t n = 0;
+  bool plaus_list = false;  // every listed record passed plausible()
   const bool live = bend > E.p0 && b.ustart < E.q_end && b.isize > 0;
   if (live && f != kForceEmpty) {
     uint64_t entry = f;
@@ -1895,6 +2054,7 @@ __global__ __launch_bounds__(256) void k_rec_walk(ChainEnv E, const uint64_t* __
           g = c;
           x = q;
           n = m;
+          plaus_list = true;
           break;
         }
         for (++c; c < bend && !plausible(E, c); ++c) {}
@@ -1904,7 +2064,7 @@ __global__ __launch_bounds__(256) void k_rec_walk(ChainEnv E, const uint64_t* __
   if (n > kListCap) atomicOr(overflow, 1u);
   g_out[i] = g;
   x_out[i] = x;
-  wcnt[i] = n;
+  wcnt[i] = n | (plaus_list ? kListPlausible : 0u);
 }
 
 // Parallel link check (in = exclusive max-scan of the guess exits).  Entries
@@ -1977,7 +2137,12 @@ __global__ __launch_bounds__(64) void k_rec_check(ChainEnv E, const uint64_t* __
   if (e != kNone) {
     const BlockInfo b = E.blocks[E.k0 + i];
     const uint64_t lim = min(b.ustart + b.isize, E.q_end);
-    const uint32_t n = min(wcnt[i], kListCap);
+    const uint32_t wc = wcnt[i];
+    const uint32_t n = min(wc & kListCountMask, kListCap);
+    // a plausible() list on fully inflated data already satisfies every rule
+    // that reads the record (block_size >= 32, refID / mate refID in range,
+    // record inside the stream): only span end and dead positions remain
+    const bool light = (wc & kListPlausible) && E.e_inf == E.e_true;
     const uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
     count = n;
     for (uint32_t r0 = 0; r0 < n; r0 += 64) {
@@ -1990,6 +2155,8 @@ __global__ __launch_bounds__(64) void k_rec_check(ChainEnv E, const uint64_t* __
         const uint64_t avail = E.e_true - q;
         if (q >= lim) {
           stop = true;  // outside the span
+        } else if (light && !dead_near(E, q)) {
+          // all rules pass without reading the record
         } else if (MODE == kReader) {
           const bool first = r == 0 && q == E.p0;  // first record follows a seek
           if (!first && is_dead(E, q)) {
@@ -2110,8 +2277,10 @@ static inline unsigned grid_for(uint64_t n, unsigned bs, unsigned cap = 65535u *
 
 hipError_t launch_bgzf_scan(const uint8_t* file, uint64_t lo, uint64_t hi, uint64_t* cand, uint32_t cap,
                             uint32_t* count, hipStream_t s) {
-  uint64_t nd = (hi - (lo & ~3ull) + 3) / 4;
-  hipLaunchKernelGGL(k_bgzf_scan, dim3(grid_for(nd, 256, 8192)), dim3(256), 0, s, file, lo, hi, cand, cap, count);
+  // file + lo is the start of the device buffer (hipMalloc: 256 B aligned)
+  const uint64_t nc = (hi - lo + 15) / 16;
+  hipLaunchKernelGGL(k_bgzf_scan, dim3(grid_for(nc, 256, 8192)), dim3(256), 0, s, file + lo, hi - lo, lo, cand, cap,
+                     count);
   return hipGetLastError();
 }
 hipError_t launch_bgzf_verify(const uint8_t* file, uint64_t lo, uint64_t hi, const uint64_t* cand, uint32_t n,
