@@ -57,6 +57,44 @@ def cpu_baseline(data, info, seconds):
                       f"oracle/hbam_oracle.c (system zlib) single thread, {dt:.1f} s"}
 
 
+def extra_configs(c2, c2_info):
+    """Side measurements reported next to the headline (not part of `value`):
+    C5-style .splitting-bai generation (g=4096) over the same C2 BAM through
+    the SplittingBAMIndexer entry point (hbam_build_splitting_index: inflate +
+    indexer-rule chain + entry emit, file resident in HBM), and a C4-like
+    long-read BAM (ONT-style 10-50 kb reads, records spanning blocks) through
+    the same device pipeline as the headline."""
+    import hbam
+    from hbam import synth
+    res = {}
+    f = hbam.BamFile(c2.tobytes() if hasattr(c2, "tobytes") else c2)
+    t = time.perf_counter()
+    sbi = f.splitting_index(4096)
+    dt = time.perf_counter() - t
+    res["c5_splitting_bai_g4096_on_c2"] = {
+        "entries": len(sbi) // 8, "seconds": round(dt, 4),
+        "uncompressed_GBps": round(c2_info["uncompressed"] / dt / 1e9, 3),
+        "note": "first call: includes inflating every block (resident compressed file)"}
+    f.close()
+    data, info = synth.make_bam(3000, mode="long", as_numpy=True, seed=0x48424D04)
+    g = hbam.Gpu(0)
+    g.load(data)
+    g.run(timing=True)
+    ts = []
+    for _ in range(3):
+        t = time.perf_counter()
+        st = g.run(timing=True)
+        ts.append(time.perf_counter() - t)
+    dt = min(ts)
+    res["c4_long_reads"] = {
+        "records": int(st["records"]), "compressed_bytes": info["compressed"],
+        "uncompressed_bytes": info["uncompressed"], "seconds": round(dt, 5),
+        "uncompressed_GBps": round(info["uncompressed"] / dt / 1e9, 3),
+        "stages_ms": {k: round(st[k], 3) for k in ("ms_locate", "ms_huff", "ms_lz77", "ms_chain", "ms_decode")}}
+    g.close()
+    return res
+
+
 def pmc_traffic(kernels):
     """HBM bytes per launch of `kernels` (summed) from the newest committed
     rocprofv3 PMC summary (profiles/*/summary.json, written by
@@ -86,6 +124,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save-bam", default=None)
+    ap.add_argument("--no-extra", action="store_true", help="skip the C4 / index side measurements")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -183,6 +222,9 @@ def main():
                      "alg_bytes_per_launch": int(alg_bytes)},
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1 and not args.no_extra:
+        g.close()
+        out["extra"] = extra_configs(data, info)
     if rank == 0 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(data.tobytes(), info, args.cpu_seconds)

@@ -1601,6 +1601,14 @@ __device__ __forceinline__ bool plausible(const ChainEnv& E, uint64_t q) {
   return E.u[q + 36 + lrn - 1] == 0;
 }
 
+// plausible() at q and at the record after it (or the end / unreadable data):
+// a cheap second check that removes most false candidates inside long records.
+__device__ __forceinline__ bool plausible2(const ChainEnv& E, uint64_t q) {
+  if (!plausible(E, q)) return false;
+  const uint64_t q2 = q + 4 + (uint64_t)(int32_t)ldu32(E.u, q);
+  return q2 == E.e_true || q2 + 36 > E.e_inf || plausible(E, q2);
+}
+
 // One chain step from q under the given rules.  Returns false if the walk
 // cannot continue (data unavailable or malformed record); *nq = next position.
 template <int MODE>
@@ -1964,7 +1972,7 @@ __global__ __launch_bounds__(64) void k_rec_cand(ChainEnv E, uint64_t* __restric
   if (bend > E.p0 && b.ustart > E.p0 && b.ustart < E.q_end && b.isize > 0) {
     for (uint64_t c0 = b.ustart; c0 < bend; c0 += 64) {
       const uint64_t p = c0 + lane;
-      const uint64_t m = __ballot(p < bend && plausible(E, p));
+      const uint64_t m = __ballot(p < bend && plausible2(E, p));
       if (m) {
         c = c0 + (uint64_t)(__ffsll((long long)m) - 1);
         break;
@@ -1975,6 +1983,7 @@ __global__ __launch_bounds__(64) void k_rec_cand(ChainEnv E, uint64_t* __restric
 }
 
 constexpr int kGuessLookahead = 4;  // plausible records required past a guess walk's exit
+constexpr uint64_t kRetry = ~0ull - 2;  // g[]: the candidate's walk failed, search on
 constexpr uint32_t kListPlausible = 0x80000000u;  // wcnt flag: the list came from a plausible() walk
 constexpr uint32_t kListCountMask = 0x7fffffffu;
 
@@ -2027,8 +2036,8 @@ __global__ __launch_bounds__(256) void k_rec_walk(ChainEnv E, const uint64_t* __
       }
       x = q;
     } else {
-      uint64_t c = cand[i];
-      while (c < bend) {  // c == kNone (no candidate): nothing to walk
+      const uint64_t c = cand[i];
+      if (c < bend) {  // c == kNone (no candidate): nothing to walk
         uint64_t q = c;
         uint32_t m = 0;
         bool valid = true;
@@ -2055,9 +2064,10 @@ __global__ __launch_bounds__(256) void k_rec_walk(ChainEnv E, const uint64_t* __
           x = q;
           n = m;
           plaus_list = true;
-          break;
+        } else {
+          g = kRetry;  // later candidates: k_rec_search (wave per block)
+          n = 0;
         }
-        for (++c; c < bend && !plausible(E, c); ++c) {}
       }
     }
   }
@@ -2065,6 +2075,64 @@ __global__ __launch_bounds__(256) void k_rec_walk(ChainEnv E, const uint64_t* __
   g_out[i] = g;
   x_out[i] = x;
   wcnt[i] = n | (plaus_list ? kListPlausible : 0u);
+}
+
+// Blocks whose first candidate failed (k_rec_walk: g == kRetry): one wave
+// per block tries the later candidates in order (64 positions per step, a
+// wave-uniform walk per candidate), as BAMSplitGuesser tries candidate after
+// candidate; the valid one's records are listed by lane 0.
+template <int MODE>
+__global__ __launch_bounds__(64) void k_rec_search(ChainEnv E, const uint64_t* __restrict__ cand,
+                                                   uint64_t* __restrict__ g_out, uint64_t* __restrict__ x_out,
+                                                   uint32_t* __restrict__ wcnt, uint16_t* __restrict__ list,
+                                                   uint32_t* __restrict__ overflow) {
+  const uint32_t i = blockIdx.x;
+  if (g_out[i] != kRetry) return;
+  const uint32_t lane = lane_id();
+  const BlockInfo b = E.blocks[E.k0 + i];
+  const uint64_t bend = b.ustart + b.isize;
+  uint64_t g = kNone, x = kNone;
+  for (uint64_t c0 = cand[i] + 1; c0 < bend && g == kNone; c0 += 64) {
+    const uint64_t p = c0 + lane;
+    uint64_t m = __ballot(p < bend && plausible2(E, p));
+    while (m) {
+      const uint64_t c = c0 + (uint64_t)(__ffsll((long long)m) - 1);
+      m &= m - 1;
+      uint64_t q = c;
+      bool valid = true;
+      while (q < bend) {
+        if (!plausible(E, q)) { valid = false; break; }
+        q += 4 + (uint64_t)(int32_t)ldu32(E.u, q);
+      }
+      if (valid) {
+        uint64_t y = q;
+        for (int k = 0; k < kGuessLookahead; ++k) {
+          if (y == E.e_true || y + 36 > E.e_inf) break;
+          if (!plausible(E, y)) { valid = false; break; }
+          y += 4 + (uint64_t)(int32_t)ldu32(E.u, y);
+        }
+      }
+      if (valid) {
+        g = c;
+        x = q;
+        break;
+      }
+    }
+  }
+  if (lane == 0) {
+    uint32_t n = 0;
+    if (g != kNone) {
+      uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
+      for (uint64_t q = g; q < bend; q += 4 + (uint64_t)(int32_t)ldu32(E.u, q)) {
+        if (n < kListCap) L[n] = (uint16_t)(q - b.ustart);
+        ++n;
+      }
+      if (n > kListCap) atomicOr(overflow, 1u);
+    }
+    g_out[i] = g;
+    x_out[i] = x;
+    wcnt[i] = n | (g != kNone ? kListPlausible : 0u);
+  }
 }
 
 // Parallel link check (in = exclusive max-scan of the guess exits).  Entries
@@ -2399,10 +2467,14 @@ hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s) 
         hipLaunchKernelGGL(k_rec_cand<kReader>, dim3(nb), dim3(64), 0, s, E, a.cand);
         hipLaunchKernelGGL(k_rec_walk<kReader>, dim3((nb + 255) / 256), dim3(256), 0, s, E, a.cand, nullptr, a.g,
                            a.x, a.wcnt, a.list, a.counters + 2, false);
+        hipLaunchKernelGGL(k_rec_search<kReader>, dim3(nb), dim3(64), 0, s, E, a.cand, a.g, a.x, a.wcnt, a.list,
+                           a.counters + 2);
       } else {
         hipLaunchKernelGGL(k_rec_cand<kIndexer>, dim3(nb), dim3(64), 0, s, E, a.cand);
         hipLaunchKernelGGL(k_rec_walk<kIndexer>, dim3((nb + 255) / 256), dim3(256), 0, s, E, a.cand, nullptr, a.g,
                            a.x, a.wcnt, a.list, a.counters + 2, false);
+        hipLaunchKernelGGL(k_rec_search<kIndexer>, dim3(nb), dim3(64), 0, s, E, a.cand, a.g, a.x, a.wcnt, a.list,
+                           a.counters + 2);
       }
       break;
     }

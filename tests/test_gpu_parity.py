@@ -209,3 +209,40 @@ def test_record_errors_match_oracle(rec, off, val, code):
         got = f.decode_all(raise_on_error=False)
         assert got["status"] == code
         assert_same_records(got, want)
+
+
+def test_c2_full_size_vs_oracle():
+    """BASELINE config C2 at full size (10 M records, 0.93 GB BGZF): every key
+    and voff of the device pipeline and the .splitting-bai (g = 4096) through
+    the SplittingBAMIndexer entry point, bit-exact against the oracle."""
+    data, info = synth.make_bam(10_000_000, as_numpy=True)
+    raw = data.tobytes()
+    g = hbam.Gpu(0)
+    g.load(data)
+    st = g.run()
+    assert st["status"] == 0 and st["records"] == 10_000_000
+    keys, voffs = g.fetch(st["records"])
+    g.close()
+    s = orc.Stream(raw)
+    rc, want = s.decode_all()
+    assert rc == 0
+    np.testing.assert_array_equal(voffs, want["voff"])
+    np.testing.assert_array_equal(keys, want["key"])
+    want_sbi = s.splitting_index(4096)
+    del want, s
+    with hbam.BamFile(raw) as f:
+        assert f.splitting_index(4096) == want_sbi
+
+
+def test_c4_long_reads_vs_oracle():
+    """C4-like ONT reads (10-50 kb, records spanning several BGZF blocks, heavy
+    aux tags, 10 % unmapped -> Murmur over ~100 KB rests)."""
+    data, info = synth.make_bam(600, mode="long", seed=0x48424D04)
+    s = orc.Stream(data)
+    rc, want = s.decode_all()
+    assert rc == 0
+    with hbam.BamFile(data) as f:
+        got = f.decode_all()
+        assert_same_records(got, want, s.data)
+        for gran in (1, 5, 4096):
+            assert f.splitting_index(gran) == s.splitting_index(gran)
