@@ -193,6 +193,10 @@ __global__ void k_block_ustart(BlockInfo* __restrict__ blocks, uint32_t n, const
 #endif
 constexpr int kHuffThreads = HBAM_HUFF_THREADS;
 constexpr int kHuffWaves = kHuffThreads / 64;
+#ifndef HBAM_HUFF_STAGE
+#define HBAM_HUFF_STAGE 1
+#endif
+constexpr bool kHuffStage = HBAM_HUFF_STAGE != 0;  // compressed block staged in LDS
 
 // Wave-local ordering of LDS traffic (code run by one wave only).
 __device__ __forceinline__ void wave_sync() {
@@ -1070,9 +1074,11 @@ __global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(co
   const uint64_t abase = sbyte & ~15ull;
   const HuffTableInfo ti = tinfo[blockIdx.x];
   {  // stage the block (+16 B of zero-padded file) and its prebuilt tables in LDS
-    const uint32_t nq = (uint32_t)((blk.coff + blk.csize - abase + 15) >> 4) + 1;
-    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(file + abase);
-    for (uint32_t i = tid; i < nq; i += kHuffThreads) s_in[i] = src[i];
+    if (kHuffStage) {
+      const uint32_t nq = (uint32_t)((blk.coff + blk.csize - abase + 15) >> 4) + 1;
+      const uint4* __restrict__ src = reinterpret_cast<const uint4*>(file + abase);
+      for (uint32_t i = tid; i < nq; i += kHuffThreads) s_in[i] = src[i];
+    }
     if (ti.status == 0) {
       const uint4* __restrict__ tsrc = reinterpret_cast<const uint4*>(tables + (uint64_t)blockIdx.x * kTableImage);
       uint4* tdst = reinterpret_cast<uint4*>(&L);
@@ -1081,7 +1087,9 @@ __global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(co
   }
   __syncthreads();
   PROF_T(0);
-  const uint32_t* __restrict__ W = reinterpret_cast<const uint32_t*>(s_in);
+  // compressed bits: the LDS copy, or (HBAM_HUFF_STAGE=0) the file in HBM
+  const uint32_t* __restrict__ W =
+      kHuffStage ? reinterpret_cast<const uint32_t*>(s_in) : reinterpret_cast<const uint32_t*>(file + abase);
   const uint32_t E = 8u * ((uint32_t)(sbyte - abase) + (blk.csize - 26));  // end of CDATA (bits from W)
 
   SReader R;  // wave 0's reader
@@ -2400,7 +2408,7 @@ static hipError_t launch_huff(const uint8_t* file, const BlockInfo* blocks, uint
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  const uint32_t lds = kHuffStaticBytes + ((max_stage + 15) & ~15u);
+  const uint32_t lds = kHuffStaticBytes + (kHuffStage ? ((max_stage + 15) & ~15u) : 0u);
   hipLaunchKernelGGL(k_inflate_huff, dim3(nb), dim3(kHuffThreads), lds, s, file, blocks, b0, chunk_ustart, tokens,
                      hout, tables, tinfo, g_huff_prof);
   return hipGetLastError();

@@ -11,7 +11,10 @@
 namespace hbam {
 
 namespace {
-constexpr uint32_t kInflateChunkBlocks = 16384;  // blocks per phase-A/B launch pair
+#ifndef HBAM_INFLATE_CHUNK
+#define HBAM_INFLATE_CHUNK 16384
+#endif
+constexpr uint32_t kInflateChunkBlocks = HBAM_INFLATE_CHUNK;  // blocks per phase-A/B launch pair
 constexpr int kMaxChainIters = 64;
 constexpr int kMaxLinkFix = 4;  // re-walk rounds before the serial link
 }  // namespace
@@ -21,14 +24,20 @@ Pipeline::Pipeline(int device) : device_(device) {
     err_ = "hipSetDevice failed";
     return;
   }
-  if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) err_ = "hipStreamCreate failed";
+  if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&stream_b_, hipStreamNonBlocking) != hipSuccess)
+    err_ = "hipStreamCreate failed";
   for (auto& e : ev_) (void)hipEventCreate(&e);
+  for (auto& e : sync_ev_) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
 }
 
 Pipeline::~Pipeline() {
   (void)hipSetDevice(device_);
   if (own_file_ && dfile_) (void)hipFree(dfile_);
   for (auto& e : ev_) (void)hipEventDestroy(e);
+  for (auto& e : sync_ev_) (void)hipEventDestroy(e);
+  for (auto& e : tev_) (void)hipEventDestroy(e);
+  if (stream_b_) (void)hipStreamDestroy(stream_b_);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -177,8 +186,15 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force) {
     HIPCHK(hipMemsetAsync(lzprof.p, 0, 8ull * nblk * 8, stream_));
     g_lz_prof = lzprof.p;
   }
+  // Chunks of up to kInflateChunkBlocks blocks.  Phase A of chunk j runs on
+  // stream_, phase B on stream_b_ after it; token buffers alternate by chunk
+  // parity, so phase A of chunk j+1 overlaps phase B of chunk j (phase A needs
+  // ~12 KiB of LDS per workgroup and fits beside a phase-B workgroup on a CU).
+  // HBAM_INFLATE_SERIAL=1 keeps both phases on stream_ (comparison runs).
+  static const bool serial = getenv("HBAM_INFLATE_SERIAL") != nullptr;
+  struct Chunk { uint32_t b, e; };
+  std::vector<Chunk> chunks;
   uint32_t b = b0;
-  bool any = false;
   while (b < b1) {
     if (!force && inflated_[b]) { ++b; continue; }
     // even chunks (a short last chunk would pay a whole wave tail for few blocks)
@@ -187,38 +203,79 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force) {
     const uint32_t per = (left + nchunks - 1) / nchunks;
     uint32_t e = b;
     while (e < b1 && e - b < per && (force || !inflated_[e])) ++e;
-    const uint64_t cu = hblocks_[b].ustart;
-    const uint64_t uend = hblocks_[e - 1].ustart + hblocks_[e - 1].isize;
-    HIPCHK(tokens_.reserve(std::max<uint64_t>(uend - cu, 64)));
+    chunks.push_back({b, e});
+    b = e;
+  }
+  const bool any = !chunks.empty();
+  const size_t nc = chunks.size();
+  if (timing && tev_.size() < 3 * nc) {
+    const size_t old = tev_.size();
+    tev_.resize(3 * nc);
+    for (size_t i = old; i < tev_.size(); ++i) HIPCHK(hipEventCreate(&tev_[i]));
+  }
+  // size every buffer up front: a reallocation inside the loop could free a
+  // token buffer that phase B of an earlier chunk is still reading
+  uint64_t max_u = 64, max_nb = 0;
+  for (const Chunk& c : chunks) {
+    max_u = std::max(max_u, hblocks_[c.e - 1].ustart + hblocks_[c.e - 1].isize - hblocks_[c.b].ustart);
+    max_nb = std::max<uint64_t>(max_nb, c.e - c.b);
+  }
+  if (any) {
+    for (int i = 0; i < (nc > 1 ? 2 : 1); ++i) HIPCHK(tokens_[i].reserve(max_u));
+    HIPCHK(tables_.reserve(max_nb * kHuffTableImage));
+    HIPCHK(tinfo_.reserve(max_nb));
+  }
+  hipStream_t sb = serial ? stream_ : stream_b_;
+  if (!serial && any) {  // phase B must see everything queued on stream_ before this call
+    HIPCHK(hipEventRecord(sync_ev_[0], stream_));
+    HIPCHK(hipStreamWaitEvent(sb, sync_ev_[0], 0));
+  }
+  for (size_t j = 0; j < nc; ++j) {
+    const uint32_t cb = chunks[j].b, ce = chunks[j].e;
+    const int par = (int)(j & 1);
+    const uint64_t cu = hblocks_[cb].ustart;
     uint32_t max_stage = 0;
-    for (uint32_t k = b; k < e; ++k) max_stage = std::max(max_stage, huff_stage_bytes(hblocks_[k]));
-    HIPCHK(tables_.reserve((uint64_t)(e - b) * kHuffTableImage));
-    HIPCHK(tinfo_.reserve(e - b));
-    if (timing) {
-      HIPCHK(hipEventRecord(ev_[4], stream_));
-      HIPCHK(launch_inflate_huff(fbase, dblocks_.p, b, e - b, cu, tokens_.p, hout_.p, max_stage, tables_.p,
-                                 tinfo_.p, stream_));
-      HIPCHK(hipEventRecord(ev_[5], stream_));
-      HIPCHK(launch_inflate_lz77(dblocks_.p, b, e - b, cu, tokens_.p, hout_.p, du_.p, stream_));
-      HIPCHK(hipEventRecord(ev_[6], stream_));
-      HIPCHK(hipEventSynchronize(ev_[6]));
+    for (uint32_t k = cb; k < ce; ++k) max_stage = std::max(max_stage, huff_stage_bytes(hblocks_[k]));
+    if (!serial && j >= 2) HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + par], 0));  // B(j-2) released the buffer
+    if (timing) HIPCHK(hipEventRecord(tev_[3 * j], stream_));
+    HIPCHK(launch_inflate_huff(fbase, dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, max_stage, tables_.p,
+                               tinfo_.p, stream_));
+    if (timing) HIPCHK(hipEventRecord(tev_[3 * j + 1], stream_));
+    if (!serial) {
+      HIPCHK(hipEventRecord(sync_ev_[par], stream_));
+      HIPCHK(hipStreamWaitEvent(sb, sync_ev_[par], 0));
+    }
+    HIPCHK(launch_inflate_lz77(dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, du_.p, sb));
+    if (timing) HIPCHK(hipEventRecord(tev_[3 * j + 2], sb));
+    if (!serial) HIPCHK(hipEventRecord(sync_ev_[2 + par], sb));
+    for (uint32_t k = cb; k < ce; ++k) inflated_[k] = 1;
+    ++inflate_launches_;
+  }
+  if (!serial && any) {  // everything after this call on stream_ sees phase B done
+    HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + ((nc - 1) & 1)], 0));
+    if (nc >= 2) HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + ((nc - 2) & 1)], 0));
+  }
+  if (timing && any) {
+    // phase A: its launch on stream_; phase B: from max(A done, previous B done)
+    HIPCHK(hipEventSynchronize(tev_[3 * nc - 1]));
+    for (size_t j = 0; j < nc; ++j) {
       float a = 0, c = 0;
-      (void)hipEventElapsedTime(&a, ev_[4], ev_[5]);
-      (void)hipEventElapsedTime(&c, ev_[5], ev_[6]);
+      (void)hipEventElapsedTime(&a, tev_[3 * j], tev_[3 * j + 1]);
+      hipEvent_t from = tev_[3 * j + 1];
+      if (j > 0) {
+        float d = 0;
+        (void)hipEventElapsedTime(&d, tev_[3 * j + 1], tev_[3 * j - 1]);
+        if (d > 0) from = tev_[3 * j - 1];
+      }
+      (void)hipEventElapsedTime(&c, from, tev_[3 * j + 2]);
       huff_ms += a;
       lz_ms += c;
-    } else {
-      HIPCHK(launch_inflate(fbase, dblocks_.p, b, e - b, cu, tokens_.p, hout_.p, du_.p, max_stage, tables_.p,
-                            tinfo_.p, stream_));
     }
-    for (uint32_t k = b; k < e; ++k) inflated_[k] = 1;
-    ++inflate_launches_;
-    any = true;
-    b = e;
   }
   g_huff_prof = nullptr;
   g_lz_prof = nullptr;
   if (prof_this && any) {
+    HIPCHK(hipStreamSynchronize(stream_));
     std::vector<uint64_t> hl(8ull * nblk);
     HIPCHK(hipMemcpy(hl.data(), lzprof.p, hl.size() * 8, hipMemcpyDeviceToHost));
     double la[6] = {0};

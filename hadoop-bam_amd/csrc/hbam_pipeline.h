@@ -112,6 +112,7 @@ class Pipeline {
 
   int device_ = 0;
   hipStream_t stream_ = nullptr;
+  hipStream_t stream_b_ = nullptr;  // inflate phase B (overlaps phase A of the next chunk)
   std::string err_;
 
   uint8_t* dfile_ = nullptr;
@@ -129,7 +130,7 @@ class Pipeline {
 
   DevBuf<uint8_t> du_;
   std::vector<uint8_t> inflated_;  // per block flag
-  DevBuf<uint32_t> tokens_;
+  DevBuf<uint32_t> tokens_[2];  // double-buffered LZ77 token streams (chunk parity)
   DevBuf<HuffOut> hout_;
   DevBuf<uint8_t> tables_;        // phase-A prebuilt table images (per chunk)
   DevBuf<HuffTableInfo> tinfo_;
@@ -149,6 +150,8 @@ class Pipeline {
   uint64_t cols_cap_ = 0;
 
   hipEvent_t ev_[8];
+  hipEvent_t sync_ev_[4];           // [0,1] phase A done, [2,3] phase B done, per token buffer
+  std::vector<hipEvent_t> tev_;     // timing events of overlapped inflate chunks
 };
 
 }  // namespace hbam
