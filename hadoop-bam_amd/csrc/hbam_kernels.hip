@@ -680,6 +680,18 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
   return ev;
 }
 
+// Inclusive wave scan on DPP (VALU lane moves, no LDS round trip): Hillis-Steele
+// inside each 16-lane row, then row_bcast:15 / row_bcast:31 carry the row totals.
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);   // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);   // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const uint32_t lane = lane_id();
 #pragma unroll
@@ -1365,6 +1377,16 @@ constexpr int kLzThreads = 1024;
 constexpr int kLzWaves = kLzThreads / 64;
 constexpr uint32_t kMapMax = 65280;
 constexpr uint32_t kLitTag = 0xFF00u;
+// phase-B resolve: raw entries loaded this many rounds ahead (1 measured best)
+#ifndef HBAM_LZ_PF
+#define HBAM_LZ_PF 1
+#endif
+constexpr int kLzPf = HBAM_LZ_PF;
+// phase-B fill: 64-token groups loaded ahead (4 vs 8 measured equal)
+#ifndef HBAM_LZ_RING
+#define HBAM_LZ_RING 4
+#endif
+constexpr int kLzRing = HBAM_LZ_RING;
 
 // exclusive scan over the workgroup; returns the prefix, *total = sum
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
@@ -1442,9 +1464,10 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
   // map index = o0 + position, so 16-byte output segments read 32 B-aligned LDS
   __shared__ __attribute__((aligned(16))) uint16_t map[kMapMax + 32];
   __shared__ uint32_t scratch[kLzWaves];
-  // optional cycle profile (thread 0): [0] token scan [2] map fill
-  // [3] resolve [4] store [5] total ([1] unused)
-  uint64_t pacc[6] = {0, 0, 0, 0, 0, 0};
+  // optional cycle profile (thread 0): [6] token loads [0] block scan
+  // [1] map fill (wave 0's own work) [2] fill barrier wait [3] resolve
+  // [4] store [5] total
+  uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t pt = prof ? clock64() : 0, pt0 = pt;
 #define LZ_T(i)                             \
   do {                                      \
@@ -1483,38 +1506,102 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
     return;
   }
 
-  // 1. contiguous token range per thread; output position by block scan
-  const uint32_t K = (ntok + kLzThreads - 1) / kLzThreads;
-  const uint32_t t0 = min(tid * K, ntok), t1 = min(t0 + K, ntok);
-  uint32_t nbytes = 0;
-  for (uint32_t i = t0; i < t1; ++i) nbytes += tok_len(tk[i]);
-  uint32_t total;
-  uint32_t p = block_excl_scan(nbytes, scratch, &total);
+  // 1. wave w expands tokens [w*TW, (w+1)*TW); its output range starts at
+  //    the byte total of the waves before it (coalesced token loads).
+  const uint32_t wid = tid >> 6, lane = tid & 63;
+  const uint32_t TW = (ntok + kLzWaves - 1) / kLzWaves;
+  const uint32_t tw0 = min(wid * TW, ntok), tw1 = min(tw0 + TW, ntok);
+  uint32_t wsum = 0;
+  for (uint32_t i0 = tw0 + lane; i0 < tw1 + lane; i0 += 8 * 64) {  // 8 loads in flight
+    uint32_t tv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) tv[k] = i0 + 64 * k < tw1 ? tk[i0 + 64 * k] : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) wsum += i0 + 64 * k < tw1 ? tok_len(tv[k]) : 0u;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) wsum += __shfl_xor(wsum, d, 64);
+  LZ_T(6);
+  if (lane == 0) scratch[wid] = wsum;
+  __syncthreads();
+  uint32_t P = 0;
+#pragma unroll
+  for (int w = 0; w < kLzWaves; ++w) P += (uint32_t)w < wid ? scratch[w] : 0u;
+  const uint32_t whi = min(P + wsum, isize);  // end of this wave's range (the last token may run past ISIZE)
   LZ_T(0);
 
-  // 2. expand tokens into the map (the last token may run past ISIZE: clamp)
+  // 2. map fill, 64 tokens (one per lane) at a time.  A token is an
+  //    arithmetic run of entries base + k*delta (match: source position, 1;
+  //    literal pair: tag|b0, b1-b0).  (i) every 8-entry aligned chunk that
+  //    starts inside a token is written whole by that token with one
+  //    ds_write_b128 -- entries past the token's end are wrong but belong to
+  //    later tokens of the same wave; (ii) then each token writes its head
+  //    (its entries before its first chunk boundary) one by one, overwriting
+  //    them.  Chunks never cross the wave's range end, so waves stay disjoint.
   uint16_t* m = map + o0;
-  for (uint32_t i = t0; i < t1 && p < isize; ++i) {
-    const uint32_t t = tk[i];
+  uint32_t ring[kLzRing];  // tokens of the next kLzRing groups (L2 hits after step 1)
+#pragma unroll
+  for (int k = 0; k < kLzRing; ++k) ring[k] = tw0 + lane + 64 * k < tw1 ? tk[tw0 + lane + 64 * k] : 0u;
+  for (uint32_t gi = tw0; gi < tw1 && P < whi; gi += 64) {  // wave-uniform
+    const uint32_t i = gi + lane;
+    const uint32_t t = ring[0];
+#pragma unroll
+    for (int k = 0; k + 1 < kLzRing; ++k) ring[k] = ring[k + 1];
+    ring[kLzRing - 1] = i + 64 * kLzRing < tw1 ? tk[i + 64 * kLzRing] : 0u;
+    const uint32_t len = i < tw1 ? tok_len(t) : 0u;
+    const uint32_t incl = wave_incl_scan_dpp(len);
+    const uint32_t pos = P + incl - len;
+    P += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const uint32_t end = min(pos + len, whi);
+    uint32_t base, delta;
     if (t >> 31) {
-      const uint32_t n = min(t & 0xffffu, isize - p);
-      const uint32_t src = p - (((t >> 16) & 0x7fffu) + 1);  // dist <= p: checked in phase A
-      for (uint32_t j = 0; j < n; ++j) m[p + j] = (uint16_t)(src + j);
-      p += n;
+      base = pos - (((t >> 16) & 0x7fffu) + 1);  // dist <= pos: checked in phase A
+      delta = 1;
     } else {
-      m[p] = (uint16_t)(kLitTag | (t & 0xffu));
-      if (((t >> 24) & 3u) == 2u && p + 1 < isize) m[p + 1] = (uint16_t)(kLitTag | ((t >> 8) & 0xffu));
-      p += (t >> 24) & 3u;
+      base = kLitTag | (t & 0xffu);
+      delta = (((t >> 8) & 0xffu) - (t & 0xffu)) & 0xffffu;
     }
+    const uint32_t hb = min(end, ((o0 + pos + 7) & ~7u) - o0);  // head end = first chunk start
+    for (uint32_t q = hb; q < end; q += 8) {
+      const uint32_t v0 = base + (q - pos) * delta;
+      if (q + 8 <= whi) {
+        const uint32_t d0 = (v0 & 0xffffu) | ((v0 + delta) << 16);
+        const uint32_t inc = (2u * delta) * 0x10001u;
+        *reinterpret_cast<uint4*>(m + q) = make_uint4(d0, d0 + inc, d0 + 2u * inc, d0 + 3u * inc);
+      } else {
+        uint32_t v = v0;
+        for (uint32_t r = q; r < whi; ++r, v += delta) m[r] = (uint16_t)v;
+      }
+    }
+    wave_sync();  // (i) before (ii): they overlap across lanes
+    uint32_t v = base;
+    for (uint32_t r = pos; r < hb; ++r, v += delta) m[r] = (uint16_t)v;
   }
+  LZ_T(1);
   __syncthreads();
   LZ_T(2);
 
   // 3. resolve, increasing positions first; results written back in place
-  for (uint32_t q = tid; q < isize; q += kLzThreads) {
-    uint32_t v = m[q];
-    while (v < kLitTag) v = m[v];
-    m[q] = (uint16_t)v;
+  //    (path compression).  Each round (1024 consecutive positions) costs one
+  //    dependent LDS latency per chase step, so the raw entries of this
+  //    thread's next positions (written by fill, rewritten only by this
+  //    thread) are loaded kLzPf rounds ahead.
+  {
+    uint32_t pre[kLzPf];
+#pragma unroll
+    for (int k = 0; k < kLzPf; ++k) {
+      const uint32_t q = tid + k * kLzThreads;
+      pre[k] = q < isize ? m[q] : kLitTag;
+    }
+    for (uint32_t q = tid; q < isize; q += kLzThreads) {
+      uint32_t v = pre[0];
+#pragma unroll
+      for (int k = 0; k + 1 < kLzPf; ++k) pre[k] = pre[k + 1];
+      const uint32_t qn = q + kLzPf * kLzThreads;
+      pre[kLzPf - 1] = qn < isize ? m[qn] : kLitTag;
+      while (v < kLitTag) v = m[v];
+      m[q] = (uint16_t)v;
+    }
   }
   __syncthreads();
   LZ_T(3);
@@ -1541,7 +1628,7 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
   LZ_T(4);
   if (prof && tid == 0) {
     pacc[5] = clock64() - pt0;
-    for (int i = 0; i < 6; ++i) prof[8ull * (b0 + blockIdx.x) + i] = pacc[i];
+    for (int i = 0; i < 8; ++i) prof[8ull * (b0 + blockIdx.x) + i] = pacc[i];
   }
 #undef LZ_T
 }

@@ -221,7 +221,7 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force) {
     max_nb = std::max<uint64_t>(max_nb, c.e - c.b);
   }
   if (any) {
-    for (int i = 0; i < (nc > 1 ? 2 : 1); ++i) HIPCHK(tokens_[i].reserve(max_u));
+    for (int i = 0; i < (nc > 1 ? 2 : 1); ++i) HIPCHK(tokens_[i].reserve(max_u + 16));  // phase B reads tokens as uint4
     HIPCHK(tables_.reserve(max_nb * kHuffTableImage));
     HIPCHK(tinfo_.reserve(max_nb));
   }
@@ -278,16 +278,16 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force) {
     HIPCHK(hipStreamSynchronize(stream_));
     std::vector<uint64_t> hl(8ull * nblk);
     HIPCHK(hipMemcpy(hl.data(), lzprof.p, hl.size() * 8, hipMemcpyDeviceToHost));
-    double la[6] = {0};
+    double la[8] = {0};
     uint64_t ln = 0;
     for (uint32_t k = b0; k < b1; ++k) {
       if (hl[8ull * k + 5] == 0) continue;
       ++ln;
-      for (int i = 0; i < 6; ++i) la[i] += (double)hl[8ull * k + i];
+      for (int i = 0; i < 8; ++i) la[i] += (double)hl[8ull * k + i];
     }
-    static const char* lnames[6] = {"scan", "-", "fill", "resolve", "store", "total"};
+    static const char* lnames[8] = {"scan", "fill_own", "fill_wait", "resolve", "store", "total", "loads", "-"};
     fprintf(stderr, "[lz77 prof] %llu blocks, mean cycles per block:", (unsigned long long)ln);
-    for (int i = 0; i < 6; ++i) fprintf(stderr, " %s=%.0f", lnames[i], ln ? la[i] / ln : 0.0);
+    for (int i = 0; i < 7; ++i) fprintf(stderr, " %s=%.0f", lnames[i], ln ? la[i] / ln : 0.0);
     fprintf(stderr, "\n");
     std::vector<uint64_t> h(16ull * nblk);
     HIPCHK(hipMemcpy(h.data(), prof.p, h.size() * 8, hipMemcpyDeviceToHost));

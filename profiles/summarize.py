@@ -77,6 +77,42 @@ def main_dispatch_durations(d):
     return out
 
 
+INFLATE = ("hbam::k_huff_tables", "hbam::k_inflate_huff", "hbam::k_inflate_lz77")
+
+
+def inflate_stage_spans(d):
+    """The inflate stage runs phase A (k_huff_tables + k_inflate_huff, pipeline
+    stream) of chunk j+1 concurrently with phase B (k_inflate_lz77, second
+    stream) of chunk j, so per-kernel durations overlap.  This groups maximal
+    runs of inflate dispatches (by start time) and reports the wall span of the
+    full-size runs: first phase-A start to last phase-B end of one pass."""
+    p = _find(os.path.join(d, "trace"), "*kernel_trace.csv")
+    if not p:
+        return None
+    ds = []
+    for r in csv.DictReader(open(p)):
+        g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        ds.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), g))
+    ds.sort()
+    runs, cur = [], []
+    for dsp in ds:
+        if dsp[2] in INFLATE:
+            cur.append(dsp)
+        elif cur:
+            runs.append(cur)
+            cur = []
+    if cur:
+        runs.append(cur)
+    if not runs:
+        return None
+    work = [sum(g for _, _, n, g in r if n == "hbam::k_inflate_lz77") for r in runs]
+    wmax = max(work)
+    main = [r for r, w in zip(runs, work) if 2 * w >= wmax]
+    spans = [max(e for _, e, _, _ in r) - min(s_ for s_, _, _, _ in r) for r in main]
+    return {"passes": len(main), "avg_span_ns": sum(spans) / len(spans),
+            "lz77_launches_per_pass": sum(1 for _, _, n, _ in main[0] if n == "hbam::k_inflate_lz77")}
+
+
 def counters(d, sub):
     p = _find(os.path.join(d, sub), "*counter_collection.csv")
     agg = defaultdict(lambda: defaultdict(list))
@@ -133,7 +169,7 @@ def main():
         if c.get("SQ_ACTIVE_INST_VALU") is not None and c.get("SQ_WAVE_CYCLES"):
             e["valu_active_frac_of_wave_cycles"] = c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"]
         res[k] = e
-    print(json.dumps({"kernels": res}, indent=1))
+    print(json.dumps({"kernels": res, "inflate_stage": inflate_stage_spans(d)}, indent=1))
 
 
 if __name__ == "__main__":
