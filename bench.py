@@ -95,6 +95,34 @@ def extra_configs(c2, c2_info):
     return res
 
 
+def host_and_copy_legs(g, data, info, pass_ms):
+    """Measurements around the headline (rank 0, N=1; never `value`):
+    * SAMRecordWritable.write of the whole decoded C2 span on the GPU
+      (k_wr_copy + k_wr_bin_patch; 2 B of HBM traffic per encoded byte);
+    * the PCIe-inclusive rate: the compressed file copied host->HBM from
+      pinned memory (hbam_gpu_reload, HIP events) plus one device pass,
+      serial, and the bound if the copy were fully overlapped;
+    * measured hipMemcpy device-to-device bandwidth (2 B per byte),
+      the practical ceiling the HBM-bound kernels are compared with."""
+    res = {}
+    ms, nb = g.encode_writables(iters=10)
+    res["writable_encode"] = {
+        "bytes": nb, "ms": round(ms, 4), "GBps_encoded": round(nb / ms / 1e6, 2),
+        "roofline": {"bound": "hbm", "achieved": round(2 * nb / ms / 1e6, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(2 * nb / ms / 1e6 / HBM_PEAK_GBS, 4)}}
+    h2d = min(g.reload(data.ctypes.data, data.nbytes, pinned=True) for _ in range(3))
+    pageable = g.reload(data.ctypes.data, data.nbytes, pinned=False)
+    res["pcie_inclusive"] = {
+        "h2d_ms_pinned": round(h2d, 3), "h2d_GBps_pinned": round(data.nbytes / h2d / 1e6, 2),
+        "h2d_ms_pageable": round(pageable, 3), "pass_ms": round(pass_ms, 3),
+        "serial_uncompressed_GBps": round(info["uncompressed"] / (h2d + pass_ms) / 1e6, 2),
+        "overlapped_bound_uncompressed_GBps": round(info["uncompressed"] / max(h2d, pass_ms) / 1e6, 2)}
+    d2d = g.d2d_bandwidth(1 << 32, 5)
+    res["d2d_copy_GBps_measured"] = round(d2d, 1)
+    res["writable_encode"]["frac_of_measured_d2d"] = round(2 * nb / ms / 1e6 / d2d, 4)
+    return res
+
+
 def pmc_traffic(kernels):
     """HBM bytes per launch of `kernels` (summed) from the newest committed
     rocprofv3 PMC summary (profiles/*/summary.json, written by
@@ -223,6 +251,7 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_extra:
+        out["io"] = host_and_copy_legs(g, data, info, ms_step)
         g.close()
         out["extra"] = extra_configs(data, info)
     if rank == 0 and not args.no_cpu_baseline:

@@ -21,8 +21,10 @@ using hadoop_bam::SplittingBAMIndexer;
 
 struct hbam_ctx {
   std::unique_ptr<BamFile> f;
+  std::unique_ptr<hbam::Pipeline> codec;  // hbam_open_codec: a pipeline with no file
   std::string err;
   BAMRecordReader::Host batch;
+  hbam::SpanDev span;  // device result of the last hbam_decode_span (valid until the next call)
   std::string text;
 };
 
@@ -31,6 +33,8 @@ struct hbam_gpu {
   std::string err;
   uint64_t first_pos = 0;  // inflated-stream position of the first record
   hbam::SpanDev span;
+  hbam::DevBuf<uint8_t> enc;  // hbam_gpu_encode_writables output
+  uint64_t enc_bytes = 0;
 };
 
 namespace {
@@ -126,17 +130,8 @@ int hbam_ref(hbam_ctx* ctx, int32_t i, const char** name, int32_t* length) {
   return HBAM_OK;
 }
 
-int hbam_decode_span(hbam_ctx* ctx, uint64_t vstart, uint64_t vend, hbam_batch* out) {
-  memset(out, 0, sizeof *out);
-  if (!ctx || !ctx->f) return HBAM_E_STATE;
-  hbam::SpanDev span;
-  int rc = ctx->f->pipe().decode_span(vstart, vend, hbam::kReader, true, &span);
-  if (rc != HBAM_OK) {
-    ctx->err = ctx->f->pipe().error();
-    return rc;
-  }
-  rc = hadoop_bam::fetch_span(ctx->f->pipe(), span, &ctx->batch, &ctx->err);
-  if (rc != HBAM_OK) return rc;
+namespace {
+void fill_batch(hbam_ctx* ctx, const hbam::SpanDev& span, hbam_batch* out) {
   auto& h = ctx->batch;
   out->n = span.n;
   out->ref_id = h.ref_id.data();
@@ -157,6 +152,108 @@ int hbam_decode_span(hbam_ctx* ctx, uint64_t vstart, uint64_t vend, hbam_batch* 
   out->data = h.data.data();
   out->data_len = h.data.size();
   out->status = span.status;
+}
+}  // namespace
+
+int hbam_decode_span(hbam_ctx* ctx, uint64_t vstart, uint64_t vend, hbam_batch* out) {
+  memset(out, 0, sizeof *out);
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  ctx->span = hbam::SpanDev();
+  hbam::SpanDev& span = ctx->span;
+  int rc = ctx->f->pipe().decode_span(vstart, vend, hbam::kReader, true, &span);
+  if (rc != HBAM_OK) {
+    ctx->err = ctx->f->pipe().error();
+    span = hbam::SpanDev();
+    return rc;
+  }
+  rc = hadoop_bam::fetch_span(ctx->f->pipe(), span, &ctx->batch, &ctx->err);
+  if (rc != HBAM_OK) return rc;
+  fill_batch(ctx, span, out);
+  if (span.status != HBAM_OK) {
+    ctx->err = span.error;
+    return span.status;
+  }
+  return HBAM_OK;
+}
+
+int hbam_open_codec(const hbam_opts* opts, hbam_ctx** out) {
+  *out = nullptr;
+  hbam_opts o{};
+  if (opts) o = *opts;
+  if (o.device < 0 || o.device >= hbam_device_count()) {
+    g_open_err = "no HIP device " + std::to_string(o.device);
+    return HBAM_E_DEVICE;
+  }
+  auto* c = new hbam_ctx();
+  c->codec.reset(new hbam::Pipeline(o.device));
+  *out = c;
+  if (!c->codec->error().empty()) {
+    c->err = g_open_err = c->codec->error();
+    return HBAM_E_DEVICE;
+  }
+  return HBAM_OK;
+}
+
+int hbam_encode_writables(hbam_ctx* ctx, uint8_t* out, uint64_t cap, uint64_t* offs, uint64_t* len) {
+  *len = 0;
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  hbam::Pipeline& p = ctx->f->pipe();
+  const hbam::SpanDev& span = ctx->span;
+  if (span.data) {
+    ctx->err = "hbam_encode_writables needs a span from hbam_decode_span";
+    return HBAM_E_STATE;
+  }
+  uint64_t bytes = 0;
+  int rc = p.encoded_bytes(span, &bytes);
+  if (rc != HBAM_OK) {
+    ctx->err = p.error();
+    return rc;
+  }
+  *len = bytes;
+  if (offs) {  // encodings have the records' own lengths: record i starts where its bytes did
+    for (uint64_t i = 0; i < span.n; ++i) offs[i] = ctx->batch.rest_off[i] - 36;
+    offs[span.n] = bytes;
+  }
+  if (!out) return HBAM_OK;
+  if (cap < bytes) {
+    ctx->err = "output buffer too small for the encoded records";
+    return HBAM_E_ARG;
+  }
+  if (bytes == 0) return HBAM_OK;
+  hbam::DevBuf<uint8_t> dst;
+  if (dst.reserve((bytes + 15) & ~15ull) != hipSuccess) {
+    ctx->err = "hipMalloc failed";
+    return HBAM_E_DEVICE;
+  }
+  rc = p.encode_writables(span, bytes, dst.p);
+  if (rc != HBAM_OK) {
+    ctx->err = p.error();
+    return rc;
+  }
+  if (hipMemcpyAsync(out, dst.p, bytes, hipMemcpyDeviceToHost, p.stream()) != hipSuccess ||
+      hipStreamSynchronize(p.stream()) != hipSuccess) {
+    ctx->err = "hipMemcpy D2H failed";
+    return HBAM_E_DEVICE;
+  }
+  return HBAM_OK;
+}
+
+int hbam_decode_writables(hbam_ctx* ctx, const void* buf, uint64_t len, const uint64_t* offs, uint64_t n,
+                          hbam_batch* out) {
+  memset(out, 0, sizeof *out);
+  if (!ctx || (!ctx->f && !ctx->codec)) return HBAM_E_STATE;
+  hbam::Pipeline& p = ctx->f ? ctx->f->pipe() : *ctx->codec;
+  ctx->span = hbam::SpanDev();
+  hbam::SpanDev& span = ctx->span;
+  int rc = p.decode_writables(static_cast<const uint8_t*>(buf), len, offs, n, &span);
+  if (rc != HBAM_OK) {
+    ctx->err = p.error();
+    span = hbam::SpanDev();
+    return rc;
+  }
+  rc = hadoop_bam::fetch_span(p, span, &ctx->batch, &ctx->err);
+  if (rc != HBAM_OK) return rc;
+  fill_batch(ctx, span, out);
   if (span.status != HBAM_OK) {
     ctx->err = span.error;
     return span.status;
@@ -360,6 +457,66 @@ int hbam_gpu_run(hbam_gpu* g, int32_t flags, hbam_gpu_stats* st) {
   }
   if (g->span.status != HBAM_OK) g->err = g->span.error;
   return g->span.status;
+}
+
+int hbam_gpu_reload(hbam_gpu* g, const void* data, uint64_t len, int32_t pinned, float* ms) {
+  *ms = 0;
+  int rc = g->p->reload(static_cast<const uint8_t*>(data), len, pinned != 0, ms);
+  if (rc != HBAM_OK) g->err = g->p->error();
+  return rc;
+}
+
+int hbam_gpu_d2d_bandwidth(hbam_gpu* g, uint64_t bytes, int32_t iters, float* gbps) {
+  int rc = g->p->d2d_bandwidth(bytes, iters, gbps);
+  if (rc != HBAM_OK) g->err = g->p->error();
+  return rc;
+}
+
+int hbam_gpu_encode_writables(hbam_gpu* g, int32_t iters, float* ms_per_iter, uint64_t* bytes) {
+  *ms_per_iter = 0;
+  *bytes = 0;
+  hbam::Pipeline& p = *g->p;
+  uint64_t nb = 0;
+  int rc = p.encoded_bytes(g->span, &nb);
+  if (rc != HBAM_OK) {
+    g->err = p.error();
+    return rc;
+  }
+  if (g->enc.reserve((nb + 15) & ~15ull) != hipSuccess) {
+    g->err = "hipMalloc failed";
+    return HBAM_E_DEVICE;
+  }
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  rc = p.encode_writables(g->span, nb, g->enc.p);  // warm-up (also checks the launch)
+  if (rc == HBAM_OK) {
+    (void)hipEventRecord(e0, p.stream());
+    for (int32_t i = 0; i < iters && rc == HBAM_OK; ++i) rc = p.encode_writables(g->span, nb, g->enc.p);
+    (void)hipEventRecord(e1, p.stream());
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    *ms_per_iter = iters > 0 ? ms / (float)iters : 0.f;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (rc != HBAM_OK) {
+    g->err = p.error();
+    return rc;
+  }
+  g->enc_bytes = nb;
+  *bytes = nb;
+  return HBAM_OK;
+}
+
+int hbam_gpu_fetch_encoded(hbam_gpu* g, uint64_t pos, uint64_t len, uint8_t* dst) {
+  if (pos > g->enc_bytes || len > g->enc_bytes - pos) {
+    g->err = "range outside the encoded records";
+    return HBAM_E_ARG;
+  }
+  if (len && hipMemcpy(dst, g->enc.p + pos, len, hipMemcpyDeviceToHost) != hipSuccess) return HBAM_E_DEVICE;
+  return HBAM_OK;
 }
 
 int hbam_gpu_fetch(hbam_gpu* g, int64_t* keys, uint64_t* voffs, uint64_t cap) {

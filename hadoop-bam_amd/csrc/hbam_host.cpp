@@ -382,7 +382,7 @@ int fetch_span(hbam::Pipeline& p, const SpanDev& s, BAMRecordReader::Host* h, st
   if (n) hi = h->rest_off[n - 1] + h->rest_len[n - 1];
   h->data.resize(hi - lo);
   if (hi > lo) {
-    if (hipMemcpy(h->data.data(), p.d_u() + lo, hi - lo, hipMemcpyDeviceToHost) != hipSuccess) {
+    if (hipMemcpy(h->data.data(), (s.data ? s.data : p.d_u()) + lo, hi - lo, hipMemcpyDeviceToHost) != hipSuccess) {
       *err = "hipMemcpy D2H failed";
       return kErrDevice;
     }

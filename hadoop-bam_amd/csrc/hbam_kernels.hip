@@ -2429,6 +2429,95 @@ __global__ void k_sbi_emit(const uint64_t* __restrict__ voff, uint64_t n, uint32
 }
 
 // ---------------------------------------------------------------------------
+// SAMRecordWritable codec (SAMRecordWritable.java:55-68)
+// ---------------------------------------------------------------------------
+// write(): [htsjdk] BAMRecordCodec.encode of an unmodified BAMRecord emits
+// block_size (= 32 + rest length), the fixed fields and the undecoded rest --
+// the record's own bytes, except that indexBin is written as 0 when refID < 0.
+// The records of a span lie back to back in the inflated stream, so the
+// encodings of a span are u[p0, p0+n) copied into a 16 B-aligned buffer
+// (k_wr_copy: HBM-bound, 2 B of traffic per byte) followed by the sparse bin
+// patches (k_wr_bin_patch: 6 B of columns per record).
+
+// 16 bytes starting sh bytes into the 32-byte pair (a, b); sh is uniform.
+__device__ __forceinline__ uint4 shift16(const uint4 a, const uint4 b, uint32_t sh) {
+  const uint32_t r = sh & 3;
+  uint32_t w0, w1, w2, w3, w4;
+  switch (sh >> 2) {
+    case 0: w0 = a.x; w1 = a.y; w2 = a.z; w3 = a.w; w4 = b.x; break;
+    case 1: w0 = a.y; w1 = a.z; w2 = a.w; w3 = b.x; w4 = b.y; break;
+    case 2: w0 = a.z; w1 = a.w; w2 = b.x; w3 = b.y; w4 = b.z; break;
+    default: w0 = a.w; w1 = b.x; w2 = b.y; w3 = b.z; w4 = b.w; break;
+  }
+  return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
+                    __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r));
+}
+
+constexpr int kWrUnroll = 4;  // 16 B chunks in flight per thread
+// dst[0, 16*ceil(n/16)) = u[p0, ...): chunk c of the destination comes from
+// the aligned source chunks c and c+1 (the stream is padded past its end).
+__global__ __launch_bounds__(256) void k_wr_copy(const uint8_t* __restrict__ u, uint64_t p0, uint64_t n,
+                                                 uint8_t* __restrict__ dst) {
+  const uint4* __restrict__ src = reinterpret_cast<const uint4*>(u + (p0 & ~15ull));
+  uint4* __restrict__ d = reinterpret_cast<uint4*>(dst);
+  const uint32_t sh = (uint32_t)(p0 & 15);
+  const uint64_t nch = (n + 15) >> 4;
+  const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  for (; c + (kWrUnroll - 1) * T < nch; c += kWrUnroll * T) {  // kWrUnroll coalesced chunks per thread
+    uint4 a[kWrUnroll], b[kWrUnroll];
+#pragma unroll
+    for (int k = 0; k < kWrUnroll; ++k) {
+      a[k] = src[c + k * T];
+      b[k] = src[c + k * T + 1];
+    }
+#pragma unroll
+    for (int k = 0; k < kWrUnroll; ++k) d[c + k * T] = shift16(a[k], b[k], sh);
+  }
+  for (; c < nch; c += T) d[c] = shift16(src[c], src[c + 1], sh);
+}
+
+__global__ void k_wr_bin_patch(const uint64_t* __restrict__ rec_pos, const int32_t* __restrict__ ref_id,
+                               const uint16_t* __restrict__ bin, uint64_t n, uint64_t p0, uint8_t* __restrict__ dst) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (ref_id[i] < 0 && bin[i] != 0) {  // [htsjdk] encode: indexBin = 0 unless refIndex >= 0
+      const uint64_t q = rec_pos[i] - p0 + 14;
+      dst[q] = 0;
+      dst[q + 1] = 0;
+    }
+  }
+}
+
+// readFields(): [htsjdk] BAMRecordCodec.decode (LazyBAMRecordFactory, no
+// header) once per framed value buf[offs[i], offs[i+1]) (the last ends at
+// len).  The first failing value's index and status go to *bad
+// ((i << 8) | status, atomicMin); values decode independently.
+__global__ void k_wr_decode(const uint8_t* __restrict__ buf, uint64_t len, const uint64_t* __restrict__ offs,
+                            uint64_t n, Columns col, uint64_t* __restrict__ rec_pos,
+                            unsigned long long* __restrict__ bad) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t p = offs[i], e = i + 1 < n ? offs[i + 1] : len;
+    uint32_t code = kOk;
+    if (e < p || e > len) {
+      code = kErrArg;
+    } else if (e - p < 4) {
+      code = kErrTrunc;  // readInt at EOF: decode() returns null
+    } else {
+      const int32_t bs = (int32_t)ldu32(buf, p);
+      if (bs < 32) code = kErrFormat;                         // "Invalid record length"
+      else if (e - p - 4 < (uint64_t)bs) code = kErrTrunc;    // readFully short: RuntimeEOFException
+    }
+    if (code != kOk) {
+      atomicMin(bad, (unsigned long long)((i << 8) | code));
+      continue;
+    }
+    decode_record(buf, p, i, col);
+    col.voff[i] = kNone;  // a shuffled record has no file position
+    rec_pos[i] = p;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host launch wrappers (hbam_launch.h)
 // ---------------------------------------------------------------------------
 static inline unsigned grid_for(uint64_t n, unsigned bs, unsigned cap = 65535u * 4) {
@@ -2674,6 +2763,28 @@ hipError_t launch_truncate_counts(uint32_t* cnt, uint32_t nb, const uint32_t* cu
 hipError_t launch_sbi_emit(const uint64_t* voff, uint64_t n, uint32_t g, uint64_t* ent, hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_sbi_emit, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, voff, n, g, ent);
+  return hipGetLastError();
+}
+hipError_t launch_wr_encode(const uint8_t* u, uint64_t p0, uint64_t nbytes, const uint64_t* rec_pos,
+                            const int32_t* ref_id, const uint16_t* bin, uint64_t n, uint8_t* dst, hipStream_t s) {
+  if (nbytes) {
+    const uint64_t nch = (nbytes + 15) >> 4;
+    // 8 workgroups of 256 per CU (2048 lanes x kWrUnroll chunks in flight each)
+    const uint64_t grid = std::min<uint64_t>((nch + 255) / 256, 256ull * 8);
+    hipLaunchKernelGGL(k_wr_copy, dim3((unsigned)std::max<uint64_t>(grid, 1)), dim3(256), 0, s, u, p0, nbytes, dst);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_wr_bin_patch, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, rec_pos, ref_id, bin, n, p0,
+                     dst);
+  return hipGetLastError();
+}
+hipError_t launch_wr_decode(const uint8_t* buf, uint64_t len, const uint64_t* offs, uint64_t n, const Columns& col,
+                            uint64_t* rec_pos, unsigned long long* bad, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_wr_decode, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, buf, len, offs, n, col, rec_pos,
+                     bad);
   return hipGetLastError();
 }
 

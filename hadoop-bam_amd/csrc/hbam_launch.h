@@ -79,5 +79,12 @@ hipError_t launch_first_error_hout(const HuffOut* hout, uint32_t b0, uint32_t nb
 hipError_t launch_first_error_i32(const int32_t* err, uint32_t nb, uint32_t* first, hipStream_t s);
 hipError_t launch_truncate_counts(uint32_t* cnt, uint32_t nb, const uint32_t* cut, hipStream_t s);
 hipError_t launch_sbi_emit(const uint64_t* voff, uint64_t n, uint32_t g, uint64_t* ent, hipStream_t s);
+// SAMRecordWritable.write of a span's records: u[p0, p0+nbytes) -> dst
+// (16 B-aligned, room for nbytes rounded up to 16) + bin patches (refID < 0)
+hipError_t launch_wr_encode(const uint8_t* u, uint64_t p0, uint64_t nbytes, const uint64_t* rec_pos,
+                            const int32_t* ref_id, const uint16_t* bin, uint64_t n, uint8_t* dst, hipStream_t s);
+// SAMRecordWritable.readFields of n framed values; *bad = min((i << 8) | status)
+hipError_t launch_wr_decode(const uint8_t* buf, uint64_t len, const uint64_t* offs, uint64_t n, const Columns& col,
+                            uint64_t* rec_pos, unsigned long long* bad, hipStream_t s);
 
 }  // namespace hbam

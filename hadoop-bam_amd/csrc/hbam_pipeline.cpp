@@ -74,6 +74,45 @@ int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base_offset) {
   return kOk;
 }
 
+int Pipeline::reload(const uint8_t* data, uint64_t len, bool pinned, float* ms) {
+  if (!dfile_ || !own_file_ || len != flen_) return fail(kErrState, "reload needs a loaded file of the same size");
+  HIPCHK(hipSetDevice(device_));
+  uint8_t* staging = nullptr;
+  if (pinned && len) {  // page-locked copy of the bytes (untimed), as a JNI direct buffer would be
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&staging), len, hipHostMallocDefault));
+    memcpy(staging, data, len);
+  }
+  int rc = kOk;
+  auto body = [&]() -> int {
+    HIPCHK(hipEventRecord(ev_[6], stream_));
+    if (len) HIPCHK(hipMemcpyAsync(dfile_, staging ? staging : data, len, hipMemcpyHostToDevice, stream_));
+    HIPCHK(hipEventRecord(ev_[7], stream_));
+    HIPCHK(hipEventSynchronize(ev_[7]));
+    HIPCHK(hipEventElapsedTime(ms, ev_[6], ev_[7]));
+    return kOk;
+  };
+  rc = body();
+  if (staging) (void)hipHostFree(staging);
+  return rc;
+}
+
+int Pipeline::d2d_bandwidth(uint64_t bytes, int iters, float* gbps) {
+  *gbps = 0;
+  DevBuf<uint8_t> a, b;
+  HIPCHK(a.reserve(bytes));
+  HIPCHK(b.reserve(bytes));
+  HIPCHK(hipMemsetAsync(a.p, 1, bytes, stream_));
+  HIPCHK(hipMemcpyAsync(b.p, a.p, bytes, hipMemcpyDeviceToDevice, stream_));  // warm-up
+  HIPCHK(hipEventRecord(ev_[6], stream_));
+  for (int i = 0; i < iters; ++i) HIPCHK(hipMemcpyAsync(b.p, a.p, bytes, hipMemcpyDeviceToDevice, stream_));
+  HIPCHK(hipEventRecord(ev_[7], stream_));
+  HIPCHK(hipEventSynchronize(ev_[7]));
+  float ms = 0;
+  HIPCHK(hipEventElapsedTime(&ms, ev_[6], ev_[7]));
+  *gbps = (float)(2.0 * (double)bytes * iters / ((double)ms * 1e6));  // read + write
+  return kOk;
+}
+
 int Pipeline::attach_device(const uint8_t* dptr, uint64_t len, uint64_t base_offset) {
   if (own_file_ && dfile_) (void)hipFree(dfile_);
   dfile_ = const_cast<uint8_t*>(dptr);
@@ -585,34 +624,8 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
   const bool dec = decode && mode == kReader;
   Columns c{};
   if (dec) {
-    // SoA backing store: 8-byte columns first, then 4, 2, 1 (alignment)
-    const uint64_t n = std::max<uint64_t>(total, 1);
-    const uint64_t per = 8 * 2 + 4 * 7 + 2 * 3 + 1 * 2;
-    if (cols_cap_ < n) {
-      HIPCHK(cols_.reserve(n * per + 256));
-      cols_cap_ = n;
-    }
-    uint8_t* p = cols_.p;
-    auto take = [&](uint64_t bytes) {
-      uint8_t* r = p;
-      p += (bytes + 15) & ~15ull;
-      return r;
-    };
-    c.key = reinterpret_cast<int64_t*>(take(8 * n));
-    c.rest_off = reinterpret_cast<uint64_t*>(take(8 * n));
-    c.voff = rec_voff_.p;
-    c.ref_id = reinterpret_cast<int32_t*>(take(4 * n));
-    c.pos = reinterpret_cast<int32_t*>(take(4 * n));
-    c.l_seq = reinterpret_cast<int32_t*>(take(4 * n));
-    c.next_ref_id = reinterpret_cast<int32_t*>(take(4 * n));
-    c.next_pos = reinterpret_cast<int32_t*>(take(4 * n));
-    c.tlen = reinterpret_cast<int32_t*>(take(4 * n));
-    c.rest_len = reinterpret_cast<uint32_t*>(take(4 * n));
-    c.bin = reinterpret_cast<uint16_t*>(take(2 * n));
-    c.n_cigar = reinterpret_cast<uint16_t*>(take(2 * n));
-    c.flag = reinterpret_cast<uint16_t*>(take(2 * n));
-    c.l_read_name = take(n);
-    c.mapq = take(n);
+    int rc = alloc_columns(total, &c);
+    if (rc != kOk) return rc;
     out->col = c;
   }
   if (lists) {  // positions + voffs (+ fused decode) straight off the per-block lists
@@ -633,6 +646,101 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
     times.decode = dcd;
     times.inflate = infl_ms;
   }
+  return kOk;
+}
+
+int Pipeline::alloc_columns(uint64_t total, Columns* cp) {
+  // SoA backing store: 8-byte columns first, then 4, 2, 1 (alignment)
+  const uint64_t n = std::max<uint64_t>(total, 1);
+  const uint64_t per = 8 * 2 + 4 * 7 + 2 * 3 + 1 * 2;
+  if (cols_cap_ < n) {
+    HIPCHK(cols_.reserve(n * per + 256));
+    cols_cap_ = n;
+  }
+  HIPCHK(rec_voff_.reserve(n + 1));
+  uint8_t* p = cols_.p;
+  auto take = [&](uint64_t bytes) {
+    uint8_t* r = p;
+    p += (bytes + 15) & ~15ull;
+    return r;
+  };
+  Columns& c = *cp;
+  c.key = reinterpret_cast<int64_t*>(take(8 * n));
+  c.rest_off = reinterpret_cast<uint64_t*>(take(8 * n));
+  c.voff = rec_voff_.p;
+  c.ref_id = reinterpret_cast<int32_t*>(take(4 * n));
+  c.pos = reinterpret_cast<int32_t*>(take(4 * n));
+  c.l_seq = reinterpret_cast<int32_t*>(take(4 * n));
+  c.next_ref_id = reinterpret_cast<int32_t*>(take(4 * n));
+  c.next_pos = reinterpret_cast<int32_t*>(take(4 * n));
+  c.tlen = reinterpret_cast<int32_t*>(take(4 * n));
+  c.rest_len = reinterpret_cast<uint32_t*>(take(4 * n));
+  c.bin = reinterpret_cast<uint16_t*>(take(2 * n));
+  c.n_cigar = reinterpret_cast<uint16_t*>(take(2 * n));
+  c.flag = reinterpret_cast<uint16_t*>(take(2 * n));
+  c.l_read_name = take(n);
+  c.mapq = take(n);
+  return kOk;
+}
+
+int Pipeline::encoded_bytes(const SpanDev& s, uint64_t* bytes) {
+  *bytes = 0;
+  if (s.n == 0) return kOk;
+  if (!s.col.rest_off) return fail(kErrState, "span was not decoded in reader mode");
+  uint64_t first = 0, last_off = 0;
+  uint32_t last_len = 0;
+  HIPCHK(hipMemcpyAsync(&first, s.rec_pos, 8, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipMemcpyAsync(&last_off, s.col.rest_off + (s.n - 1), 8, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipMemcpyAsync(&last_len, s.col.rest_len + (s.n - 1), 4, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  *bytes = last_off + last_len - first;
+  return kOk;
+}
+
+int Pipeline::encode_writables(const SpanDev& s, uint64_t bytes, uint8_t* dst) {
+  if (s.n == 0) return kOk;
+  if (!s.col.ref_id) return fail(kErrState, "span was not decoded in reader mode");
+  uint64_t first = 0;
+  HIPCHK(hipMemcpyAsync(&first, s.rec_pos, 8, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  const uint8_t* src = s.data ? s.data : du_.p;
+  HIPCHK(launch_wr_encode(src, first, bytes, s.rec_pos, s.col.ref_id, s.col.bin, s.n, dst, stream_));
+  return kOk;
+}
+
+int Pipeline::decode_writables(const uint8_t* buf, uint64_t len, const uint64_t* offs, uint64_t n, SpanDev* out) {
+  *out = SpanDev();
+  // 64 zero bytes after the values: the 8-byte field loads and Murmur's tail
+  // loads may read past the last value
+  HIPCHK(wbuf_.reserve(len + 64));
+  HIPCHK(woffs_.reserve(n + 1));
+  HIPCHK(wbad_.reserve(1));
+  HIPCHK(rec_pos_.reserve(n + 1));
+  if (len) HIPCHK(hipMemcpyAsync(wbuf_.p, buf, len, hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipMemsetAsync(wbuf_.p + len, 0, 64, stream_));
+  if (n) HIPCHK(hipMemcpyAsync(woffs_.p, offs, n * 8, hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipMemsetAsync(wbad_.p, 0xff, sizeof(unsigned long long), stream_));
+  Columns c{};
+  int rc = alloc_columns(n, &c);
+  if (rc != kOk) return rc;
+  HIPCHK(launch_wr_decode(wbuf_.p, len, woffs_.p, n, c, rec_pos_.p, wbad_.p, stream_));
+  unsigned long long bad = ~0ull;
+  HIPCHK(hipMemcpyAsync(&bad, wbad_.p, sizeof bad, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  out->n = n;
+  if (bad != ~0ull) {
+    out->n = bad >> 8;
+    out->status = (int)(bad & 0xff);
+    const std::string at = "value " + std::to_string(out->n);
+    if (out->status == kErrFormat) out->error = "Invalid record length (" + at + ")";
+    else if (out->status == kErrTrunc) out->error = "Premature EOF in serialized record (" + at + ")";
+    else out->error = "value framing outside the buffer (" + at + ")";
+  }
+  out->p0 = 0;
+  out->rec_pos = rec_pos_.p;
+  out->rec_voff = rec_voff_.p;
+  out->col = c;
+  out->data = wbuf_.p;
   return kOk;
 }
 

@@ -46,6 +46,7 @@ struct SpanDev {
   uint64_t* rec_pos = nullptr;    // device
   uint64_t* rec_voff = nullptr;   // device
   Columns col{};                  // device (reader mode + decode)
+  const uint8_t* data = nullptr;  // device stream rec_pos / rest_off index (nullptr = the inflated stream)
 };
 
 struct StageTimes {  // milliseconds of the last decode (HIP events)
@@ -66,6 +67,11 @@ class Pipeline {
   // Copy a BGZF file (or a BGZF-aligned shard) into HBM.  base_offset is the
   // file offset of data[0] (shards); voffs are reported in file coordinates.
   int load(const uint8_t* data, uint64_t len, uint64_t base_offset = 0);
+  // Copy the same-size file bytes into the resident buffer again, timed with
+  // HIP events (PCIe-inclusive measurements); pinned: from a page-locked copy.
+  int reload(const uint8_t* data, uint64_t len, bool pinned, float* ms);
+  // hipMemcpy device-to-device bandwidth (read + write bytes per second / 1e9)
+  int d2d_bandwidth(uint64_t bytes, int iters, float* gbps);
   // Use an already device-resident buffer (must be padded by kFilePad bytes).
   int attach_device(const uint8_t* dptr, uint64_t len, uint64_t base_offset = 0);
   uint64_t file_len() const { return flen_; }
@@ -88,6 +94,17 @@ class Pipeline {
   // Header bytes: inflate the first blocks until `need` stream bytes exist.
   int read_stream(uint64_t pos, uint64_t len, std::vector<uint8_t>* out);
 
+  // SAMRecordWritable.write (SAMRecordWritable.java:55-64) of every record of
+  // a decoded reader span, back to back: *bytes = size of the encodings;
+  // encode_writables writes them to dst (device; room for bytes rounded up
+  // to 16).  Record i's encoding starts at rec_pos[i] - rec_pos[0].
+  int encoded_bytes(const SpanDev& span, uint64_t* bytes);
+  int encode_writables(const SpanDev& span, uint64_t bytes, uint8_t* dst);
+  // SAMRecordWritable.readFields (SAMRecordWritable.java:65-68) of n values
+  // framed by offs in host memory (value i = buf[offs[i], offs[i+1]), the
+  // last ends at len): SoA columns + keys; out->n stops at the first bad value.
+  int decode_writables(const uint8_t* buf, uint64_t len, const uint64_t* offs, uint64_t n, SpanDev* out);
+
   // .splitting-bai entries (without the leading header voff / trailing size)
   int splitting_entries(const SpanDev& span, uint32_t granularity, std::vector<uint64_t>* out);
 
@@ -108,6 +125,7 @@ class Pipeline {
 
  private:
   int fail(int code, const std::string& msg);
+  int alloc_columns(uint64_t n, Columns* c);  // SoA store for n records (voff = rec_voff_)
   int hip_check(hipError_t e, const char* what);
 
   int device_ = 0;
@@ -148,6 +166,9 @@ class Pipeline {
   DevBuf<uint8_t> scan_tmp_;
   DevBuf<uint8_t> cols_;  // SoA backing store
   uint64_t cols_cap_ = 0;
+  DevBuf<uint8_t> wbuf_;                 // readFields: serialized values
+  DevBuf<uint64_t> woffs_;               // readFields: value framing
+  DevBuf<unsigned long long> wbad_;      // readFields: first bad value
 
   hipEvent_t ev_[8];
   hipEvent_t sync_ev_[4];           // [0,1] phase A done, [2,3] phase B done, per token buffer

@@ -88,6 +88,13 @@ _sig("hbam_gpu_error", C.c_char_p, [P])
 _sig("hbam_gpu_load", C.c_int, [P, P, u64, u64, i32, u64])
 _sig("hbam_gpu_run", C.c_int, [P, i32, C.POINTER(GpuStats)])
 _sig("hbam_gpu_fetch", C.c_int, [P, P, P, u64])
+_sig("hbam_encode_writables", C.c_int, [P, P, u64, P, C.POINTER(u64)])
+_sig("hbam_decode_writables", C.c_int, [P, P, u64, P, u64, C.POINTER(Batch)])
+_sig("hbam_open_codec", C.c_int, [C.POINTER(Opts), C.POINTER(P)])
+_sig("hbam_gpu_encode_writables", C.c_int, [P, i32, C.POINTER(C.c_float), C.POINTER(u64)])
+_sig("hbam_gpu_fetch_encoded", C.c_int, [P, u64, u64, P])
+_sig("hbam_gpu_reload", C.c_int, [P, P, u64, i32, C.POINTER(C.c_float)])
+_sig("hbam_gpu_d2d_bandwidth", C.c_int, [P, u64, i32, C.POINTER(C.c_float)])
 
 
 def lib():
@@ -123,6 +130,54 @@ def get_key(ref_idx, alignment_start):
     return _L.hbam_get_key(ref_idx, alignment_start)
 
 
+def _batch_dict(b, rc):
+    out = {"status": rc}
+    for name, dt in _COLS:
+        p = getattr(b, name)
+        nb = b.n * np.dtype(dt).itemsize
+        out[name] = np.frombuffer(C.string_at(p, nb), dt).copy() if b.n else np.zeros(0, dt)
+    out["data"] = C.string_at(b.data, b.data_len) if b.data_len else b""
+    return out
+
+
+def _decode_writables(h, buf, offs, raise_on_error):
+    offs = np.ascontiguousarray(offs, np.uint64)
+    keep = C.create_string_buffer(bytes(buf), max(len(buf), 1))
+    b = Batch()
+    rc = _L.hbam_decode_writables(h, keep, len(buf), offs.ctypes.data, len(offs), C.byref(b))
+    if rc != OK and (raise_on_error or rc not in (E_FORMAT, E_TRUNC, E_ARG)):
+        raise HbamError(rc, _L.hbam_last_error(h).decode(errors="replace"))
+    return _batch_dict(b, rc)
+
+
+class Codec:
+    """SAMRecordWritable.readFields in bulk on a GPU with no file open
+    (a reducer's view: hbam_open_codec + hbam_decode_writables)."""
+
+    def __init__(self, device=0):
+        self._h = P()
+        rc = _L.hbam_open_codec(C.byref(Opts(device, 0, 0, 0)), C.byref(self._h))
+        if rc != OK:
+            msg = _L.hbam_last_error(self._h).decode(errors="replace")
+            _L.hbam_close(self._h)
+            self._h = None
+            raise HbamError(rc, msg)
+
+    def decode_writables(self, buf: bytes, offs, raise_on_error=True):
+        return _decode_writables(self._h, buf, offs, raise_on_error)
+
+    def close(self):
+        if self._h:
+            _L.hbam_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
 class BamFile:
     """An opened BAM (or plain BGZF with bam=False) on one GPU."""
 
@@ -143,6 +198,7 @@ class BamFile:
             self._h = None
             raise HbamError(rc, msg)
         self.bam = bam
+        self._last_n = 0
 
     def close(self):
         if self._h:
@@ -189,13 +245,26 @@ class BamFile:
         rc = _L.hbam_decode_span(self._h, vstart, vend, C.byref(b))
         if rc != OK and (raise_on_error or b.n == 0 and rc not in (E_FORMAT, E_TRUNC, E_ARG, E_IO)):
             raise self._err(rc)
-        out = {"status": rc}
-        for name, dt in _COLS:
-            p = getattr(b, name)
-            nb = b.n * np.dtype(dt).itemsize
-            out[name] = np.frombuffer(C.string_at(p, nb), dt).copy() if b.n else np.zeros(0, dt)
-        out["data"] = C.string_at(b.data, b.data_len) if b.data_len else b""
-        return out
+        self._last_n = b.n
+        return _batch_dict(b, rc)
+
+    def encode_writables(self):
+        """SAMRecordWritable.write of every record of the last decode_span
+        (GPU): (bytes, offsets[n+1])."""
+        n = u64()
+        rc = _L.hbam_encode_writables(self._h, None, 0, None, C.byref(n))
+        if rc != OK:
+            raise self._err(rc)
+        total = n.value
+        out = C.create_string_buffer(max(total, 1))
+        offs = np.zeros(self._last_n + 1, np.uint64)
+        rc = _L.hbam_encode_writables(self._h, out, total, offs.ctypes.data, C.byref(n))
+        if rc != OK:
+            raise self._err(rc)
+        return out.raw[:total], offs
+
+    def decode_writables(self, buf: bytes, offs, raise_on_error=True):
+        return _decode_writables(self._h, buf, offs, raise_on_error)
 
     def decode_all(self, raise_on_error=True):
         return self.decode_span(self.header()["first_record_voff"], (1 << 64) - 1, raise_on_error)
@@ -296,6 +365,39 @@ class Gpu:
         if rc != OK:
             raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
         return {f: getattr(st, f) for f, _ in GpuStats._fields_}
+
+    def reload(self, ptr, nbytes, pinned=True):
+        """Host->HBM copy of the loaded file's bytes from `ptr` (through a
+        page-locked staging copy if pinned), timed: milliseconds."""
+        ms = C.c_float()
+        rc = _L.hbam_gpu_reload(self._h, ptr, nbytes, int(pinned), C.byref(ms))
+        if rc != OK:
+            raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
+        return ms.value
+
+    def d2d_bandwidth(self, nbytes=1 << 32, iters=5):
+        gbps = C.c_float()
+        rc = _L.hbam_gpu_d2d_bandwidth(self._h, nbytes, iters, C.byref(gbps))
+        if rc != OK:
+            raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
+        return gbps.value
+
+    def encode_writables(self, iters=10):
+        """SAMRecordWritable.write of the last run's records into device
+        memory, timed over `iters` launches: (ms per encode, bytes)."""
+        ms = C.c_float()
+        nb = u64()
+        rc = _L.hbam_gpu_encode_writables(self._h, iters, C.byref(ms), C.byref(nb))
+        if rc != OK:
+            raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
+        return ms.value, nb.value
+
+    def fetch_encoded(self, pos, length):
+        buf = C.create_string_buffer(max(length, 1))
+        rc = _L.hbam_gpu_fetch_encoded(self._h, pos, length, buf)
+        if rc != OK:
+            raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
+        return buf.raw[:length]
 
     def fetch(self, n):
         keys = np.zeros(max(n, 1), np.int64)

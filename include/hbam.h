@@ -125,6 +125,28 @@ int hbam_get_splits(hbam_ctx *ctx, const uint64_t *starts, const uint64_t *lengt
                     const uint8_t *sbi, uint64_t sbi_len, uint64_t *vstarts, uint64_t *vends,
                     uint64_t *nout);
 
+/* ---- SAMRecordWritable codec (map-output serialization for the shuffle) ---- */
+/* SAMRecordWritable.write (SAMRecordWritable.java:55-64) of every record of
+ * the last hbam_decode_span on ctx, computed on the GPU: [htsjdk]
+ * BAMRecordCodec.encode of each BAMRecord, back to back (block_size, the fixed
+ * fields, the undecoded rest; indexBin written as 0 when refID < 0).  *len
+ * receives the total size; out == NULL only sizes.  offs (NULL or n+1
+ * entries) receives each record's start, offs[n] = *len.  cap < *len ->
+ * HBAM_E_ARG. */
+int hbam_encode_writables(hbam_ctx *ctx, uint8_t *out, uint64_t cap, uint64_t *offs, uint64_t *len);
+/* SAMRecordWritable.readFields (SAMRecordWritable.java:65-68) for n serialized
+ * values at once: value i = buf[offs[i], offs[i+1]) (the last ends at len), as
+ * the shuffle frames them.  Decodes into out like hbam_decode_span (voff =
+ * UINT64_MAX: no file position; key = BAMRecordReader.getKey of the record).
+ * Stops at the first bad value: too short for block_size (readFields would
+ * get a null record) or a short rest -> HBAM_E_TRUNC; block_size < 32 ->
+ * HBAM_E_FORMAT; framing outside buf -> HBAM_E_ARG. */
+int hbam_decode_writables(hbam_ctx *ctx, const void *buf, uint64_t len, const uint64_t *offs, uint64_t n,
+                          hbam_batch *out);
+/* A ctx with a device and no file, for reducers that only call
+ * hbam_decode_writables. */
+int hbam_open_codec(const hbam_opts *opts, hbam_ctx **out);
+
 /* BGZF block table (coff, csize, isize, ustart) and inflated bytes: used by
  * tests and by the BGZF text formats. */
 int hbam_blocks(hbam_ctx *ctx, uint64_t *coff, uint32_t *csize, uint32_t *isize, uint64_t *ustart,
@@ -168,6 +190,17 @@ int hbam_gpu_load(hbam_gpu *g, const void *data, uint64_t len, uint64_t base_off
  * record scan, field decode + keys + voffs (flags bit0: also timing per stage,
  * bit1: skip decode). */
 int hbam_gpu_run(hbam_gpu *g, int32_t flags, hbam_gpu_stats *stats);
+/* Copy the loaded file's bytes (same length) from host memory into HBM again,
+ * timed (*ms, HIP events): the host->device leg of a PCIe-inclusive rate.
+ * pinned != 0 copies from a page-locked staging copy (made untimed). */
+int hbam_gpu_reload(hbam_gpu *g, const void *data, uint64_t len, int32_t pinned, float *ms);
+/* Measured hipMemcpy device-to-device bandwidth, (read + write) GB/s. */
+int hbam_gpu_d2d_bandwidth(hbam_gpu *g, uint64_t bytes, int32_t iters, float *gbps);
+/* SAMRecordWritable.write of every record of the last run into a device
+ * buffer owned by g, iters timed times (HIP events on the pipeline stream);
+ * hbam_gpu_fetch_encoded copies [pos, pos+len) of the result to the host. */
+int hbam_gpu_encode_writables(hbam_gpu *g, int32_t iters, float *ms_per_iter, uint64_t *bytes);
+int hbam_gpu_fetch_encoded(hbam_gpu *g, uint64_t pos, uint64_t len, uint8_t *dst);
 /* Copy results of the last run to the host (any pointer may be NULL). */
 int hbam_gpu_fetch(hbam_gpu *g, int64_t *keys, uint64_t *voffs, uint64_t cap);
 int32_t hbam_device_count(void);

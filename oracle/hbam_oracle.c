@@ -398,6 +398,98 @@ void orc_records_free(orc_records *r) {
 void orc_free(void *p) { free(p); }
 
 /* ------------------------------------------------------------------------ */
+/* SAMRecordWritable.write (SAMRecordWritable.java:55-64): [htsjdk]          */
+/* BAMRecordCodec.encode of the BAMRecord BAMRecordReader hands out          */
+/* (unmodified, lazily decoded).  Restated field by field:                   */
+/*   blockSize = 32 + getReadNameLength()+1 + 4*cigarLen + (readLen+1)/2     */
+/*             + readLen + getAttributesBinarySize(), the last being         */
+/*             rest.length - (l_read_name + 4*n_cigar + (l_seq+1)/2 + l_seq) */
+/*             ([htsjdk] BAMRecord; -1 = "stale" would re-encode the parsed  */
+/*             attributes instead -- unreachable for records that decoded);  */
+/*   indexBin  = refIndex >= 0 ? getIndexingBin() (the decoded bin) : 0;     */
+/*   then refID, pos (=alignmentStart-1), l_read_name, mapq, bin, n_cigar,   */
+/*   flag, l_seq, next_refID, next_pos, tlen, getVariableBinaryRepresentation*/
+/*   (= the undecoded rest).  out may be NULL (size only); offs[i] = start   */
+/*   of record i's encoding, offs[n] = total.                               */
+/* ------------------------------------------------------------------------ */
+static void put_le32(uint8_t *o, uint32_t v) {
+  o[0] = (uint8_t)v; o[1] = (uint8_t)(v >> 8); o[2] = (uint8_t)(v >> 16); o[3] = (uint8_t)(v >> 24);
+}
+uint64_t orc_writable_encode(const uint8_t *data, const orc_records *r, uint8_t *out, uint64_t *offs) {
+  uint64_t o = 0;
+  for (uint64_t i = 0; i < r->n; i++) {
+    const int64_t lrn = r->l_read_name[i], nc = r->n_cigar[i], ls = r->l_seq[i];
+    const int64_t fixed_var = lrn + 4 * nc + (ls + 1) / 2 + ls;
+    const int64_t attrs = (int64_t)r->rest_len[i] - fixed_var;
+    const int32_t block_size = (int32_t)(32 + fixed_var + attrs);
+    const uint16_t bin = r->ref_id[i] >= 0 ? r->bin[i] : 0;
+    if (offs) offs[i] = o;
+    if (out) {
+      uint8_t *p = out + o;
+      put_le32(p, (uint32_t)block_size);
+      put_le32(p + 4, (uint32_t)r->ref_id[i]);
+      put_le32(p + 8, (uint32_t)r->pos[i]);
+      p[12] = r->l_read_name[i];
+      p[13] = r->mapq[i];
+      p[14] = (uint8_t)bin; p[15] = (uint8_t)(bin >> 8);
+      p[16] = (uint8_t)r->n_cigar[i]; p[17] = (uint8_t)(r->n_cigar[i] >> 8);
+      p[18] = (uint8_t)r->flag[i]; p[19] = (uint8_t)(r->flag[i] >> 8);
+      put_le32(p + 20, (uint32_t)r->l_seq[i]);
+      put_le32(p + 24, (uint32_t)r->next_ref_id[i]);
+      put_le32(p + 28, (uint32_t)r->next_pos[i]);
+      put_le32(p + 32, (uint32_t)r->tlen[i]);
+      memcpy(p + 36, data + r->offset[i] + 36, r->rest_len[i]);
+    }
+    o += 4 + (uint64_t)(uint32_t)block_size;
+  }
+  if (offs) offs[r->n] = o;
+  return o;
+}
+
+/* SAMRecordWritable.readFields (SAMRecordWritable.java:65-68): [htsjdk]     */
+/* BAMRecordCodec.decode through LazyBAMRecordFactory with no header, once   */
+/* per serialized value; value i is buf[offs[i], offs[i+1]), offs[n] = len.  */
+/* readInt(block_size) hitting EOF makes decode() return null: reported as   */
+/* ORC_E_TRUNC (a batch has no null record); block_size < 32 ->              */
+/* SAMFormatException; a short rest -> RuntimeEOFException (ORC_E_TRUNC).    */
+/* No dictionary check (null header).  offset = start of value i in buf;     */
+/* voff = ~0 (a shuffled record has no file position).                       */
+int orc_writable_decode(const uint8_t *buf, uint64_t len, const uint64_t *offs, uint64_t n, orc_records *out) {
+  memset(out, 0, sizeof *out);
+  rec_buf b;
+  memset(&b, 0, sizeof b);
+  int rc = ORC_OK;
+  for (uint64_t i = 0; i < n; i++) {
+    const uint64_t p = offs[i], e = i + 1 < n ? offs[i + 1] : len;
+    if (e < p || e > len) { rc = ORC_E_ARG; break; }
+    if (e - p < 4) { rc = ORC_E_TRUNC; break; }
+    const uint8_t *r = buf + p;
+    const int32_t bs = rdi32(r);
+    if (bs < 32) { rc = ORC_E_FORMAT; break; }
+    if (e - p - 4 < (uint64_t)bs) { rc = ORC_E_TRUNC; break; }
+    if (b.r.n == b.cap && (rc = rec_grow(&b)) != ORC_OK) break;
+    const uint64_t k = b.r.n++;
+    b.r.ref_id[k] = rdi32(r + 4);
+    b.r.pos[k] = rdi32(r + 8);
+    b.r.l_read_name[k] = r[12];
+    b.r.mapq[k] = r[13];
+    b.r.bin[k] = rd16(r + 14);
+    b.r.n_cigar[k] = rd16(r + 16);
+    b.r.flag[k] = rd16(r + 18);
+    b.r.l_seq[k] = rdi32(r + 20);
+    b.r.next_ref_id[k] = rdi32(r + 24);
+    b.r.next_pos[k] = rdi32(r + 28);
+    b.r.tlen[k] = rdi32(r + 32);
+    b.r.voff[k] = ~0ull;
+    b.r.offset[k] = p;
+    b.r.rest_len[k] = (uint32_t)(bs - 32);
+    b.r.key[k] = orc_get_key(b.r.ref_id[k], b.r.pos[k], b.r.flag[k], r + 36, (uint32_t)(bs - 32));
+  }
+  *out = b.r;
+  return rc;
+}
+
+/* ------------------------------------------------------------------------ */
 /* SplittingBAMIndexer.index (SplittingBAMIndexer.java:248-290)              */
 /* ------------------------------------------------------------------------ */
 static void put_be64(uint8_t *o, uint64_t v) {

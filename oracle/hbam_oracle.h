@@ -81,6 +81,14 @@ typedef struct {
 int orc_decode_span(orc_stream *s, uint64_t vstart, uint64_t vend, orc_records *out);
 void orc_records_free(orc_records *r);
 
+/* SAMRecordWritable.write (SAMRecordWritable.java:55-64) of every record in r
+ * ([htsjdk] BAMRecordCodec.encode); data = the inflated stream r->offset
+ * indexes.  Returns the total size; out may be NULL; offs has r->n+1 slots. */
+uint64_t orc_writable_encode(const uint8_t *data, const orc_records *r, uint8_t *out, uint64_t *offs);
+/* SAMRecordWritable.readFields (SAMRecordWritable.java:65-68) for n values
+ * framed by offs (value i = buf[offs[i], offs[i+1]), the last ends at len). */
+int orc_writable_decode(const uint8_t *buf, uint64_t len, const uint64_t *offs, uint64_t n, orc_records *out);
+
 /* SplittingBAMIndexer.index (SplittingBAMIndexer.java:248-368). */
 int orc_splitting_index(orc_stream *s, uint64_t file_size, int32_t granularity,
                         uint8_t **out, uint64_t *out_len);

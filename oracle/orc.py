@@ -53,6 +53,9 @@ def lib():
         L.orc_get_splits.argtypes = [P, P, u64, P, P, u64, P, u64, P, P, C.POINTER(u64)]
         L.orc_crc32.argtypes = [P, u64]
         L.orc_crc32.restype = u32
+        L.orc_writable_encode.argtypes = [P, P, P, P]
+        L.orc_writable_encode.restype = u64
+        L.orc_writable_decode.argtypes = [P, u64, P, u64, P]
         _LIB = L
     return _LIB
 
@@ -143,15 +146,24 @@ class Stream:
         L = lib()
         r = _Records()
         rc = L.orc_decode_span(self._h, vstart, vend, C.byref(r))
-        out = {}
-        for name, dt in RECORD_FIELDS:
-            p = getattr(r, name)
-            if r.n and p:
-                out[name] = np.frombuffer(C.string_at(p, r.n * np.dtype(dt).itemsize), dt).copy()
-            else:
-                out[name] = np.zeros(0, dt)
+        out = _columns(r)
         L.orc_records_free(C.byref(r))
         return rc, out
+
+    def writable_encode_span(self, vstart, vend):
+        """SAMRecordWritable.write of every record of the span:
+        (status, concatenated bytes, offsets[n+1])."""
+        L = lib()
+        r = _Records()
+        rc = L.orc_decode_span(self._h, vstart, vend, C.byref(r))
+        try:
+            total = L.orc_writable_encode(L.orc_data(self._h), C.byref(r), None, None)
+            out = C.create_string_buffer(max(total, 1))
+            offs = np.zeros(r.n + 1, np.uint64)
+            L.orc_writable_encode(L.orc_data(self._h), C.byref(r), out, offs.ctypes.data)
+            return rc, out.raw[:total], offs
+        finally:
+            L.orc_records_free(C.byref(r))
 
     def decode_all(self):
         return self.decode_span(self.first_record_voff, (1 << 64) - 1)
@@ -189,6 +201,29 @@ class Stream:
         if rc != 0:
             raise OracleError(rc, L.orc_error(self._h).decode())
         return [(vs[i], ve[i]) for i in range(nout.value)]
+
+
+def _columns(r):
+    out = {}
+    for name, dt in RECORD_FIELDS:
+        p = getattr(r, name)
+        if r.n and p:
+            out[name] = np.frombuffer(C.string_at(p, r.n * np.dtype(dt).itemsize), dt).copy()
+        else:
+            out[name] = np.zeros(0, dt)
+    return out
+
+
+def writable_decode(buf: bytes, offs):
+    """SAMRecordWritable.readFields per framed value: (status, columns)."""
+    L = lib()
+    offs = np.ascontiguousarray(offs, np.uint64)
+    b = C.create_string_buffer(bytes(buf), max(len(buf), 1))
+    r = _Records()
+    rc = L.orc_writable_decode(b, len(buf), offs.ctypes.data, len(offs), C.byref(r))
+    out = _columns(r)
+    L.orc_records_free(C.byref(r))
+    return rc, out
 
 
 def murmurhash3(data: bytes, seed=0):

@@ -8,6 +8,7 @@ for keys).  Pure-Python loops: small inputs only.
   get_key      <- BAMRecordReader.java:81-121
   records      <- [htsjdk] BAMRecordCodec.decode chain from the header end
   splitting_index <- SplittingBAMIndexer.java:248-290
+  writable_encode <- SAMRecordWritable.java:55-64 ([htsjdk] BAMRecordCodec.encode)
 """
 import struct
 import zlib
@@ -173,3 +174,31 @@ def splitting_index(data: bytes, g: int) -> bytes:
             p += bs
     ent.append(len(data) << 16)
     return b"".join(struct.pack(">Q", v) for v in ent)
+
+
+def writable_encode(data: bytes) -> bytes:
+    """SAMRecordWritable.write of every record, concatenated: each record is
+    re-serialized from its parsed fields the way [htsjdk] BAMRecordCodec.encode
+    does (block_size recomputed from the field lengths + attribute bytes,
+    indexBin 0 for refID < 0, rest written back verbatim)."""
+    bl, ustart, u = inflate(data)
+    l_text = struct.unpack_from("<i", u, 4)[0]
+    p = 8 + l_text
+    n_ref = struct.unpack_from("<i", u, p)[0]
+    p += 4
+    for _ in range(n_ref):
+        ln = struct.unpack_from("<i", u, p)[0]
+        p += 4 + ln + 4
+    out = []
+    while len(u) - p >= 4:
+        bs = struct.unpack_from("<i", u, p)[0]
+        (ref, pos0, lrn, mapq, bin_, ncig, flag, lseq, nref, npos,
+         tlen) = struct.unpack_from("<iiBBHHHiiii", u, p + 4)
+        rest = u[p + 36:p + 4 + bs]
+        var = lrn + 4 * ncig + (lseq + 1) // 2 + lseq
+        attrs = len(rest) - var
+        out.append(struct.pack("<iiiBBHHHiiii", 32 + var + attrs, ref, pos0, lrn, mapq,
+                               bin_ if ref >= 0 else 0, ncig, flag, lseq, nref, npos, tlen))
+        out.append(rest)
+        p += 4 + bs
+    return b"".join(out)
