@@ -76,7 +76,7 @@ def extra_configs(c2, c2_info):
         "uncompressed_GBps": round(c2_info["uncompressed"] / dt / 1e9, 3),
         "note": "first call: includes inflating every block (resident compressed file)"}
     f.close()
-    data, info = synth.make_bam(3000, mode="long", as_numpy=True, seed=0x48424D04)
+    data, info = synth.make_bam(12000, mode="long", as_numpy=True, seed=0x48424D04)
     g = hbam.Gpu(0)
     g.load(data)
     g.run(timing=True)

@@ -68,6 +68,13 @@ struct Columns {
   int64_t *key;
   uint64_t *voff, *rest_off;
   uint32_t *rest_len;
+  // Keys whose Murmur input (the rest) is longer than kLongHash bytes are
+  // deferred to k_long_hash (one wave per record): decode appends the record
+  // index here (nullptr: hash inline).
+  uint64_t* long_rec;
+  uint32_t* long_n;
+  uint32_t long_cap;
 };
+constexpr uint32_t kLongHash = 2048;
 
 }  // namespace hbam

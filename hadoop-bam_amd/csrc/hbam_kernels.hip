@@ -2026,10 +2026,79 @@ __device__ __forceinline__ void decode_record(const uint8_t* __restrict__ u, uin
   if (!((flag & 4) || ref < 0 || start < 0)) {
     key = (int64_t)(((uint64_t)(int64_t)ref << 32) | (uint64_t)(int64_t)(int32_t)(start - 1));
   } else {
+    if (col.long_rec && (uint32_t)(bs - 32) > kLongHash) {  // long rest: k_long_hash
+      const uint32_t slot = atomicAdd(col.long_n, 1u);
+      if (slot < col.long_cap) {
+        col.long_rec[slot] = i;
+        return;
+      }
+    }
     const int32_t h = (int32_t)murmur3_dev(u, q + 36, (uint32_t)(bs - 32), 0);
     key = (int64_t)((0x7fffffffull << 32) | (uint64_t)(int64_t)h);
   }
   col.key[i] = key;
+}
+
+// Murmur keys of long unmapped records (C4-like reads: the rest is tens of
+// KB), one wave per record.  The per-block input mixing (k1*c1, rotl, *c2 and
+// the k2 twin) is independent across 16 B blocks, so the 64 lanes do it for
+// 64 consecutive blocks from one coalesced 1 KB load; only the h1/h2 chain is
+// serial, and it runs on wave-uniform values (scalar ALU) fed by readlane.
+__global__ __launch_bounds__(64) void k_long_hash(const uint8_t* __restrict__ u, const uint64_t* __restrict__ rec_pos,
+                                                  Columns col) {
+  const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+  const uint32_t lane = lane_id();
+  const uint32_t nrec = min(*col.long_n, col.long_cap);
+  for (uint32_t li = blockIdx.x; li < nrec; li += gridDim.x) {
+    const uint64_t i = col.long_rec[li];
+    const uint64_t q = rec_pos[i];
+    const uint32_t len = ldu32(u, q) - 32u;
+    const uint64_t off = q + 36;
+    uint64_t h1 = 0, h2 = 0;  // seed 0 (BAMRecordReader.java:101)
+    const uint32_t nblocks = len / 16;
+    for (uint32_t c = 0; c < nblocks; c += 64) {
+      const uint32_t b = c + lane;
+      uint64_t k1 = 0, k2 = 0;
+      if (b < nblocks) {
+        k1 = ldu64(u, off + 16ull * b);
+        k2 = ldu64(u, off + 16ull * b + 8);
+      }
+      k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2;
+      k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1;
+      const uint32_t k1lo = (uint32_t)k1, k1hi = (uint32_t)(k1 >> 32);
+      const uint32_t k2lo = (uint32_t)k2, k2hi = (uint32_t)(k2 >> 32);
+      const uint32_t m = min(64u, nblocks - c);
+      for (uint32_t j = 0; j < m; ++j) {  // util/MurmurHash3.java:48-60, :59 quirk
+        const uint64_t K1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)k1hi, (int)j) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)k1lo, (int)j);
+        const uint64_t K2 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)k2hi, (int)j) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)k2lo, (int)j);
+        h1 ^= K1;
+        h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+        h2 ^= K2;
+        h2 = (h2 << 31) | (h1 >> 33); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+      }
+    }
+    const uint64_t t = off + 16ull * nblocks;
+    const uint32_t r = len & 15;
+    if (r) {  // tail (:62-88), as murmur3_dev
+      const uint64_t lo = ldu64(u, t), hi = ldu64(u, t + 8);
+      if (r > 8) {
+        uint64_t k2 = hi & (~0ull >> (64 - 8 * (r - 8)));
+        k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+      }
+      uint64_t k1 = r >= 8 ? lo : (lo & (~0ull >> (64 - 8 * r)));
+      k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    }
+    h1 ^= (uint64_t)len;
+    h2 ^= (uint64_t)len;
+    h1 += h2;
+    h2 += h1;
+    h1 = fmix64(h1);
+    h2 = fmix64(h2);
+    h1 += h2;
+    if (lane == 0) col.key[i] = (int64_t)((0x7fffffffull << 32) | (uint64_t)(int64_t)(int32_t)h1);
+  }
 }
 
 __global__ void k_rec_decode(const uint8_t* __restrict__ u, const uint64_t* __restrict__ rec_pos, uint64_t n,
@@ -2778,6 +2847,12 @@ hipError_t launch_wr_encode(const uint8_t* u, uint64_t p0, uint64_t nbytes, cons
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_wr_bin_patch, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, rec_pos, ref_id, bin, n, p0,
                      dst);
+  return hipGetLastError();
+}
+hipError_t launch_long_hash(const uint8_t* u, const uint64_t* rec_pos, const Columns& col, hipStream_t s) {
+  if (!col.long_rec || col.long_cap == 0) return hipSuccess;
+  const uint32_t grid = std::min<uint32_t>(col.long_cap, 256u * 16u);
+  hipLaunchKernelGGL(k_long_hash, dim3(grid), dim3(64), 0, s, u, rec_pos, col);
   return hipGetLastError();
 }
 hipError_t launch_wr_decode(const uint8_t* buf, uint64_t len, const uint64_t* offs, uint64_t n, const Columns& col,

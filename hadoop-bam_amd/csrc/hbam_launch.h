@@ -79,6 +79,8 @@ hipError_t launch_first_error_hout(const HuffOut* hout, uint32_t b0, uint32_t nb
 hipError_t launch_first_error_i32(const int32_t* err, uint32_t nb, uint32_t* first, hipStream_t s);
 hipError_t launch_truncate_counts(uint32_t* cnt, uint32_t nb, const uint32_t* cut, hipStream_t s);
 hipError_t launch_sbi_emit(const uint64_t* voff, uint64_t n, uint32_t g, uint64_t* ent, hipStream_t s);
+// keys deferred by decode_record (rest > kLongHash bytes): one wave per record
+hipError_t launch_long_hash(const uint8_t* u, const uint64_t* rec_pos, const Columns& col, hipStream_t s);
 // SAMRecordWritable.write of a span's records: u[p0, p0+nbytes) -> dst
 // (16 B-aligned, room for nbytes rounded up to 16) + bin patches (refID < 0)
 hipError_t launch_wr_encode(const uint8_t* u, uint64_t p0, uint64_t nbytes, const uint64_t* rec_pos,

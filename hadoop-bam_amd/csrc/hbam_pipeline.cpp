@@ -624,7 +624,7 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
   const bool dec = decode && mode == kReader;
   Columns c{};
   if (dec) {
-    int rc = alloc_columns(total, &c);
+    int rc = alloc_columns(total, total_u_, &c);
     if (rc != kOk) return rc;
     out->col = c;
   }
@@ -636,6 +636,7 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
     if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
     if (dec) HIPCHK(launch_rec_decode(du_.p, rec_pos_.p, total, c, stream_));
   }
+  if (dec) HIPCHK(launch_long_hash(du_.p, rec_pos_.p, c, stream_));
   if (timing) HIPCHK(hipEventRecord(ev_[2], stream_));
   HIPCHK(hipStreamSynchronize(stream_));
   if (timing) {
@@ -649,7 +650,7 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
   return kOk;
 }
 
-int Pipeline::alloc_columns(uint64_t total, Columns* cp) {
+int Pipeline::alloc_columns(uint64_t total, uint64_t stream_bytes, Columns* cp) {
   // SoA backing store: 8-byte columns first, then 4, 2, 1 (alignment)
   const uint64_t n = std::max<uint64_t>(total, 1);
   const uint64_t per = 8 * 2 + 4 * 7 + 2 * 3 + 1 * 2;
@@ -680,6 +681,14 @@ int Pipeline::alloc_columns(uint64_t total, Columns* cp) {
   c.flag = reinterpret_cast<uint16_t*>(take(2 * n));
   c.l_read_name = take(n);
   c.mapq = take(n);
+  // deferred long-record keys: at most one per kLongHash stream bytes
+  const uint64_t cap = std::min<uint64_t>(stream_bytes / kLongHash + 64, 0xffffffffull);
+  HIPCHK(long_rec_.reserve(cap));
+  HIPCHK(long_n_.reserve(1));
+  HIPCHK(hipMemsetAsync(long_n_.p, 0, 4, stream_));
+  c.long_rec = long_rec_.p;
+  c.long_n = long_n_.p;
+  c.long_cap = (uint32_t)cap;
   return kOk;
 }
 
@@ -721,9 +730,10 @@ int Pipeline::decode_writables(const uint8_t* buf, uint64_t len, const uint64_t*
   if (n) HIPCHK(hipMemcpyAsync(woffs_.p, offs, n * 8, hipMemcpyHostToDevice, stream_));
   HIPCHK(hipMemsetAsync(wbad_.p, 0xff, sizeof(unsigned long long), stream_));
   Columns c{};
-  int rc = alloc_columns(n, &c);
+  int rc = alloc_columns(n, len, &c);
   if (rc != kOk) return rc;
   HIPCHK(launch_wr_decode(wbuf_.p, len, woffs_.p, n, c, rec_pos_.p, wbad_.p, stream_));
+  HIPCHK(launch_long_hash(wbuf_.p, rec_pos_.p, c, stream_));
   unsigned long long bad = ~0ull;
   HIPCHK(hipMemcpyAsync(&bad, wbad_.p, sizeof bad, hipMemcpyDeviceToHost, stream_));
   HIPCHK(hipStreamSynchronize(stream_));

@@ -125,7 +125,8 @@ class Pipeline {
 
  private:
   int fail(int code, const std::string& msg);
-  int alloc_columns(uint64_t n, Columns* c);  // SoA store for n records (voff = rec_voff_)
+  // SoA store for n records (voff = rec_voff_) + the deferred long-key list
+  int alloc_columns(uint64_t n, uint64_t stream_bytes, Columns* c);
   int hip_check(hipError_t e, const char* what);
 
   int device_ = 0;
@@ -166,6 +167,8 @@ class Pipeline {
   DevBuf<uint8_t> scan_tmp_;
   DevBuf<uint8_t> cols_;  // SoA backing store
   uint64_t cols_cap_ = 0;
+  DevBuf<uint64_t> long_rec_;            // records whose key k_long_hash computes
+  DevBuf<uint32_t> long_n_;
   DevBuf<uint8_t> wbuf_;                 // readFields: serialized values
   DevBuf<uint64_t> woffs_;               // readFields: value framing
   DevBuf<unsigned long long> wbad_;      // readFields: first bad value

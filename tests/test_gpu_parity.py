@@ -116,6 +116,7 @@ SYNTH = [
     dict(n_records=2500, strategy="filtered"),
     dict(n_records=800, all_unmapped=True, block_payload=65498, eof_block=False),  # test.bam-like
     dict(n_records=40, mode="long"),                    # records span many blocks
+    dict(n_records=60, mode="long", all_unmapped=True),  # every key through k_long_hash
     dict(n_records=2000, block_payload=4096),           # small blocks, many straddles
     dict(n_records=500, block_payload=65536 - 1024, level=6),
     dict(n_records=3000, block_payload=65536, level=6),  # ISIZE 65536: phase-B round path

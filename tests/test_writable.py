@@ -124,8 +124,11 @@ def test_gpu_encode_split_spans_concatenate(test_bam):
 
 
 @pytest.mark.gpu
-def test_gpu_readfields_matches_oracle():
-    data, _ = synth.make_bam(5000, seed=0x57524956)
+@pytest.mark.parametrize("mode", ["short", "long"])
+def test_gpu_readfields_matches_oracle(mode):
+    # long: ONT-like unmapped records take the deferred k_long_hash key path
+    data, _ = synth.make_bam(5000 if mode == "short" else 80, mode=mode, all_unmapped=mode == "long",
+                             seed=0x57524956)
     _, enc, offs = _oracle_encode(data)
     # frame with gaps, as a shuffle stream would (a vint length before each value)
     gap = 3
