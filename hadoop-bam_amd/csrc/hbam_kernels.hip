@@ -1387,6 +1387,17 @@ constexpr int kLzPf = HBAM_LZ_PF;
 #define HBAM_LZ_RING 4
 #endif
 constexpr int kLzRing = HBAM_LZ_RING;
+// phase-B fill: 64-token groups taken dynamically by waves (1) instead of
+// static token ranges (0).  Measured on C2: the waits vanish but the fill
+// itself doubles (the fill is issue-bound across all 16 waves, not
+// imbalanced): 7.91 vs 7.14 ms per pass.  Kept for reference, off.
+#ifndef HBAM_LZ_DYN
+#define HBAM_LZ_DYN 0
+#endif
+// phase-B resolve: two independent chases per thread per pass
+#ifndef HBAM_LZ_DUAL
+#define HBAM_LZ_DUAL 1
+#endif
 
 // exclusive scan over the workgroup; returns the prefix, *total = sum
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
@@ -1464,6 +1475,10 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
   // map index = o0 + position, so 16-byte output segments read 32 B-aligned LDS
   __shared__ __attribute__((aligned(16))) uint16_t map[kMapMax + 32];
   __shared__ uint32_t scratch[kLzWaves];
+#if HBAM_LZ_DYN
+  __shared__ uint16_t gpos[1024 + 2];  // output position of each 64-token group
+  __shared__ uint32_t gnext;           // next group to take
+#endif
   // optional cycle profile (thread 0): [6] token loads [0] block scan
   // [1] map fill (wave 0's own work) [2] fill barrier wait [3] resolve
   // [4] store [5] total
@@ -1506,6 +1521,94 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
     return;
   }
 
+#if HBAM_LZ_DYN
+  // 1. per-group byte totals (a group = 64 consecutive tokens, one per lane;
+  //    G <= 1020 since every token emits >= 1 byte and isize <= 65280),
+  //    scanned over the workgroup into gpos[] (clamped to isize: u16).
+  const uint32_t wid = tid >> 6, lane = tid & 63;
+  const uint32_t G = (ntok + 63) >> 6;
+  for (uint32_t g0 = wid; g0 < G; g0 += 4 * kLzWaves) {  // 4 group loads in flight per wave
+    uint32_t tv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t i = (g0 + k * kLzWaves) * 64 + lane;
+      tv[k] = i < ntok ? tk[i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t g = g0 + k * kLzWaves;
+      const uint32_t i = g * 64 + lane;
+      uint32_t v = i < ntok ? tok_len(tv[k]) : 0u;
+#pragma unroll
+      for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+      if (lane == 0 && g < G) gpos[g] = (uint16_t)v;  // <= 64 * 258
+    }
+  }
+  if (tid == 0) gnext = kLzWaves;  // groups 0..15 are taken statically below
+  __syncthreads();
+  LZ_T(6);
+  {
+    uint32_t total;
+    const uint32_t v = tid < G ? gpos[tid] : 0u;
+    const uint32_t pre = block_excl_scan(v, scratch, &total);  // both barriers inside
+    if (tid < G) gpos[tid] = (uint16_t)min(pre, isize);
+    if (tid == 0) gpos[G] = (uint16_t)min(total, isize);
+  }
+  __syncthreads();
+  LZ_T(0);
+
+  // 2. map fill.  Waves take 64-token groups dynamically (LDS counter), so a
+  //    wave that drew long matches does not hold the others at the barrier.
+  //    A token is an arithmetic run of entries base + k*delta (match: source
+  //    position, 1; literal pair: tag|b0, b1-b0).  (i) every 8-entry aligned
+  //    chunk that starts inside a token is written whole by that token with
+  //    one ds_write_b128 -- entries past the token's end are wrong but belong
+  //    to later tokens of the same group; (ii) then each token writes its head
+  //    (its entries before its first chunk boundary) one by one, overwriting
+  //    them.  Chunks never cross the group's range end, so groups stay
+  //    disjoint.
+  uint16_t* m = map + o0;
+  uint32_t g = wid;
+  uint32_t tcur = g * 64 + lane < ntok ? tk[g * 64 + lane] : 0u;
+  while (g < G) {  // wave-uniform
+    uint32_t gn = 0;
+    if (lane == 0) gn = atomicAdd(&gnext, 1u);
+    gn = rfl(gn);
+    const uint32_t tnext = gn * 64 + lane < ntok && gn < G ? tk[gn * 64 + lane] : 0u;  // in flight meanwhile
+    const uint32_t i = g * 64 + lane;
+    const uint32_t t = tcur;
+    const uint32_t P = gpos[g], ghi = gpos[g + 1];
+    const uint32_t len = i < ntok ? tok_len(t) : 0u;
+    const uint32_t incl = wave_incl_scan_dpp(len);
+    const uint32_t pos = P + incl - len;
+    const uint32_t end = min(pos + len, ghi);
+    uint32_t base, delta;
+    if (t >> 31) {
+      base = pos - (((t >> 16) & 0x7fffu) + 1);  // dist <= pos: checked in phase A
+      delta = 1;
+    } else {
+      base = kLitTag | (t & 0xffu);
+      delta = (((t >> 8) & 0xffu) - (t & 0xffu)) & 0xffffu;
+    }
+    const uint32_t hb = min(end, ((o0 + pos + 7) & ~7u) - o0);  // head end = first chunk start
+    for (uint32_t q = hb; q < end; q += 8) {
+      const uint32_t v0 = base + (q - pos) * delta;
+      if (q + 8 <= ghi) {
+        const uint32_t d0 = (v0 & 0xffffu) | ((v0 + delta) << 16);
+        const uint32_t inc = (2u * delta) * 0x10001u;
+        *reinterpret_cast<uint4*>(m + q) = make_uint4(d0, d0 + inc, d0 + 2u * inc, d0 + 3u * inc);
+      } else {
+        uint32_t v = v0;
+        for (uint32_t r = q; r < ghi; ++r, v += delta) m[r] = (uint16_t)v;
+      }
+    }
+    wave_sync();  // (i) before (ii): they overlap across lanes
+    uint32_t v = base;
+    for (uint32_t r = pos; r < hb; ++r, v += delta) m[r] = (uint16_t)v;
+    g = gn;
+    tcur = tnext;
+  }
+#else
   // 1. wave w expands tokens [w*TW, (w+1)*TW); its output range starts at
   //    the byte total of the waves before it (coalesced token loads).
   const uint32_t wid = tid >> 6, lane = tid & 63;
@@ -1577,6 +1680,7 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
     uint32_t v = base;
     for (uint32_t r = pos; r < hb; ++r, v += delta) m[r] = (uint16_t)v;
   }
+#endif
   LZ_T(1);
   __syncthreads();
   LZ_T(2);
@@ -1586,6 +1690,25 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
   //    dependent LDS latency per chase step, so the raw entries of this
   //    thread's next positions (written by fill, rewritten only by this
   //    thread) are loaded kLzPf rounds ahead.
+#if HBAM_LZ_DUAL
+  // two rounds per pass: the chases of positions q and q + 1024 are
+  // independent, so their dependent LDS loads overlap (any visiting order is
+  // correct: entries always point to smaller positions and a chase ends at a
+  // literal, resolved or not)
+  for (uint32_t q = tid; q < isize; q += 2 * kLzThreads) {
+    const uint32_t q2 = q + kLzThreads;
+    const bool has2 = q2 < isize;
+    uint32_t v1 = m[q], v2 = has2 ? m[q2] : kLitTag;
+    while ((v1 < kLitTag) | (v2 < kLitTag)) {
+      const uint32_t n1 = v1 < kLitTag ? m[v1] : v1;
+      const uint32_t n2 = v2 < kLitTag ? m[v2] : v2;
+      v1 = n1;
+      v2 = n2;
+    }
+    m[q] = (uint16_t)v1;
+    if (has2) m[q2] = (uint16_t)v2;
+  }
+#else
   {
     uint32_t pre[kLzPf];
 #pragma unroll
@@ -1603,6 +1726,7 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
       m[q] = (uint16_t)v;
     }
   }
+#endif
   __syncthreads();
   LZ_T(3);
 
