@@ -135,8 +135,8 @@ def pmc_traffic(kernels):
     try:
         ks = json.load(open(best[-1]))["kernels"]
         tot = 0.0
-        for k in kernels:
-            e = ks[k]
+        for k in kernels:  # phase A is templated on LDS staging: C2 runs the staged instance
+            e = ks[k] if k in ks else ks[k + "<true>"]
             tot += e["main_fetch_bytes_corrected"] + e["main_write_bytes"]
         return int(tot), os.path.relpath(best[-1], ROOT)
     except (KeyError, ValueError, OSError):
@@ -152,7 +152,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save-bam", default=None)
-    ap.add_argument("--no-extra", action="store_true", help="skip the C4 / index side measurements")
+    ap.add_argument("--no-extra", action="store_true", help="skip the C4 / index side measurements (the io legs always run at N=1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -250,8 +250,9 @@ def main():
                      "alg_bytes_per_launch": int(alg_bytes)},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_extra:
+    if rank == 0 and world == 1:
         out["io"] = host_and_copy_legs(g, data, info, ms_step)
+    if rank == 0 and world == 1 and not args.no_extra:
         g.close()
         out["extra"] = extra_configs(data, info)
     if rank == 0 and not args.no_cpu_baseline:

@@ -196,7 +196,12 @@ constexpr int kHuffWaves = kHuffThreads / 64;
 #ifndef HBAM_HUFF_STAGE
 #define HBAM_HUFF_STAGE 1
 #endif
-constexpr bool kHuffStage = HBAM_HUFF_STAGE != 0;  // compressed block staged in LDS
+// Phase A reads the compressed block from an LDS copy (staged) or straight
+// from HBM/L2.  1 = per chunk: staged while the workgroup's LDS (tables +
+// the chunk's largest block) leaves room for 4 workgroups per CU, else
+// unstaged (C4: 7.4 -> 3.9 ms; C2: staged 7.6 vs 8.0 ms); 0 = never, 2 = always.
+constexpr int kHuffStageMode = HBAM_HUFF_STAGE;
+constexpr uint32_t kHuffStageMaxLds = 40 * 1024;
 
 // Wave-local ordering of LDS traffic (code run by one wave only).
 __device__ __forceinline__ void wave_sync() {
@@ -1047,6 +1052,7 @@ constexpr uint32_t kHuffStaticBytes = kHuffLdsBytes + kHuffCtlBytes;
 #ifndef HBAM_HUFF_WPE
 #define HBAM_HUFF_WPE 5  // waves per SIMD (VGPR cap 96; measured best on C2)
 #endif
+template <bool STAGE>
 __global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(const uint8_t* __restrict__ file,
                                                                const BlockInfo* __restrict__ blocks, uint32_t b0,
                                                                uint64_t chunk_ustart, uint32_t* __restrict__ tokens,
@@ -1086,7 +1092,7 @@ __global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(co
   const uint64_t abase = sbyte & ~15ull;
   const HuffTableInfo ti = tinfo[blockIdx.x];
   {  // stage the block (+16 B of zero-padded file) and its prebuilt tables in LDS
-    if (kHuffStage) {
+    if (STAGE) {
       const uint32_t nq = (uint32_t)((blk.coff + blk.csize - abase + 15) >> 4) + 1;
       const uint4* __restrict__ src = reinterpret_cast<const uint4*>(file + abase);
       for (uint32_t i = tid; i < nq; i += kHuffThreads) s_in[i] = src[i];
@@ -1099,9 +1105,9 @@ __global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(co
   }
   __syncthreads();
   PROF_T(0);
-  // compressed bits: the LDS copy, or (HBAM_HUFF_STAGE=0) the file in HBM
+  // compressed bits: the LDS copy, or (unstaged) the file in HBM
   const uint32_t* __restrict__ W =
-      kHuffStage ? reinterpret_cast<const uint32_t*>(s_in) : reinterpret_cast<const uint32_t*>(file + abase);
+      STAGE ? reinterpret_cast<const uint32_t*>(s_in) : reinterpret_cast<const uint32_t*>(file + abase);
   const uint32_t E = 8u * ((uint32_t)(sbyte - abase) + (blk.csize - 26));  // end of CDATA (bits from W)
 
   SReader R;  // wave 0's reader
@@ -1381,12 +1387,12 @@ constexpr uint32_t kLitTag = 0xFF00u;
 #ifndef HBAM_LZ_PF
 #define HBAM_LZ_PF 1
 #endif
-constexpr int kLzPf = HBAM_LZ_PF;
+[[maybe_unused]] constexpr int kLzPf = HBAM_LZ_PF;
 // phase-B fill: 64-token groups loaded ahead (4 vs 8 measured equal)
 #ifndef HBAM_LZ_RING
 #define HBAM_LZ_RING 4
 #endif
-constexpr int kLzRing = HBAM_LZ_RING;
+[[maybe_unused]] constexpr int kLzRing = HBAM_LZ_RING;
 // phase-B fill: 64-token groups taken dynamically by waves (1) instead of
 // static token ranges (0).  Measured on C2: the waits vanish but the fill
 // itself doubles (the fill is issue-bound across all 16 waves, not
@@ -2772,14 +2778,19 @@ static hipError_t launch_huff(const uint8_t* file, const BlockInfo* blocks, uint
   if (e0 != hipSuccess) return e0;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_inflate_huff),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_inflate_huff<true>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  const uint32_t lds = kHuffStaticBytes + (kHuffStage ? ((max_stage + 15) & ~15u) : 0u);
-  hipLaunchKernelGGL(k_inflate_huff, dim3(nb), dim3(kHuffThreads), lds, s, file, blocks, b0, chunk_ustart, tokens,
-                     hout, tables, tinfo, g_huff_prof);
+  const uint32_t staged_lds = kHuffStaticBytes + ((max_stage + 15) & ~15u);
+  const bool stage = kHuffStageMode == 2 || (kHuffStageMode == 1 && staged_lds <= kHuffStageMaxLds);
+  if (stage)
+    hipLaunchKernelGGL(k_inflate_huff<true>, dim3(nb), dim3(kHuffThreads), staged_lds, s, file, blocks, b0,
+                       chunk_ustart, tokens, hout, tables, tinfo, g_huff_prof);
+  else
+    hipLaunchKernelGGL(k_inflate_huff<false>, dim3(nb), dim3(kHuffThreads), kHuffStaticBytes, s, file, blocks, b0,
+                       chunk_ustart, tokens, hout, tables, tinfo, g_huff_prof);
   return hipGetLastError();
 }
 hipError_t launch_inflate(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,

@@ -77,7 +77,8 @@ def main_dispatch_durations(d):
     return out
 
 
-INFLATE = ("hbam::k_huff_tables", "hbam::k_inflate_huff", "hbam::k_inflate_lz77")
+INFLATE = ("hbam::k_huff_tables", "hbam::k_inflate_huff", "hbam::k_inflate_huff<true>",
+           "hbam::k_inflate_huff<false>", "hbam::k_inflate_lz77")
 
 
 def inflate_stage_spans(d):
