@@ -459,6 +459,42 @@ int hbam_gpu_run(hbam_gpu* g, int32_t flags, hbam_gpu_stats* st) {
   return g->span.status;
 }
 
+int hbam_gpu_run_streamed(hbam_gpu* g, const void* data, uint64_t len, uint64_t piece_bytes, hbam_gpu_stats* st) {
+  memset(st, 0, sizeof *st);
+  hbam::Pipeline& p = *g->p;
+  p.timing = false;
+  const uint64_t il0 = p.inflate_launches();
+  g->span = hbam::SpanDev();
+  int rc = p.run_streamed(static_cast<const uint8_t*>(data), len, piece_bytes, g->first_pos, &g->span, &st->ms_total);
+  if (rc != HBAM_OK) {
+    g->err = p.error();
+    st->status = rc;
+    return rc;
+  }
+  st->n_blocks = p.blocks().size();
+  st->compressed_bytes = p.file_len();
+  st->inflated_bytes = p.total_u();
+  st->records = g->span.n;
+  st->status = g->span.status;
+  st->inflate_launches = (int32_t)(p.inflate_launches() - il0);
+  if (g->span.n) {
+    (void)hipMemcpy(&st->first_voff, g->span.rec_voff, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(&st->last_voff, g->span.rec_voff + g->span.n - 1, 8, hipMemcpyDeviceToHost);
+  }
+  if (g->span.status != HBAM_OK) g->err = g->span.error;
+  return g->span.status;
+}
+
+void* hbam_host_alloc(uint64_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+
+void hbam_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
 int hbam_gpu_reload(hbam_gpu* g, const void* data, uint64_t len, int32_t pinned, float* ms) {
   *ms = 0;
   int rc = g->p->reload(static_cast<const uint8_t*>(data), len, pinned != 0, ms);

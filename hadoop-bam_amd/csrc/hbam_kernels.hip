@@ -53,7 +53,7 @@ __device__ __forceinline__ uint64_t ldu64(const uint8_t* base, uint64_t off) {
 // exact framing htsjdk writes and requires (XLEN==6), plus the BC subfield id
 // for selectivity.  Candidates are appended unordered, sorted, then the BSIZE
 // chain is verified; any break falls back to the serial walk (bgzf_walk).
-__global__ void k_bgzf_scan(const uint8_t* __restrict__ buf, uint64_t len, uint64_t base,
+__global__ void k_bgzf_scan(const uint8_t* __restrict__ buf, uint64_t len, uint64_t base, uint64_t from,
                             uint64_t* __restrict__ cand, uint32_t cap, uint32_t* __restrict__ count) {
   // buf = first byte of the loaded range (16 B aligned, zero padded past
   // len); 16 positions per thread from one 16 B load + the next word;
@@ -69,7 +69,7 @@ __global__ void k_bgzf_scan(const uint8_t* __restrict__ buf, uint64_t len, uint6
       const uint32_t magic = __builtin_amdgcn_alignbyte(w[(s >> 2) + 1], w[s >> 2], s & 3);
       if (magic != 0x04088b1fu) continue;
       const uint64_t p = 16 * t + s;
-      if (p + 18 > len) continue;
+      if (p + 18 > len || base + p < from) continue;
       const uint32_t xlen = ldu32(buf, p + 10) & 0xffffu;
       const uint32_t sub = ldu32(buf, p + 12);
       if (xlen != 6 || sub != 0x00024342u) continue;
@@ -81,9 +81,11 @@ __global__ void k_bgzf_scan(const uint8_t* __restrict__ buf, uint64_t len, uint6
 
 // Verify the sorted candidate chain and fill BlockInfo.  flags[0] |= 1 on any
 // break (fallback), flags[1] = first block index with ISIZE > 64 KiB.
+// partial (streamed upload, bytes past hi not there yet): a last candidate
+// whose block runs past hi is the incomplete tail -> flags[2] = 1, not a break.
 __global__ void k_bgzf_verify(const uint8_t* __restrict__ file, uint64_t lo, uint64_t hi,
                               const uint64_t* __restrict__ cand, uint32_t n,
-                              BlockInfo* __restrict__ blocks, uint32_t* __restrict__ flags) {
+                              BlockInfo* __restrict__ blocks, uint32_t* __restrict__ flags, uint32_t partial) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint64_t c = cand[i];
@@ -91,6 +93,10 @@ __global__ void k_bgzf_verify(const uint8_t* __restrict__ file, uint64_t lo, uin
   uint32_t total = (ldu32(file, c + 16) & 0xffffu) + 1;
   uint64_t next = c + total;
   uint64_t expect = (i + 1 < n) ? cand[i + 1] : hi;
+  if (partial && i + 1 == n && next > hi && total >= 26) {
+    flags[2] = 1u;
+    return;
+  }
   if (next != expect || total < 26) {
     atomicOr(&flags[0], 1u);
     return;
@@ -108,17 +114,19 @@ __global__ void k_bgzf_verify(const uint8_t* __restrict__ file, uint64_t lo, uin
 
 // Serial fallback: walk BSIZE from lo with htsjdk's framing rules.
 // out[0] = nblocks, out[1] = status, out[2] = failing offset (low 32), out[3] = hi 32.
+// partial: a block cut by hi ends the walk cleanly (out[2..3] = its start).
 __global__ void k_bgzf_walk(const uint8_t* __restrict__ file, uint64_t lo, uint64_t hi,
-                            BlockInfo* __restrict__ blocks, uint32_t cap, uint32_t* __restrict__ out) {
+                            BlockInfo* __restrict__ blocks, uint32_t cap, uint32_t* __restrict__ out,
+                            uint32_t partial) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   uint64_t p = lo;
   uint32_t n = 0;
   int st = kOk;
   while (p < hi) {
-    if (hi - p < 18) { st = kErrIO; break; }
+    if (hi - p < 18) { st = partial ? kOk : kErrIO; break; }
     uint32_t total = (ldu32(file, p + 16) & 0xffffu) + 1;
     if (total < 18) { st = kErrIO; break; }
-    if (p + total > hi) { st = kErrTrunc; break; }
+    if (p + total > hi) { st = partial ? kOk : kErrTrunc; break; }
     uint32_t w0 = ldu32(file, p);
     uint32_t xlen = ldu32(file, p + 10) & 0xffffu;
     if (w0 != 0x04088b1fu || xlen != 6 || total < 26) { st = kErrFormat; break; }
@@ -144,9 +152,10 @@ __global__ void k_block_isize(const BlockInfo* __restrict__ blocks, uint32_t n, 
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) isz[i] = blocks[i].isize;
 }
-__global__ void k_block_ustart(BlockInfo* __restrict__ blocks, uint32_t n, const uint64_t* __restrict__ us) {
+__global__ void k_block_ustart(BlockInfo* __restrict__ blocks, uint32_t n, const uint64_t* __restrict__ us,
+                               uint64_t base) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) blocks[i].ustart = us[i];
+  if (i < n) blocks[i].ustart = base + us[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -2726,27 +2735,31 @@ static inline unsigned grid_for(uint64_t n, unsigned bs, unsigned cap = 65535u *
   return (unsigned)g;
 }
 
-hipError_t launch_bgzf_scan(const uint8_t* file, uint64_t lo, uint64_t hi, uint64_t* cand, uint32_t cap,
-                            uint32_t* count, hipStream_t s) {
-  // file + lo is the start of the device buffer (hipMalloc: 256 B aligned)
-  const uint64_t nc = (hi - lo + 15) / 16;
-  hipLaunchKernelGGL(k_bgzf_scan, dim3(grid_for(nc, 256, 8192)), dim3(256), 0, s, file + lo, hi - lo, lo, cand, cap,
-                     count);
+hipError_t launch_bgzf_scan(const uint8_t* file, uint64_t buf_base, uint64_t lo, uint64_t hi, uint64_t* cand,
+                            uint32_t cap, uint32_t* count, hipStream_t s) {
+  // scan from the position at or below lo that is 16 B aligned in the device
+  // buffer (file + buf_base = the buffer start, hipMalloc-aligned);
+  // candidates below lo are dropped
+  const uint64_t a = buf_base + ((lo - buf_base) & ~15ull);
+  const uint64_t nc = (hi - a + 15) / 16;
+  hipLaunchKernelGGL(k_bgzf_scan, dim3(grid_for(nc, 256, 8192)), dim3(256), 0, s, file + a, hi - a, a, lo, cand,
+                     cap, count);
   return hipGetLastError();
 }
 hipError_t launch_bgzf_verify(const uint8_t* file, uint64_t lo, uint64_t hi, const uint64_t* cand, uint32_t n,
-                              BlockInfo* blocks, uint32_t* flags, hipStream_t s) {
+                              BlockInfo* blocks, uint32_t* flags, uint32_t partial, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_bgzf_verify, dim3((n + 255) / 256), dim3(256), 0, s, file, lo, hi, cand, n, blocks, flags);
+  hipLaunchKernelGGL(k_bgzf_verify, dim3((n + 255) / 256), dim3(256), 0, s, file, lo, hi, cand, n, blocks, flags,
+                     partial);
   return hipGetLastError();
 }
 hipError_t launch_bgzf_walk(const uint8_t* file, uint64_t lo, uint64_t hi, BlockInfo* blocks, uint32_t cap,
-                            uint32_t* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_bgzf_walk, dim3(1), dim3(64), 0, s, file, lo, hi, blocks, cap, out);
+                            uint32_t* out, uint32_t partial, hipStream_t s) {
+  hipLaunchKernelGGL(k_bgzf_walk, dim3(1), dim3(64), 0, s, file, lo, hi, blocks, cap, out, partial);
   return hipGetLastError();
 }
 hipError_t launch_block_ustart(BlockInfo* blocks, uint32_t n, uint64_t* tmp_isize, uint64_t* tmp_ustart,
-                               void* scan_tmp, size_t* scan_bytes, hipStream_t s) {
+                               void* scan_tmp, size_t* scan_bytes, uint64_t base, hipStream_t s) {
   if (scan_tmp == nullptr) {  // size query
     return hipcub::DeviceScan::ExclusiveSum(nullptr, *scan_bytes, tmp_isize, tmp_ustart, (int)n, s);
   }
@@ -2754,7 +2767,7 @@ hipError_t launch_block_ustart(BlockInfo* blocks, uint32_t n, uint64_t* tmp_isiz
   hipLaunchKernelGGL(k_block_isize, dim3((n + 255) / 256), dim3(256), 0, s, blocks, n, tmp_isize);
   hipError_t e = hipcub::DeviceScan::ExclusiveSum(scan_tmp, *scan_bytes, tmp_isize, tmp_ustart, (int)n, s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_block_ustart, dim3((n + 255) / 256), dim3(256), 0, s, blocks, n, tmp_ustart);
+  hipLaunchKernelGGL(k_block_ustart, dim3((n + 255) / 256), dim3(256), 0, s, blocks, n, tmp_ustart, base);
   return hipGetLastError();
 }
 hipError_t sort_u64(void* tmp, size_t* tmp_bytes, uint64_t* keys_in, uint64_t* keys_out, uint32_t n,

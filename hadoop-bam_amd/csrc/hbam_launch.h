@@ -36,14 +36,18 @@ struct ChainArgs {
 constexpr uint32_t kListCap = 2048;              // >= 65536 / 36 + 2: every reader-mode record start
 constexpr uint64_t kForceEmpty = ~0ull - 1;      // force[]: the block holds no record start
 
-hipError_t launch_bgzf_scan(const uint8_t* file, uint64_t lo, uint64_t hi, uint64_t* cand, uint32_t cap,
-                            uint32_t* count, hipStream_t s);
+// candidates in [lo, hi); file + buf_base is the (aligned) device buffer start
+hipError_t launch_bgzf_scan(const uint8_t* file, uint64_t buf_base, uint64_t lo, uint64_t hi, uint64_t* cand,
+                            uint32_t cap, uint32_t* count, hipStream_t s);
+// partial != 0: bytes past hi are not uploaded yet; a block cut by hi ends
+// the range (verify: flags[2] = 1; walk: out[2..3] = its start, status OK)
 hipError_t launch_bgzf_verify(const uint8_t* file, uint64_t lo, uint64_t hi, const uint64_t* cand, uint32_t n,
-                              BlockInfo* blocks, uint32_t* flags, hipStream_t s);
+                              BlockInfo* blocks, uint32_t* flags, uint32_t partial, hipStream_t s);
 hipError_t launch_bgzf_walk(const uint8_t* file, uint64_t lo, uint64_t hi, BlockInfo* blocks, uint32_t cap,
-                            uint32_t* out, hipStream_t s);
+                            uint32_t* out, uint32_t partial, hipStream_t s);
+// ustart = base + exclusive scan of ISIZE
 hipError_t launch_block_ustart(BlockInfo* blocks, uint32_t n, uint64_t* tmp_isize, uint64_t* tmp_ustart,
-                               void* scan_tmp, size_t* scan_bytes, hipStream_t s);
+                               void* scan_tmp, size_t* scan_bytes, uint64_t base, hipStream_t s);
 hipError_t sort_u64(void* tmp, size_t* tmp_bytes, uint64_t* keys_in, uint64_t* keys_out, uint32_t n,
                     hipStream_t s);
 hipError_t scan_u32_to_u64(void* tmp, size_t* tmp_bytes, const uint32_t* in, uint64_t* out, uint32_t n,

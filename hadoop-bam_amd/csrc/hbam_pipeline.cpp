@@ -25,7 +25,9 @@ Pipeline::Pipeline(int device) : device_(device) {
     return;
   }
   if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&stream_b_, hipStreamNonBlocking) != hipSuccess)
+      hipStreamCreateWithFlags(&stream_b_, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&stream_copy_, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&stream_loc_, hipStreamNonBlocking) != hipSuccess)
     err_ = "hipStreamCreate failed";
   for (auto& e : ev_) (void)hipEventCreate(&e);
   for (auto& e : sync_ev_) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -37,7 +39,10 @@ Pipeline::~Pipeline() {
   for (auto& e : ev_) (void)hipEventDestroy(e);
   for (auto& e : sync_ev_) (void)hipEventDestroy(e);
   for (auto& e : tev_) (void)hipEventDestroy(e);
+  for (auto& e : copy_ev_) (void)hipEventDestroy(e);
   if (stream_b_) (void)hipStreamDestroy(stream_b_);
+  if (stream_copy_) (void)hipStreamDestroy(stream_copy_);
+  if (stream_loc_) (void)hipStreamDestroy(stream_loc_);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -124,74 +129,86 @@ int Pipeline::attach_device(const uint8_t* dptr, uint64_t len, uint64_t base_off
   return kOk;
 }
 
-int Pipeline::locate() {
-  HIPCHK(hipSetDevice(device_));
-  if (timing) HIPCHK(hipEventRecord(ev_[0], stream_));
+int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, uint32_t nprev, uint64_t ubase, hipStream_t s,
+                           uint32_t* nnew, uint64_t* tail) {
+  *nnew = 0;
+  *tail = hi;
   const uint8_t* fbase = dfile_ - base_;  // absolute file coordinates
-  const uint64_t lo = base_, hi = base_ + flen_;
+  const uint64_t len = hi - lo;
   // candidate capacity assumes >= 1 KiB per block on average; denser files
   // (or any chain break) take the serial walk, whose table bound is len/26.
-  const uint32_t cap = (uint32_t)std::min<uint64_t>(flen_ / 1024 + 4096, 0x7fffffffu);
-  const uint32_t walk_cap = (uint32_t)std::min<uint64_t>(flen_ / 26 + 16, 0x7fffffffu);
+  const uint32_t cap = (uint32_t)std::min<uint64_t>(len / 1024 + 4096, 0x7fffffffu);
+  const uint32_t walk_cap = (uint32_t)std::min<uint64_t>(len / 26 + 16, 0x7fffffffu);
   DevBuf<uint64_t>& cand = cand_;
   DevBuf<uint64_t>& sorted = sorted_;
   HIPCHK(cand.reserve(cap));
   HIPCHK(flags_.reserve(4));
   uint32_t init[4] = {0, 0, 0xffffffffu, 0};
-  HIPCHK(hipMemcpyAsync(flags_.p, init, sizeof init, hipMemcpyHostToDevice, stream_));
-  // flags_[0] = candidate count, flags_[1] = chain break, flags_[2] = first big ISIZE
-  HIPCHK(launch_bgzf_scan(fbase, lo, hi, cand.p, cap, flags_.p, stream_));
+  HIPCHK(hipMemcpyAsync(flags_.p, init, sizeof init, hipMemcpyHostToDevice, s));
+  // flags_[0] = candidate count, [1] = chain break, [2] = first big ISIZE, [3] = cut tail
+  HIPCHK(launch_bgzf_scan(fbase, base_, lo, hi, cand.p, cap, flags_.p, s));
   uint32_t count = 0;
-  HIPCHK(hipMemcpyAsync(&count, flags_.p, 4, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
-  bool serial = count > cap || (count == 0 && flen_ > 0);
+  HIPCHK(hipMemcpyAsync(&count, flags_.p, 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  bool serial = count > cap || (count == 0 && len > 0);
   uint32_t n = serial ? 0 : count;
   if (!serial && n > 0) {
-    HIPCHK(dblocks_.reserve(n + 1));
+    HIPCHK(dblocks_.grow(nprev + n + 1));
     HIPCHK(sorted.reserve(n));
     size_t tmp_bytes = 0;
-    HIPCHK(sort_u64(nullptr, &tmp_bytes, cand.p, sorted.p, n, stream_));
+    HIPCHK(sort_u64(nullptr, &tmp_bytes, cand.p, sorted.p, n, s));
     HIPCHK(scan_tmp_.reserve(tmp_bytes + 16));
-    HIPCHK(sort_u64(scan_tmp_.p, &tmp_bytes, cand.p, sorted.p, n, stream_));
-    HIPCHK(launch_bgzf_verify(fbase, lo, hi, sorted.p, n, dblocks_.p, flags_.p + 1, stream_));
-    uint32_t fl[2];
-    HIPCHK(hipMemcpyAsync(fl, flags_.p + 1, 8, hipMemcpyDeviceToHost, stream_));
-    HIPCHK(hipStreamSynchronize(stream_));
+    HIPCHK(sort_u64(scan_tmp_.p, &tmp_bytes, cand.p, sorted.p, n, s));
+    HIPCHK(launch_bgzf_verify(fbase, lo, hi, sorted.p, n, dblocks_.p + nprev, flags_.p + 1, partial ? 1u : 0u, s));
+    uint32_t fl[3];
+    uint64_t last = 0;
+    HIPCHK(hipMemcpyAsync(fl, flags_.p + 1, 12, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&last, sorted.p + n - 1, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
     if (fl[0]) serial = true;
     else if (fl[1] != 0xffffffffu) return fail(kErrFormat, "BGZF block with ISIZE > 65536 (unsupported on device)");
+    else if (fl[2]) {  // the last candidate's block is cut by hi: next range
+      n -= 1;
+      *tail = last;
+    }
   }
   if (serial) {
     uint32_t out[4];
-    HIPCHK(dblocks_.reserve(walk_cap + 1));
-    HIPCHK(hipMemsetAsync(flags_.p, 0, 16, stream_));
-    HIPCHK(launch_bgzf_walk(fbase, lo, hi, dblocks_.p, walk_cap, flags_.p, stream_));
-    HIPCHK(hipMemcpyAsync(out, flags_.p, 16, hipMemcpyDeviceToHost, stream_));
-    HIPCHK(hipStreamSynchronize(stream_));
+    HIPCHK(dblocks_.grow(nprev + walk_cap + 1));
+    HIPCHK(hipMemsetAsync(flags_.p, 0, 16, s));
+    HIPCHK(launch_bgzf_walk(fbase, lo, hi, dblocks_.p + nprev, walk_cap, flags_.p, partial ? 1u : 0u, s));
+    HIPCHK(hipMemcpyAsync(out, flags_.p, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
     n = out[0];
-    if (out[1] != kOk) {
-      uint64_t at = (uint64_t)out[2] | ((uint64_t)out[3] << 32);
-      return fail((int)out[1], "malformed BGZF block at offset " + std::to_string(at));
-    }
+    const uint64_t at = (uint64_t)out[2] | ((uint64_t)out[3] << 32);
+    if (out[1] != kOk) return fail((int)out[1], "malformed BGZF block at offset " + std::to_string(at));
+    if (partial) *tail = at;
   }
-  HIPCHK(dblocks_.reserve(n + 1));
+  HIPCHK(dblocks_.grow(nprev + n + 1));
   DevBuf<uint64_t>& isz = isz_;
   DevBuf<uint64_t>& ust = ust_;
   HIPCHK(isz.reserve(n + 1));
   HIPCHK(ust.reserve(n + 1));
   size_t sb = 0;
-  HIPCHK(launch_block_ustart(dblocks_.p, n, isz.p, ust.p, nullptr, &sb, stream_));
+  HIPCHK(launch_block_ustart(dblocks_.p + nprev, n, isz.p, ust.p, nullptr, &sb, ubase, s));
   HIPCHK(scan_tmp_.reserve(sb + 16));
-  HIPCHK(launch_block_ustart(dblocks_.p, n, isz.p, ust.p, scan_tmp_.p, &sb, stream_));
-  hblocks_.resize(n);
-  if (n) HIPCHK(hipMemcpyAsync(hblocks_.data(), dblocks_.p, n * sizeof(BlockInfo), hipMemcpyDeviceToHost, stream_));
-  if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
-  if (timing) (void)hipEventElapsedTime(&times.locate, ev_[0], ev_[1]);
+  HIPCHK(launch_block_ustart(dblocks_.p + nprev, n, isz.p, ust.p, scan_tmp_.p, &sb, ubase, s));
+  hblocks_.resize(nprev + n);
+  if (n)
+    HIPCHK(hipMemcpyAsync(hblocks_.data() + nprev, dblocks_.p + nprev, n * sizeof(BlockInfo), hipMemcpyDeviceToHost,
+                          s));
+  HIPCHK(hipStreamSynchronize(s));
+  *nnew = n;
+  return kOk;
+}
+
+int Pipeline::finish_blocks() {
+  const uint32_t n = (uint32_t)hblocks_.size();
   total_u_ = n ? hblocks_[n - 1].ustart + hblocks_[n - 1].isize : 0;
-  HIPCHK(du_.reserve(total_u_ + kUPad));
+  HIPCHK(du_.grow(total_u_ + kUPad));
   HIPCHK(hipMemsetAsync(du_.p + total_u_, 0, kUPad, stream_));
-  inflated_.assign(n, 0);
-  HIPCHK(hout_.reserve(n + 1));
+  inflated_.resize(n, 0);
+  HIPCHK(hout_.grow(n + 1));
   // dead positions: [htsjdk] an empty block right after an exhausted one
   std::vector<uint64_t> dead;
   for (uint32_t k = 1; k < n; ++k)
@@ -204,7 +221,103 @@ int Pipeline::locate() {
   return kOk;
 }
 
-int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force) {
+int Pipeline::locate() {
+  HIPCHK(hipSetDevice(device_));
+  if (timing) HIPCHK(hipEventRecord(ev_[0], stream_));
+  hblocks_.clear();
+  inflated_.clear();
+  uint32_t n = 0;
+  uint64_t tail = 0;
+  int rc = locate_range(base_, base_ + flen_, false, 0, 0, stream_, &n, &tail);
+  if (rc != kOk) return rc;
+  if (timing) {
+    HIPCHK(hipEventRecord(ev_[1], stream_));
+    HIPCHK(hipEventSynchronize(ev_[1]));
+    (void)hipEventElapsedTime(&times.locate, ev_[0], ev_[1]);
+  }
+  return finish_blocks();
+}
+
+int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, uint64_t first_pos, SpanDev* out,
+                           float* ms) {
+  *ms = 0;
+  *out = SpanDev();
+  if (!dfile_ || !own_file_ || len != flen_) return fail(kErrState, "run_streamed needs a loaded file of the same size");
+  HIPCHK(hipSetDevice(device_));
+  piece = std::max<uint64_t>(piece, 1ull << 20);
+  const uint64_t np = std::max<uint64_t>(1, (len + piece - 1) / piece);
+  while (copy_ev_.size() < np) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    copy_ev_.push_back(e);
+  }
+  // capacity up front, so that nothing reallocates under queued work (grow()
+  // still handles a file that outruns the estimates, at the cost of a wait)
+  HIPCHK(dblocks_.grow(len / 16384 + 4096));
+  HIPCHK(hout_.grow(len / 16384 + 4096));
+  HIPCHK(du_.grow(std::max<uint64_t>(total_u_, 4 * len) + kUPad));
+  const uint64_t chunk_u = std::min<uint64_t>(8 * piece, (uint64_t)kInflateChunkBlocks * 65536);
+  for (int i = 0; i < 2; ++i) HIPCHK(tokens_[i].reserve(chunk_u + 16));
+  HIPCHK(tables_.reserve((uint64_t)kInflateChunkBlocks * kHuffTableImage));
+  HIPCHK(tinfo_.reserve(kInflateChunkBlocks));
+  HIPCHK(hipDeviceSynchronize());
+
+  HIPCHK(hipEventRecord(ev_[6], stream_copy_));
+  for (uint64_t k = 0; k < np; ++k) {
+    const uint64_t o = k * piece, sz = std::min(piece, len - o);
+    HIPCHK(hipMemcpyAsync(dfile_ + o, data + o, sz, hipMemcpyHostToDevice, stream_copy_));
+    HIPCHK(hipEventRecord(copy_ev_[k], stream_copy_));
+  }
+  hblocks_.clear();
+  inflated_.clear();
+  total_u_ = 0;
+  uint64_t lo = base_;
+  uint32_t nb = 0;
+  for (uint64_t k = 0; k < np; ++k) {
+    HIPCHK(hipEventSynchronize(copy_ev_[k]));
+    const bool last = k + 1 == np;
+    const uint64_t hi = base_ + (last ? len : (k + 1) * piece);
+    uint32_t nnew = 0;
+    uint64_t tail = hi;
+    int rc = locate_range(lo, hi, !last, nb, total_u_, stream_loc_, &nnew, &tail);
+    if (rc != kOk) return rc;
+    if (nnew) {
+      const BlockInfo& e = hblocks_[nb + nnew - 1];
+      total_u_ = e.ustart + e.isize;
+      HIPCHK(du_.grow(total_u_ + kUPad));
+      HIPCHK(hout_.grow(nb + nnew + 1));
+      inflated_.resize(nb + nnew, 0);
+      rc = inflate(nb, nb + nnew, true, false);
+      if (rc != kOk) return rc;
+      nb += nnew;
+    }
+    lo = tail;
+  }
+  int rc = finish_blocks();  // waits for the queued inflates (stream_)
+  if (rc != kOk) return rc;
+  HIPCHK(flags_.reserve(4));
+  const uint32_t none = 0xffffffffu;
+  uint32_t first = none;
+  HIPCHK(hipMemcpyAsync(flags_.p + 3, &none, 4, hipMemcpyHostToDevice, stream_));
+  HIPCHK(launch_first_error_hout(hout_.p, 0, nb, flags_.p + 3, stream_));
+  HIPCHK(hipMemcpyAsync(&first, flags_.p + 3, 4, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  if (first != none) {
+    HuffOut ho;
+    HIPCHK(hipMemcpy(&ho, hout_.p + first, sizeof ho, hipMemcpyDeviceToHost));
+    std::fill(inflated_.begin(), inflated_.end(), 0);
+    const char* what = ho.status == kErrFormat ? "Did not inflate expected amount" : "invalid DEFLATE data";
+    return fail(ho.status, std::string(what) + " in BGZF block at offset " + std::to_string(hblocks_[first].coff));
+  }
+  rc = decode_span(voff_of(first_pos), ~0ull, kReader, true, out);
+  if (rc != kOk) return rc;
+  HIPCHK(hipEventRecord(ev_[7], stream_));
+  HIPCHK(hipEventSynchronize(ev_[7]));
+  HIPCHK(hipEventElapsedTime(ms, ev_[6], ev_[7]));
+  return kOk;
+}
+
+int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
   HIPCHK(hipSetDevice(device_));
   const uint32_t nblk = (uint32_t)hblocks_.size();
   b1 = std::min(b1, nblk);
@@ -348,6 +461,7 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force) {
     times.inflate = times.huff = times.lz77 = 0;
     return kOk;
   }
+  if (!check) return kOk;  // the caller checks hout_ once all blocks are queued
   HIPCHK(flags_.reserve(4));
   const uint32_t none = 0xffffffffu;
   HIPCHK(hipMemcpyAsync(flags_.p + 3, &none, 4, hipMemcpyHostToDevice, stream_));

@@ -26,9 +26,27 @@ struct DevBuf {
     p = nullptr;
     n = 0;
   }
+  // grow, keeping the contents (waits for the whole device first: the old
+  // buffer may be in use on any stream)
+  hipError_t grow(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    const size_t c = count > 2 * n ? count : 2 * n;
+    T* q = nullptr;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&q), c * sizeof(T));
+    if (e != hipSuccess) return e;
+    if (p) {
+      if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+      if ((e = hipMemcpy(q, p, n * sizeof(T), hipMemcpyDeviceToDevice)) != hipSuccess) return e;
+      (void)hipFree(p);
+    }
+    p = q;
+    n = c;
+    return hipSuccess;
+  }
   // grow-only (contents not preserved)
   hipError_t reserve(size_t count) {
     if (count <= n && p) return hipSuccess;
+    if (p) (void)hipDeviceSynchronize();  // queued work on any stream may still use it
     release();
     size_t c = count ? count : 1;
     hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), c * sizeof(T));
@@ -83,8 +101,18 @@ class Pipeline {
   uint64_t total_u() const { return total_u_; }
   const BlockInfo* d_blocks() const { return dblocks_.p; }
 
-  // Inflate blocks [b0, b1) into the contiguous inflated stream.
-  int inflate(uint32_t b0, uint32_t b1, bool force = false);
+  // Inflate blocks [b0, b1) into the contiguous inflated stream.  check =
+  // false leaves the work queued (no DEFLATE error check, no host wait).
+  int inflate(uint32_t b0, uint32_t b1, bool force = false, bool check = true);
+
+  // End-to-end pass from host memory: the file (same length as the loaded
+  // one) is copied to HBM in pieces on a copy stream while the BGZF blocks of
+  // every piece that has landed are located and inflated, then the record
+  // chain + decode run over the whole file (first record at stream position
+  // first_pos).  data should be page-locked for the copies to overlap.
+  // *ms = first copy to last decode (HIP events).
+  int run_streamed(const uint8_t* data, uint64_t len, uint64_t piece_bytes, uint64_t first_pos, SpanDev* out,
+                   float* ms);
   const uint8_t* d_u() const { return du_.p; }
 
   // Record chain over the span [vstart, vend) under reader or indexer rules;
@@ -125,6 +153,12 @@ class Pipeline {
 
  private:
   int fail(int code, const std::string& msg);
+  // BGZF blocks of [lo, hi) appended at index nprev with ustart from ubase,
+  // on stream s (synchronized).  partial: a block cut by hi is left out and
+  // *tail = its start (hi when none).
+  int locate_range(uint64_t lo, uint64_t hi, bool partial, uint32_t nprev, uint64_t ubase, hipStream_t s,
+                   uint32_t* nnew, uint64_t* tail);
+  int finish_blocks();  // total_u_, dead positions, pads, per-block state after locate
   // SoA store for n records (voff = rec_voff_) + the deferred long-key list
   int alloc_columns(uint64_t n, uint64_t stream_bytes, Columns* c);
   int hip_check(hipError_t e, const char* what);
@@ -132,6 +166,9 @@ class Pipeline {
   int device_ = 0;
   hipStream_t stream_ = nullptr;
   hipStream_t stream_b_ = nullptr;  // inflate phase B (overlaps phase A of the next chunk)
+  hipStream_t stream_copy_ = nullptr;  // run_streamed: host->HBM pieces
+  hipStream_t stream_loc_ = nullptr;   // run_streamed: per-piece block discovery
+  std::vector<hipEvent_t> copy_ev_;
   std::string err_;
 
   uint8_t* dfile_ = nullptr;

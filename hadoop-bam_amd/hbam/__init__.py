@@ -94,6 +94,9 @@ _sig("hbam_open_codec", C.c_int, [C.POINTER(Opts), C.POINTER(P)])
 _sig("hbam_gpu_encode_writables", C.c_int, [P, i32, C.POINTER(C.c_float), C.POINTER(u64)])
 _sig("hbam_gpu_fetch_encoded", C.c_int, [P, u64, u64, P])
 _sig("hbam_gpu_reload", C.c_int, [P, P, u64, i32, C.POINTER(C.c_float)])
+_sig("hbam_gpu_run_streamed", C.c_int, [P, P, u64, u64, C.POINTER(GpuStats)])
+_sig("hbam_host_alloc", P, [u64])
+_sig("hbam_host_free", None, [P])
 _sig("hbam_gpu_d2d_bandwidth", C.c_int, [P, u64, i32, C.POINTER(C.c_float)])
 
 
@@ -148,6 +151,29 @@ def _decode_writables(h, buf, offs, raise_on_error):
     if rc != OK and (raise_on_error or rc not in (E_FORMAT, E_TRUNC, E_ARG)):
         raise HbamError(rc, _L.hbam_last_error(h).decode(errors="replace"))
     return _batch_dict(b, rc)
+
+
+class PinnedBuffer:
+    """Page-locked host memory from hbam_host_alloc, as a numpy uint8 view."""
+
+    def __init__(self, nbytes):
+        self.ptr = _L.hbam_host_alloc(nbytes)
+        if not self.ptr:
+            raise HbamError(E_NOMEM, "hbam_host_alloc failed")
+        self.nbytes = nbytes
+        self.array = np.ctypeslib.as_array((C.c_uint8 * max(nbytes, 1)).from_address(self.ptr))[:nbytes]
+
+    def close(self):
+        if self.ptr:
+            self.array = None
+            _L.hbam_host_free(self.ptr)
+            self.ptr = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
 
 class Codec:
@@ -362,6 +388,15 @@ class Gpu:
     def run(self, timing=False, decode=True):
         st = GpuStats()
         rc = _L.hbam_gpu_run(self._h, (1 if timing else 0) | (0 if decode else 2), C.byref(st))
+        if rc != OK:
+            raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
+        return {f: getattr(st, f) for f, _ in GpuStats._fields_}
+
+    def run_streamed(self, ptr, nbytes, piece_bytes=64 << 20):
+        """hbam_gpu_run_streamed: copy the file from host memory at `ptr` in
+        pieces while inflating the pieces already in HBM, then chain + decode."""
+        st = GpuStats()
+        rc = _L.hbam_gpu_run_streamed(self._h, ptr, nbytes, piece_bytes, C.byref(st))
         if rc != OK:
             raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
         return {f: getattr(st, f) for f, _ in GpuStats._fields_}

@@ -190,6 +190,17 @@ int hbam_gpu_load(hbam_gpu *g, const void *data, uint64_t len, uint64_t base_off
  * record scan, field decode + keys + voffs (flags bit0: also timing per stage,
  * bit1: skip decode). */
 int hbam_gpu_run(hbam_gpu *g, int32_t flags, hbam_gpu_stats *stats);
+/* End-to-end pass from host memory: the file (same bytes/length as the
+ * loaded one) is copied host->HBM in pieces of piece_bytes on a copy stream
+ * while the BGZF blocks of every landed piece are located and inflated on
+ * the compute streams; then the record chain + decode (as hbam_gpu_run).
+ * st->ms_total = first copy to last decode.  data should come from
+ * hbam_host_alloc (page-locked) for the copies to overlap the kernels. */
+int hbam_gpu_run_streamed(hbam_gpu *g, const void *data, uint64_t len, uint64_t piece_bytes, hbam_gpu_stats *st);
+/* Page-locked host memory (what a JNI caller would wrap as a direct
+ * ByteBuffer for the copy engine); NULL on failure. */
+void *hbam_host_alloc(uint64_t bytes);
+void hbam_host_free(void *p);
 /* Copy the loaded file's bytes (same length) from host memory into HBM again,
  * timed (*ms, HIP events): the host->device leg of a PCIe-inclusive rate.
  * pinned != 0 copies from a page-locked staging copy (made untimed). */
