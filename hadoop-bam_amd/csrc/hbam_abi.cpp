@@ -291,6 +291,16 @@ int hbam_guess_record_starts(hbam_ctx* ctx, const uint64_t* begs, const uint64_t
   return HBAM_OK;
 }
 
+int hbam_guess_bgzf_block_starts(hbam_ctx* ctx, const uint64_t* begs, const uint64_t* ends, uint64_t n,
+                                 uint64_t* out) {
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  std::vector<uint64_t> b(begs, begs + n), e(ends, ends + n), r;
+  int rc = hadoop_bam::guess_bgzf_batch(*ctx->f, b, e, &r, &ctx->err);
+  if (rc != HBAM_OK) return rc;
+  if (n) memcpy(out, r.data(), n * 8);
+  return HBAM_OK;
+}
+
 int hbam_get_splits(hbam_ctx* ctx, const uint64_t* starts, const uint64_t* lengths, uint64_t n, const uint8_t* sbi,
                     uint64_t sbi_len, uint64_t* vstarts, uint64_t* vends, uint64_t* nout) {
   *nout = 0;

@@ -369,6 +369,69 @@ __global__ void k_guess_splits(GuessEnv E, const uint64_t* __restrict__ begs, co
   }
 }
 
+// util/BGZFSplitGuesser.java:64-167 (guessNextBGZFBlockStart): its own
+// guessNextBGZFPos over arr = file[beg, beg + min(end-beg, 2*0xffff-1)),
+// candidates below firstBGZFEnd = min(end-beg, 0xffff); the first candidate
+// whose block reads whole from arr and inflates with a good CRC wins.
+// in.read past the array end keeps the stale bytes of buf
+// (ByteArraySeekableStream), restated with a per-lane 4-byte buffer.
+constexpr uint64_t kBgzfGuessWindow = 2 * 0xffff - 1;  // :74
+
+__global__ void k_guess_bgzf_starts(GuessEnv E, const uint64_t* __restrict__ begs, const uint64_t* __restrict__ ends,
+                                    uint32_t n, uint64_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t beg = begs[i], end = ends[i];
+  uint64_t alen = min(end - beg, kBgzfGuessWindow);
+  if (beg + alen > E.flen) alen = E.flen > beg ? E.flen - beg : 0;
+  const uint8_t* a = E.file + beg;
+  const int32_t firstEnd = (int32_t)min(end - beg, (uint64_t)0xffff);
+  uint8_t buf[4] = {0, 0, 0, 0};
+  for (int32_t pos = 0;;) {
+    int32_t p = pos, got = -1;
+    for (;;) {  // guessNextBGZFPos (:114-166)
+      bool stop = false;
+      for (;;) {
+        for (int k = 0; k < 4; ++k) {  // in.seek(p); in.read(buf, 0, 4)
+          if (p >= 0 && (uint64_t)p + k < alen) buf[k] = a[p + k];
+          else if (k == 0 && (uint64_t)p >= alen) break;
+        }
+        const uint32_t nn = g_rd32(buf);
+        if (nn == 0x04088b1fu) break;
+        if ((nn >> 8) == (0x04088b1fu & 0xffffffu)) ++p;
+        else if ((nn >> 16) == (0x04088b1fu & 0xffffu)) p += 2;
+        else p += 3;
+        if (p >= firstEnd) { stop = true; break; }
+      }
+      if (stop) break;
+      const int32_t p0 = p;
+      p += 12;
+      if ((uint64_t)p0 + 12 > alen) break;
+      const int32_t xlen = (int32_t)g_rd16(a + p0 + 10), subEnd = p + xlen;
+      while (p < subEnd) {
+        if ((uint64_t)p + 4 > alen) break;
+        if (g_rd32(a + p) != 0x00024342u) { p += 4 + (int32_t)g_rd16(a + p + 2); continue; }
+        got = p0;
+        break;
+      }
+      if (got >= 0) break;
+      p = p0 + 4;
+    }
+    if (got < 0) { out[i] = end; return; }
+    pos = got;
+    // bgzf.seek(pos << 16): a real block read whole from arr, inflating with a good CRC
+    const int64_t kb = find_block(E, beg + (uint64_t)pos);
+    if (kb >= 0) {
+      const BlockInfo b = E.blocks[kb];
+      if (b.coff + b.csize <= beg + alen && E.valid[kb] && (b.isize > 0 || b.crc == 0)) {
+        out[i] = beg + (uint64_t)pos;
+        return;
+      }
+    }
+    ++pos;
+  }
+}
+
 }  // namespace hbam
 
 // ---------------------------------------------------------------------------
@@ -456,6 +519,79 @@ int guess_batch(BamFile& f, const std::vector<uint64_t>& begs, const std::vector
   if (!chk(hipMemcpyAsync(res.data(), dout.p, m * 8, hipMemcpyDeviceToHost, s)) || !chk(hipStreamSynchronize(s)))
     return kErrDevice;
   for (uint32_t j = 0; j < m; ++j) (*out)[dev_slot[j]] = res[j];
+  return kOk;
+}
+
+int guess_bgzf_batch(BamFile& f, const std::vector<uint64_t>& begs, const std::vector<uint64_t>& ends,
+                     std::vector<uint64_t>* out, std::string* err) {
+  using namespace hbam;
+  Pipeline& p = f.pipe();
+  const size_t n = begs.size();
+  out->assign(n, 0);
+  if (n == 0) return kOk;
+  const auto& blk = p.blocks();
+  const uint32_t nblk = (uint32_t)blk.size();
+  for (size_t i = 0; i < n; ++i)
+    if (ends[i] < begs[i]) {
+      *err = "split end before its start";
+      return kErrArg;
+    }
+  // blocks a window can accept: coff in [beg, beg + firstBGZFEnd)
+  std::vector<uint8_t> need(nblk, 0);
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t lim = begs[i] + std::min<uint64_t>(ends[i] - begs[i], 0xffff);
+    auto it = std::lower_bound(blk.begin(), blk.end(), begs[i], [](const BlockInfo& b, uint64_t c) { return b.coff < c; });
+    for (; it != blk.end() && it->coff < lim; ++it) need[it - blk.begin()] = 1;
+  }
+  std::vector<uint8_t> valid(nblk, 0);
+  std::vector<uint32_t> dev_idx;
+  for (uint32_t k = 0; k < nblk;) {
+    if (!need[k]) { ++k; continue; }
+    uint32_t e = k;
+    while (e < nblk && need[e]) ++e;
+    if (p.inflate(k, e) == kOk) {
+      for (uint32_t j = k; j < e; ++j) valid[j] = 1;
+    } else {  // a bad block fails the range: per block, as a failed seek would
+      for (uint32_t j = k; j < e; ++j) valid[j] = p.inflate(j, j + 1) == kOk;
+    }
+    for (uint32_t j = k; j < e; ++j)
+      if (valid[j] && blk[j].isize > 0) dev_idx.push_back(j);
+    k = e;
+  }
+  DevBuf<uint8_t> dvalid;
+  DevBuf<uint32_t> dlist;
+  DevBuf<uint64_t> dbeg, dend, dout;
+  hipStream_t s = p.stream();
+  auto chk = [&](hipError_t e) {
+    if (e != hipSuccess) *err = std::string("HIP: ") + hipGetErrorString(e);
+    return e == hipSuccess;
+  };
+  if (!chk(dvalid.reserve(nblk + 1)) || !chk(dlist.reserve(dev_idx.size() + 1)) || !chk(dbeg.reserve(n)) ||
+      !chk(dend.reserve(n)) || !chk(dout.reserve(n)))
+    return kErrDevice;
+  if (!chk(hipMemcpyAsync(dvalid.p, valid.data(), nblk, hipMemcpyHostToDevice, s))) return kErrDevice;
+  if (!dev_idx.empty()) {  // setCheckCrcs(true) (:89)
+    if (!chk(hipMemcpyAsync(dlist.p, dev_idx.data(), dev_idx.size() * 4, hipMemcpyHostToDevice, s))) return kErrDevice;
+    hipLaunchKernelGGL(k_block_crc, dim3((uint32_t)dev_idx.size()), dim3(256), 0, s, p.d_blocks(), dlist.p,
+                       (uint32_t)dev_idx.size(), p.d_u(), dvalid.p);
+    if (!chk(hipGetLastError())) return kErrDevice;
+  }
+  if (!chk(hipMemcpyAsync(dbeg.p, begs.data(), n * 8, hipMemcpyHostToDevice, s)) ||
+      !chk(hipMemcpyAsync(dend.p, ends.data(), n * 8, hipMemcpyHostToDevice, s)))
+    return kErrDevice;
+  GuessEnv E;
+  E.file = p.d_file();
+  E.flen = f.file_size();
+  E.blocks = p.d_blocks();
+  E.nblk = nblk;
+  E.u = p.d_u();
+  E.valid = dvalid.p;
+  E.n_ref = f.n_ref();
+  hipLaunchKernelGGL(k_guess_bgzf_starts, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s, E, dbeg.p, dend.p,
+                     (uint32_t)n, dout.p);
+  if (!chk(hipGetLastError())) return kErrDevice;
+  if (!chk(hipMemcpyAsync(out->data(), dout.p, n * 8, hipMemcpyDeviceToHost, s)) || !chk(hipStreamSynchronize(s)))
+    return kErrDevice;
   return kOk;
 }
 

@@ -128,6 +128,12 @@ class BAMSplitGuesser {
   BamFile& f_;
 };
 
+// util/BGZFSplitGuesser.guessNextBGZFBlockStart(beg, end) (:64-112) for many
+// split points at once (VCF/BCF BGZF inputs; BCFSplitGuesser shares the block
+// search); end when nothing is found.
+int guess_bgzf_batch(BamFile& f, const std::vector<uint64_t>& begs, const std::vector<uint64_t>& ends,
+                     std::vector<uint64_t>* out, std::string* err);
+
 // BAMInputFormat split planning (BAMInputFormat.java:222-318, 469-530).
 class BAMInputFormat {
  public:

@@ -75,6 +75,7 @@ _sig("hbam_ref", C.c_int, [P, i32, C.POINTER(C.c_char_p), C.POINTER(i32)])
 _sig("hbam_decode_span", C.c_int, [P, u64, u64, C.POINTER(Batch)])
 _sig("hbam_build_splitting_index", C.c_int, [P, i32, C.POINTER(P), C.POINTER(u64)])
 _sig("hbam_guess_record_starts", C.c_int, [P, P, P, u64, P])
+_sig("hbam_guess_bgzf_block_starts", C.c_int, [P, P, P, u64, P])
 _sig("hbam_get_splits", C.c_int, [P, P, P, u64, P, u64, P, P, C.POINTER(u64)])
 _sig("hbam_blocks", C.c_int, [P, P, P, P, P, u64, C.POINTER(u64)])
 _sig("hbam_read_inflated", C.c_int, [P, u64, u64, P])
@@ -311,6 +312,17 @@ class BamFile:
         e = np.ascontiguousarray(ends, np.uint64)
         out = np.zeros(max(n, 1), np.uint64)
         rc = _L.hbam_guess_record_starts(self._h, b.ctypes.data, e.ctypes.data, n, out.ctypes.data)
+        if rc != OK:
+            raise self._err(rc)
+        return [int(x) for x in out[:n]]
+
+    def guess_bgzf_block_starts(self, begs, ends):
+        """BGZFSplitGuesser.guessNextBGZFBlockStart for many split points."""
+        n = len(begs)
+        b = np.ascontiguousarray(begs, np.uint64)
+        e = np.ascontiguousarray(ends, np.uint64)
+        out = np.zeros(max(n, 1), np.uint64)
+        rc = _L.hbam_guess_bgzf_block_starts(self._h, b.ctypes.data, e.ctypes.data, n, out.ctypes.data)
         if rc != OK:
             raise self._err(rc)
         return [int(x) for x in out[:n]]

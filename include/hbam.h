@@ -118,6 +118,15 @@ int hbam_build_splitting_index(hbam_ctx *ctx, int32_t granularity, uint8_t **buf
 int hbam_guess_record_starts(hbam_ctx *ctx, const uint64_t *begs, const uint64_t *ends, uint64_t n,
                              uint64_t *out);
 
+/* util/BGZFSplitGuesser.guessNextBGZFBlockStart(beg, end)
+ * (util/BGZFSplitGuesser.java:64-112) for n split points at once: the first
+ * BGZF block start in [beg, beg + min(end-beg, 0xffff)) whose block lies in
+ * the guesser's 2*0xffff-1 byte window and inflates with a good CRC;
+ * out[i] == ends[i] when none.  The split search of the BGZF text formats
+ * (VCFInputFormat / BCFSplitGuesser); works on a ctx from hbam_open_bgzf. */
+int hbam_guess_bgzf_block_starts(hbam_ctx *ctx, const uint64_t *begs, const uint64_t *ends, uint64_t n,
+                                 uint64_t *out);
+
 /* BAMInputFormat.getSplits for the FileSplits of one file
  * (BAMInputFormat.java:222-318 addIndexedSplits, 469-530 addProbabilisticSplits).
  * sbi = .splitting-bai bytes or NULL.  vstarts/vends need room for n entries. */
