@@ -1058,6 +1058,14 @@ constexpr uint32_t kHuffLdsBytes = (sizeof(HuffLds) + 15) & ~15u;
 constexpr uint32_t kHuffCtlBytes = (sizeof(HuffCtl) + 15) & ~15u;
 constexpr uint32_t kHuffStaticBytes = kHuffLdsBytes + kHuffCtlBytes;
 
+// Per-block cycle profiles (HBAM_HUFF_PROF=1 at run time) are compiled in only
+// with -DHBAM_KPROF=1: their accumulators would otherwise stay live (22 VGPRs
+// in phase A) for the whole kernel.
+#ifndef HBAM_KPROF
+#define HBAM_KPROF 0
+#endif
+constexpr bool kProf = HBAM_KPROF != 0;
+
 #ifndef HBAM_HUFF_WPE
 #define HBAM_HUFF_WPE 5  // waves per SIMD (VGPR cap 96; measured best on C2)
 #endif
@@ -1075,6 +1083,7 @@ __global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(co
   // exchange) [3] sync [4] end scan [5] emit [6] result hand-back
   // [7] of [1]: dynamic litlen/dist table builds + literal pairing
   // [8] all-lane passes [9] sync iterations [10] total
+  if (!kProf) prof = nullptr;
   uint64_t pacc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t pt = prof ? clock64() : 0, pt0 = pt;
 #define PROF_T(i)                           \
@@ -1101,15 +1110,33 @@ __global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(co
   const uint64_t abase = sbyte & ~15ull;
   const HuffTableInfo ti = tinfo[blockIdx.x];
   {  // stage the block (+16 B of zero-padded file) and its prebuilt tables in LDS
-    if (STAGE) {
-      const uint32_t nq = (uint32_t)((blk.coff + blk.csize - abase + 15) >> 4) + 1;
-      const uint4* __restrict__ src = reinterpret_cast<const uint4*>(file + abase);
-      for (uint32_t i = tid; i < nq; i += kHuffThreads) s_in[i] = src[i];
-    }
-    if (ti.status == 0) {
-      const uint4* __restrict__ tsrc = reinterpret_cast<const uint4*>(tables + (uint64_t)blockIdx.x * kTableImage);
-      uint4* tdst = reinterpret_cast<uint4*>(&L);
-      for (uint32_t i = tid; i < kTableImage / 16; i += kHuffThreads) tdst[i] = tsrc[i];
+    // One index space over both copies ([0, nq): block, [nq, nq + nt): table
+    // image), kStageBatch 16 B loads in flight per thread before their LDS
+    // stores: the copy costs about one memory latency instead of one per
+    // loop trip.
+    const uint32_t nq = STAGE ? (uint32_t)((blk.coff + blk.csize - abase + 15) >> 4) + 1 : 0u;
+    const uint32_t nt = ti.status == 0 ? kTableImage / 16 : 0u;
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(file + abase);
+    const uint4* __restrict__ tsrc = reinterpret_cast<const uint4*>(tables + (uint64_t)blockIdx.x * kTableImage);
+    uint4* tdst = reinterpret_cast<uint4*>(&L);
+#ifndef HBAM_STAGE_BATCH
+#define HBAM_STAGE_BATCH 4
+#endif
+    constexpr int kStageBatch = HBAM_STAGE_BATCH;
+    for (uint32_t i0 = tid; i0 < nq + nt; i0 += kStageBatch * kHuffThreads) {
+      uint4 v[kStageBatch];
+#pragma unroll
+      for (int k = 0; k < kStageBatch; ++k) {
+        const uint32_t i = i0 + k * kHuffThreads;
+        if (i < nq) v[k] = src[i];
+        else if (i < nq + nt) v[k] = tsrc[i - nq];
+      }
+#pragma unroll
+      for (int k = 0; k < kStageBatch; ++k) {
+        const uint32_t i = i0 + k * kHuffThreads;
+        if (i < nq) s_in[i] = v[k];
+        else if (i < nq + nt) tdst[i - nq] = v[k];
+      }
     }
   }
   __syncthreads();
@@ -1497,6 +1524,7 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
   // optional cycle profile (thread 0): [6] token loads [0] block scan
   // [1] map fill (wave 0's own work) [2] fill barrier wait [3] resolve
   // [4] store [5] total
+  if (!kProf) prof = nullptr;
   uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t pt = prof ? clock64() : 0, pt0 = pt;
 #define LZ_T(i)                             \
