@@ -2811,12 +2811,16 @@ uint64_t* g_huff_prof = nullptr;
 uint64_t* g_lz_prof = nullptr;  // HBAM_HUFF_PROF: phase-B per-block cycle profile (8 u64 per block)  // HBAM_HUFF_PROF: per-block cycle profile (hbam_pipeline.cpp)
 
 // max_stage = largest staged span of the chunk's blocks (huff_stage_bytes)
-static hipError_t launch_huff(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                              uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
+hipError_t launch_huff_tables(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
                               uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s) {
+  if (nb == 0) return hipSuccess;
   hipLaunchKernelGGL(k_huff_tables, dim3(nb), dim3(64), 0, s, file, blocks, b0, tables, tinfo);
-  hipError_t e0 = hipGetLastError();
-  if (e0 != hipSuccess) return e0;
+  return hipGetLastError();
+}
+// phase A proper; the chunk's tables must be built (launch_huff_tables)
+static hipError_t launch_huff_only(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
+                                   uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
+                                   const uint8_t* tables, const HuffTableInfo* tinfo, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_inflate_huff<true>),
@@ -2833,6 +2837,19 @@ static hipError_t launch_huff(const uint8_t* file, const BlockInfo* blocks, uint
     hipLaunchKernelGGL(k_inflate_huff<false>, dim3(nb), dim3(kHuffThreads), kHuffStaticBytes, s, file, blocks, b0,
                        chunk_ustart, tokens, hout, tables, tinfo, g_huff_prof);
   return hipGetLastError();
+}
+static hipError_t launch_huff(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
+                              uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
+                              uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s) {
+  hipError_t e = launch_huff_tables(file, blocks, b0, nb, tables, tinfo, s);
+  if (e != hipSuccess) return e;
+  return launch_huff_only(file, blocks, b0, nb, chunk_ustart, tokens, hout, max_stage, tables, tinfo, s);
+}
+hipError_t launch_inflate_huff_prebuilt(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
+                                        uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
+                                        const uint8_t* tables, const HuffTableInfo* tinfo, hipStream_t s) {
+  if (nb == 0) return hipSuccess;
+  return launch_huff_only(file, blocks, b0, nb, chunk_ustart, tokens, hout, max_stage, tables, tinfo, s);
 }
 hipError_t launch_inflate(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
                           uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint8_t* u, uint32_t max_stage,

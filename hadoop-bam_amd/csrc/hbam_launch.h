@@ -58,6 +58,13 @@ hipError_t launch_inflate(const uint8_t* file, const BlockInfo* blocks, uint32_t
 hipError_t launch_inflate_huff(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
                                uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
                                uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s);
+// phase A split in two: the first DEFLATE block's header + tables of every
+// block of a chunk (k_huff_tables), then the decode reading them
+hipError_t launch_huff_tables(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
+                              uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s);
+hipError_t launch_inflate_huff_prebuilt(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
+                                        uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
+                                        const uint8_t* tables, const HuffTableInfo* tinfo, hipStream_t s);
 // HBAM_HUFF_PROF profile buffer (16 u64 per block) or nullptr
 extern uint64_t* g_huff_prof;
 extern uint64_t* g_lz_prof;

@@ -27,10 +27,13 @@ Pipeline::Pipeline(int device) : device_(device) {
   if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&stream_b_, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&stream_copy_, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&stream_loc_, hipStreamNonBlocking) != hipSuccess)
+      hipStreamCreateWithFlags(&stream_loc_, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&stream_t_, hipStreamNonBlocking) != hipSuccess)
     err_ = "hipStreamCreate failed";
   for (auto& e : ev_) (void)hipEventCreate(&e);
   for (auto& e : sync_ev_) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  for (auto& e : tab_ev_) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  for (auto& e : hdone_ev_) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
 }
 
 Pipeline::~Pipeline() {
@@ -43,6 +46,9 @@ Pipeline::~Pipeline() {
   if (stream_b_) (void)hipStreamDestroy(stream_b_);
   if (stream_copy_) (void)hipStreamDestroy(stream_copy_);
   if (stream_loc_) (void)hipStreamDestroy(stream_loc_);
+  if (stream_t_) (void)hipStreamDestroy(stream_t_);
+  for (auto& e : tab_ev_) (void)hipEventDestroy(e);
+  for (auto& e : hdone_ev_) (void)hipEventDestroy(e);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -258,8 +264,10 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
   HIPCHK(du_.grow(std::max<uint64_t>(total_u_, 4 * len) + kUPad));
   const uint64_t chunk_u = std::min<uint64_t>(8 * piece, (uint64_t)kInflateChunkBlocks * 65536);
   for (int i = 0; i < 2; ++i) HIPCHK(tokens_[i].reserve(chunk_u + 16));
-  HIPCHK(tables_.reserve((uint64_t)kInflateChunkBlocks * kHuffTableImage));
-  HIPCHK(tinfo_.reserve(kInflateChunkBlocks));
+  for (int i = 0; i < 2; ++i) {
+    HIPCHK(tables_[i].reserve((uint64_t)kInflateChunkBlocks * kHuffTableImage));
+    HIPCHK(tinfo_[i].reserve(kInflateChunkBlocks));
+  }
   HIPCHK(hipDeviceSynchronize());
 
   HIPCHK(hipEventRecord(ev_[6], stream_copy_));
@@ -374,13 +382,16 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
   }
   if (any) {
     for (int i = 0; i < (nc > 1 ? 2 : 1); ++i) HIPCHK(tokens_[i].reserve(max_u + 16));  // phase B reads tokens as uint4
-    HIPCHK(tables_.reserve(max_nb * kHuffTableImage));
-    HIPCHK(tinfo_.reserve(max_nb));
+    for (int i = 0; i < (nc > 1 ? 2 : 1); ++i) {
+      HIPCHK(tables_[i].reserve(max_nb * kHuffTableImage));
+      HIPCHK(tinfo_[i].reserve(max_nb));
+    }
   }
   hipStream_t sb = serial ? stream_ : stream_b_;
-  if (!serial && any) {  // phase B must see everything queued on stream_ before this call
+  if (!serial && any) {  // phase B and the table builds see everything queued on stream_ before this call
     HIPCHK(hipEventRecord(sync_ev_[0], stream_));
     HIPCHK(hipStreamWaitEvent(sb, sync_ev_[0], 0));
+    HIPCHK(hipStreamWaitEvent(stream_t_, sync_ev_[0], 0));
   }
   for (size_t j = 0; j < nc; ++j) {
     const uint32_t cb = chunks[j].b, ce = chunks[j].e;
@@ -390,8 +401,18 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
     for (uint32_t k = cb; k < ce; ++k) max_stage = std::max(max_stage, huff_stage_bytes(hblocks_[k]));
     if (!serial && j >= 2) HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + par], 0));  // B(j-2) released the buffer
     if (timing) HIPCHK(hipEventRecord(tev_[3 * j], stream_));
-    HIPCHK(launch_inflate_huff(fbase, dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, max_stage, tables_.p,
-                               tinfo_.p, stream_));
+    // tables of chunk j on stream_t_ (they overlap phase A of chunk j-1; the
+    // parity buffer is free once phase A of chunk j-2 is done)
+    hipStream_t st = serial ? stream_ : stream_t_;
+    if (!serial && j >= 2) HIPCHK(hipStreamWaitEvent(st, hdone_ev_[par], 0));
+    HIPCHK(launch_huff_tables(fbase, dblocks_.p, cb, ce - cb, tables_[par].p, tinfo_[par].p, st));
+    if (!serial) {
+      HIPCHK(hipEventRecord(tab_ev_[par], st));
+      HIPCHK(hipStreamWaitEvent(stream_, tab_ev_[par], 0));
+    }
+    HIPCHK(launch_inflate_huff_prebuilt(fbase, dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, max_stage,
+                                        tables_[par].p, tinfo_[par].p, stream_));
+    if (!serial) HIPCHK(hipEventRecord(hdone_ev_[par], stream_));
     if (timing) HIPCHK(hipEventRecord(tev_[3 * j + 1], stream_));
     if (!serial) {
       HIPCHK(hipEventRecord(sync_ev_[par], stream_));

@@ -188,8 +188,11 @@ class Pipeline {
   std::vector<uint8_t> inflated_;  // per block flag
   DevBuf<uint32_t> tokens_[2];  // double-buffered LZ77 token streams (chunk parity)
   DevBuf<HuffOut> hout_;
-  DevBuf<uint8_t> tables_;        // phase-A prebuilt table images (per chunk)
-  DevBuf<HuffTableInfo> tinfo_;
+  DevBuf<uint8_t> tables_[2];     // phase-A prebuilt table images (per chunk, by chunk parity)
+  DevBuf<HuffTableInfo> tinfo_[2];
+  hipStream_t stream_t_ = nullptr;  // table prebuild of chunk j+1 beside phase A of chunk j
+  hipEvent_t tab_ev_[2];            // tables of the chunk of that parity built
+  hipEvent_t hdone_ev_[2];          // phase A of the chunk of that parity done (tables free)
 
   // span scratch
   DevBuf<uint64_t> g_, x_, x2_, entry_, base_arr_, summary_, dead_;
