@@ -5,11 +5,13 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <string>
 #include <vector>
 
+#include "hbam_deflate_api.h"
 #include "hbam_host.h"
 
 using hadoop_bam::BAMInputFormat;
@@ -35,6 +37,7 @@ struct hbam_gpu {
   hbam::SpanDev span;
   hbam::DevBuf<uint8_t> enc;  // hbam_gpu_encode_writables output
   uint64_t enc_bytes = 0;
+  std::unique_ptr<hbam::BgzfCompressor> bgzf;  // hbam_gpu_bgzf_compress
 };
 
 namespace {
@@ -105,6 +108,74 @@ void hbam_close(hbam_ctx* ctx) { delete ctx; }
 const char* hbam_last_error(hbam_ctx* ctx) { return ctx ? ctx->err.c_str() : g_open_err.c_str(); }
 
 void hbam_free(void* p) { free(p); }
+
+int hbam_bgzf_compress(const hbam_opts* opts, const void* data, uint64_t len, const uint32_t* block_lens,
+                       uint64_t n_blocks, int32_t block_size, int32_t level, int32_t flags, uint8_t** out,
+                       uint64_t* out_len) {
+  *out = nullptr;
+  *out_len = 0;
+  hbam_opts o{};
+  if (opts) o = *opts;
+  std::vector<uint64_t> ustart;
+  std::vector<uint32_t> lens;
+  uint64_t pos = 0;
+  if (block_lens) {
+    for (uint64_t i = 0; i < n_blocks; ++i) {
+      ustart.push_back(pos);
+      lens.push_back(block_lens[i]);
+      pos += block_lens[i];
+    }
+    if (pos != len) {
+      g_open_err = "block_lens do not sum to len";
+      return HBAM_E_ARG;
+    }
+  } else {
+    if (block_size <= 0 || block_size > 65536) {
+      g_open_err = "block_size must be 1..65536";
+      return HBAM_E_ARG;
+    }
+    for (; pos < len; pos += (uint64_t)block_size) {
+      ustart.push_back(pos);
+      lens.push_back((uint32_t)std::min<uint64_t>((uint64_t)block_size, len - pos));
+    }
+  }
+  if (o.device < 0 || o.device >= hbam_device_count()) {
+    g_open_err = "no HIP device " + std::to_string(o.device);
+    return HBAM_E_DEVICE;
+  }
+  if (hipSetDevice(o.device) != hipSuccess) return HBAM_E_DEVICE;
+  hipStream_t s;
+  if (hipStreamCreate(&s) != hipSuccess) return HBAM_E_DEVICE;
+  uint8_t* d_in = nullptr;
+  int rc = HBAM_OK;
+  if (hipMalloc(reinterpret_cast<void**>(&d_in), len ? len : 1) != hipSuccess ||
+      (len && hipMemcpyAsync(d_in, data, len, hipMemcpyHostToDevice, s) != hipSuccess)) {
+    g_open_err = "device buffer for the payload";
+    rc = HBAM_E_DEVICE;
+  }
+  {
+    hbam::BgzfCompressor c(o.device);
+    if (rc == HBAM_OK) {
+      rc = c.compress(d_in, ustart, lens, level, (flags & HBAM_BGZF_EOF) != 0, s, nullptr);
+      if (rc != HBAM_OK) g_open_err = c.error();
+    }
+    if (rc == HBAM_OK) {
+      uint8_t* h = static_cast<uint8_t*>(malloc(c.out_len() ? c.out_len() : 1));
+      if (!h) {
+        rc = HBAM_E_NOMEM;
+      } else if (c.out_len() && hipMemcpy(h, c.d_out(), c.out_len(), hipMemcpyDeviceToHost) != hipSuccess) {
+        free(h);
+        rc = HBAM_E_DEVICE;
+      } else {
+        *out = h;
+        *out_len = c.out_len();
+      }
+    }
+  }
+  if (d_in) (void)hipFree(d_in);
+  (void)hipStreamDestroy(s);
+  return rc;
+}
 
 int hbam_header(hbam_ctx* ctx, hbam_header_info* out) {
   if (!ctx || !ctx->f) return HBAM_E_STATE;
@@ -562,6 +633,47 @@ int hbam_gpu_fetch_encoded(hbam_gpu* g, uint64_t pos, uint64_t len, uint8_t* dst
     return HBAM_E_ARG;
   }
   if (len && hipMemcpy(dst, g->enc.p + pos, len, hipMemcpyDeviceToHost) != hipSuccess) return HBAM_E_DEVICE;
+  return HBAM_OK;
+}
+
+int hbam_gpu_bgzf_compress(hbam_gpu* g, int32_t level, int32_t flags, int32_t iters, float* ms_per_iter,
+                           uint64_t* out_len) {
+  *ms_per_iter = 0;
+  *out_len = 0;
+  hbam::Pipeline& p = *g->p;
+  if (!p.d_u()) {
+    g->err = "hbam_gpu_bgzf_compress needs a run (inflated stream) first";
+    return HBAM_E_STATE;
+  }
+  std::vector<uint64_t> ustart;
+  std::vector<uint32_t> lens;
+  for (const auto& b : p.blocks()) {
+    ustart.push_back(b.ustart);
+    lens.push_back(b.isize);
+  }
+  if (!g->bgzf) g->bgzf.reset(new hbam::BgzfCompressor(p.device()));
+  float ms = 0, tot = 0;
+  int rc = g->bgzf->compress(p.d_u(), ustart, lens, level, (flags & HBAM_BGZF_EOF) != 0, p.stream(), &ms);
+  for (int32_t i = 0; i < iters && rc == HBAM_OK; ++i) {
+    rc = g->bgzf->compress(p.d_u(), ustart, lens, level, (flags & HBAM_BGZF_EOF) != 0, p.stream(), &ms);
+    tot += ms;
+  }
+  if (rc != HBAM_OK) {
+    g->err = g->bgzf->error();
+    return rc;
+  }
+  *ms_per_iter = iters > 0 ? tot / (float)iters : ms;
+  *out_len = g->bgzf->out_len();
+  return HBAM_OK;
+}
+
+int hbam_gpu_fetch_compressed(hbam_gpu* g, uint64_t pos, uint64_t len, uint8_t* dst) {
+  const uint64_t n = g->bgzf ? g->bgzf->out_len() : 0;
+  if (pos > n || len > n - pos) {
+    g->err = "range outside the compressed output";
+    return HBAM_E_ARG;
+  }
+  if (len && hipMemcpy(dst, g->bgzf->d_out() + pos, len, hipMemcpyDeviceToHost) != hipSuccess) return HBAM_E_DEVICE;
   return HBAM_OK;
 }
 

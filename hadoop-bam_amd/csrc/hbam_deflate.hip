@@ -1,0 +1,277 @@
+// hbam_deflate.hip -- BGZF write path on the GPU: [htsjdk]
+// BlockCompressedOutputStream.deflateBlock + writeGzipBlock for every block
+// of a payload stream at once (the compressor behind BAMRecordWriter /
+// KeyIgnoringBAMRecordWriter output, BAMRecordWriter.java:131-149).
+//
+//   k_deflate_blocks  one lane per BGZF block: zlib 1.2.11 deflate_slow +
+//                     trees.c restated in hbam_deflate.h (byte-identical
+//                     output), hash chains / symbol buffer / trees in a
+//                     per-lane arena in HBM, cdata into a 64 KiB slot.
+//   k_dfl_crc         one workgroup per block: CRC-32 of the payload
+//                     (per-thread slices combined with x^(8n) mod P).
+//   k_dfl_frame       one workgroup per block: 18-byte BGZF header, cdata
+//                     (or htsjdk's level-0 fallback: one stored block) and
+//                     the CRC32 / ISIZE footer at the block's file offset.
+// Deflate is a serial recurrence within a block (lazy matching over hash
+// chains), so parallelism is across blocks; the host only turns the per-block
+// sizes into file offsets.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "hbam_deflate.h"
+#include "hbam_deflate_api.h"
+
+namespace hbam {
+
+namespace {
+
+constexpr uint32_t kSlot = 65536;      // cdata slot per block
+constexpr uint32_t kMaxLanes = 65536;  // concurrent arenas (~184 KiB each)
+constexpr uint32_t kCrcPoly = 0xedb88320u;
+constexpr uint32_t kWavesTarget = 2048;
+
+__device__ inline uint32_t crc_mul(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = (b & 1) ? (b >> 1) ^ kCrcPoly : b >> 1;
+  }
+  return p;
+}
+
+__device__ inline uint32_t crc_x8n(uint64_t n) {  // x^(8n) mod P (zlib x2nmodp(n, 3))
+  uint32_t p = 1u << 31, x2n = 1u << 30;
+  for (int k = 0; k < 3; ++k) x2n = crc_mul(x2n, x2n);
+  while (n) {
+    if (n & 1) p = crc_mul(x2n, p);
+    n >>= 1;
+    x2n = crc_mul(x2n, x2n);
+  }
+  return p;
+}
+
+__global__ __launch_bounds__(64) void k_deflate_blocks(const uint8_t* __restrict__ in, const uint64_t* __restrict__ ustart,
+                                                       const uint32_t* __restrict__ lens, uint32_t b0, uint32_t nb,
+                                                       int level, const dfl::Tables* __restrict__ tables,
+                                                       dfl::Arena* __restrict__ arenas, uint8_t* __restrict__ slots,
+                                                       uint32_t* __restrict__ csize, uint8_t* __restrict__ ovf,
+                                                       uint32_t lpw) {
+  // lpw active lanes per wave: the work is a serial, latency-bound recurrence
+  // per lane, so spreading blocks over more SIMDs (and fewer divergent lanes
+  // per wave) beats packing 64 lanes into one wave
+  if (threadIdx.x >= lpw) return;
+  const uint32_t i = blockIdx.x * lpw + threadIdx.x;
+  if (i >= nb) return;
+  const uint32_t b = b0 + i;
+  dfl::Arena* a = arenas + i;
+  uint4* h = reinterpret_cast<uint4*>(a->head);
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  for (int k = 0; k < (int)(sizeof(a->head) / 16); ++k) h[k] = z;
+  bool o = false;
+  const uint32_t n = dfl::deflate_block(a, tables, level, in + ustart[b], lens[b], slots + (uint64_t)b * kSlot,
+                                        dfl::kOutCap, &o, true);
+  csize[b] = n;
+  ovf[b] = o ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void k_dfl_crc(const uint8_t* __restrict__ in, const uint64_t* __restrict__ ustart,
+                                                 const uint32_t* __restrict__ lens, uint32_t* __restrict__ crc) {
+  __shared__ uint32_t tab[256];
+  __shared__ uint32_t part[256];
+  const uint32_t b = blockIdx.x;
+  const uint32_t len = lens[b];
+  const uint8_t* p = in + ustart[b];
+  {
+    uint32_t c = threadIdx.x;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
+    tab[threadIdx.x] = c;
+  }
+  __syncthreads();
+  const uint32_t slice = (len + 255) / 256;
+  const uint32_t s0 = min(len, threadIdx.x * slice), s1 = min(len, s0 + slice);
+  uint32_t r = 0;
+  for (uint32_t i = s0; i < s1; ++i) r = tab[(r ^ p[i]) & 0xff] ^ (r >> 8);
+  part[threadIdx.x] = r;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t R = 0xffffffffu;
+    const uint32_t xs = slice ? crc_x8n(slice) : 0;
+    for (uint32_t t = 0; t < 256; ++t) {
+      const uint32_t a = min(len, t * slice), e = min(len, a + slice);
+      if (e == a) continue;
+      R = crc_mul(e - a == slice ? xs : crc_x8n(e - a), R) ^ part[t];
+    }
+    crc[b] = R ^ 0xffffffffu;
+  }
+}
+
+// BGZF framing ([htsjdk] BlockCompressedOutputStream.writeGzipBlock)
+__global__ __launch_bounds__(256) void k_dfl_frame(const uint8_t* __restrict__ in, const uint64_t* __restrict__ ustart,
+                                                   const uint32_t* __restrict__ lens,
+                                                   const uint8_t* __restrict__ slots,
+                                                   const uint32_t* __restrict__ csize, const uint8_t* __restrict__ ovf,
+                                                   const uint32_t* __restrict__ crc, const uint64_t* __restrict__ offs,
+                                                   uint8_t* __restrict__ out) {
+  const uint32_t b = blockIdx.x;
+  const uint32_t len = lens[b];
+  const bool stored = ovf[b] != 0;
+  const uint32_t cn = stored ? len + 5 : csize[b];
+  uint8_t* o = out + offs[b];
+  const uint32_t total = cn + 26;
+  if (threadIdx.x < 18) {
+    const uint8_t hdr[16] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C', 2, 0};
+    const uint32_t t = threadIdx.x;
+    o[t] = t < 16 ? hdr[t] : (uint8_t)((total - 1) >> (8 * (t - 16)));
+  } else if (threadIdx.x < 26) {
+    const uint32_t t = threadIdx.x - 18;
+    o[18 + cn + t] = (uint8_t)((t < 4 ? crc[b] : len) >> (8 * (t & 3)));
+  }
+  uint8_t* c = o + 18;
+  if (!stored) {
+    const uint8_t* s = slots + (uint64_t)b * kSlot;
+    for (uint32_t i = threadIdx.x; i < cn; i += 256) c[i] = s[i];
+  } else {  // Deflater(NO_COMPRESSION): one final stored block
+    if (threadIdx.x == 0) {
+      c[0] = 1;
+      c[1] = (uint8_t)len;
+      c[2] = (uint8_t)(len >> 8);
+      c[3] = (uint8_t)~len;
+      c[4] = (uint8_t)(~len >> 8);
+    }
+    const uint8_t* s = in + ustart[b];
+    for (uint32_t i = threadIdx.x; i < len; i += 256) c[5 + i] = s[i];
+  }
+}
+
+}  // namespace
+
+#define DCHK(x)                                                   \
+  do {                                                            \
+    hipError_t e_ = (x);                                          \
+    if (e_ != hipSuccess) {                                       \
+      err_ = std::string(#x) + ": " + hipGetErrorString(e_);      \
+      return kDeviceErr;                                          \
+    }                                                             \
+  } while (0)
+
+BgzfCompressor::BgzfCompressor(int device) : device_(device) {}
+
+BgzfCompressor::~BgzfCompressor() {
+  for (void* p : {(void*)tables_, (void*)arenas_, (void*)slots_, (void*)csize_, (void*)ovf_, (void*)crc_,
+                  (void*)offs_, (void*)out_, (void*)ustart_, (void*)lens_})
+    if (p) (void)hipFree(p);
+}
+
+template <typename T>
+static hipError_t grow_buf(T** p, size_t* have, size_t need) {
+  if (*p && *have >= need) return hipSuccess;
+  if (*p) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(*p);
+  }
+  *p = nullptr;
+  *have = 0;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), need ? need : 1);
+  if (e == hipSuccess) *have = need;
+  return e;
+}
+
+int BgzfCompressor::compress(const uint8_t* d_in, const std::vector<uint64_t>& ustart,
+                             const std::vector<uint32_t>& lens, int level, bool eof, hipStream_t s, float* ms) {
+  const int kDeviceErr = 5, kArgErr = 3, kFormatErr = 1;
+  if (level < 4 || level > 9) {
+    err_ = "level must be 4..9 (deflate_slow levels; htsjdk default 5)";
+    return kArgErr;
+  }
+  const uint64_t nb = lens.size();
+  for (uint32_t l : lens)
+    if (l > 65536) {
+      err_ = "BGZF payload above 65536 bytes";
+      return kArgErr;
+    }
+  DCHK(hipSetDevice(device_));
+  if (!tables_) {
+    dfl::Tables t;
+    dfl::build_tables(&t);
+    DCHK(hipMalloc(reinterpret_cast<void**>(&tables_), sizeof t));
+    DCHK(hipMemcpy(tables_, &t, sizeof t, hipMemcpyHostToDevice));
+  }
+  const uint32_t lanes = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(nb, 1), kMaxLanes);
+  DCHK(grow_buf(&arenas_, &arenas_n_, (size_t)lanes * sizeof(dfl::Arena)));
+  DCHK(grow_buf(&slots_, &slots_n_, std::max<uint64_t>(nb, 1) * kSlot));
+  DCHK(grow_buf(&csize_, &csize_n_, std::max<uint64_t>(nb, 1) * 4));
+  DCHK(grow_buf(&ovf_, &ovf_n_, std::max<uint64_t>(nb, 1)));
+  DCHK(grow_buf(&crc_, &crc_n_, std::max<uint64_t>(nb, 1) * 4));
+  DCHK(grow_buf(&offs_, &offs_n_, (nb + 1) * 8));
+  DCHK(grow_buf(&ustart_, &ustart_n_, std::max<uint64_t>(nb, 1) * 8));
+  DCHK(grow_buf(&lens_, &lens_n_, std::max<uint64_t>(nb, 1) * 4));
+  hipEvent_t e0, e1;
+  DCHK(hipEventCreate(&e0));
+  DCHK(hipEventCreate(&e1));
+  DCHK(hipEventRecord(e0, s));
+  if (nb) {
+    DCHK(hipMemcpyAsync(ustart_, ustart.data(), nb * 8, hipMemcpyHostToDevice, s));
+    DCHK(hipMemcpyAsync(lens_, lens.data(), nb * 4, hipMemcpyHostToDevice, s));
+    for (uint64_t b0 = 0; b0 < nb; b0 += lanes) {
+      const uint32_t n = (uint32_t)std::min<uint64_t>(lanes, nb - b0);
+      // about kWavesTarget waves in flight (2 per SIMD on 256 CUs x 4 SIMDs)
+      const uint32_t lpw = std::max<uint32_t>(1, std::min<uint32_t>(64, (n + kWavesTarget - 1) / kWavesTarget));
+      hipLaunchKernelGGL(k_deflate_blocks, dim3((n + lpw - 1) / lpw), dim3(64), 0, s, d_in, ustart_, lens_,
+                         (uint32_t)b0, n, level, tables_, arenas_, slots_, csize_, ovf_, lpw);
+      DCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_dfl_crc, dim3((uint32_t)nb), dim3(256), 0, s, d_in, ustart_, lens_, crc_);
+    DCHK(hipGetLastError());
+  }
+  std::vector<uint32_t> cs(nb);
+  std::vector<uint8_t> ov(nb);
+  if (nb) {
+    DCHK(hipMemcpyAsync(cs.data(), csize_, nb * 4, hipMemcpyDeviceToHost, s));
+    DCHK(hipMemcpyAsync(ov.data(), ovf_, nb, hipMemcpyDeviceToHost, s));
+  }
+  DCHK(hipStreamSynchronize(s));
+  std::vector<uint64_t> offs(nb + 1);
+  uint64_t o = 0;
+  for (uint64_t b = 0; b < nb; ++b) {
+    offs[b] = o;
+    if (ov[b] && lens[b] + 5 > dfl::kOutCap) {
+      err_ = "incompressible BGZF payload does not fit one stored block";
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      return kFormatErr;
+    }
+    o += 26 + (ov[b] ? lens[b] + 5 : cs[b]);
+  }
+  offs[nb] = o;
+  static const uint8_t kEof[28] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43,
+                                   2,    0,    0x1b, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  out_len_ = o + (eof ? 28 : 0);
+  DCHK(grow_buf(&out_, &out_n_, out_len_ + 16));
+  if (nb) {
+    DCHK(hipMemcpyAsync(offs_, offs.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_dfl_frame, dim3((uint32_t)nb), dim3(256), 0, s, d_in, ustart_, lens_, slots_, csize_, ovf_,
+                       crc_, offs_, out_);
+    DCHK(hipGetLastError());
+  }
+  if (eof) DCHK(hipMemcpyAsync(out_ + o, kEof, 28, hipMemcpyHostToDevice, s));
+  DCHK(hipEventRecord(e1, s));
+  DCHK(hipEventSynchronize(e1));
+  float t = 0;
+  DCHK(hipEventElapsedTime(&t, e0, e1));
+  if (ms) *ms = t;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  fallbacks_ = 0;
+  for (uint8_t v : ov) fallbacks_ += v;
+  return 0;
+}
+
+}  // namespace hbam

@@ -99,6 +99,12 @@ _sig("hbam_gpu_run_streamed", C.c_int, [P, P, u64, u64, C.POINTER(GpuStats)])
 _sig("hbam_host_alloc", P, [u64])
 _sig("hbam_host_free", None, [P])
 _sig("hbam_gpu_d2d_bandwidth", C.c_int, [P, u64, i32, C.POINTER(C.c_float)])
+_sig("hbam_bgzf_compress", C.c_int, [C.POINTER(Opts), P, u64, P, u64, i32, i32, i32, C.POINTER(P), C.POINTER(u64)])
+_sig("hbam_gpu_bgzf_compress", C.c_int, [P, i32, i32, i32, C.POINTER(C.c_float), C.POINTER(u64)])
+_sig("hbam_gpu_fetch_compressed", C.c_int, [P, u64, u64, P])
+
+BGZF_EOF = 1
+HTSJDK_BLOCK_SIZE = 65498  # ISIZE of every full block of test.bam (htsjdk-written)
 
 
 def lib():
@@ -124,6 +130,34 @@ def device_count():
 
 def murmurhash3(data: bytes, seed=0):
     return _L.hbam_murmurhash3(C.c_char_p(bytes(data)), len(data), seed)
+
+
+def bgzf_compress(data, block_lens=None, block_size=HTSJDK_BLOCK_SIZE, level=5, eof=True, device=0):
+    """[htsjdk] BlockCompressedOutputStream over `data` on the GPU
+    (hbam_bgzf_compress): the BGZF file bytes.  block_lens (optional) cuts
+    the payload as the writer's flushes did; else every block_size bytes."""
+    if isinstance(data, np.ndarray):
+        buf, n = data, data.nbytes
+        ptr = data.ctypes.data if n else None
+    else:
+        buf = C.create_string_buffer(bytes(data), max(len(data), 1))
+        ptr, n = buf, len(data)
+    lens = None
+    nl = 0
+    if block_lens is not None:
+        lens = np.ascontiguousarray(np.asarray(block_lens, dtype=np.uint32))
+        nl = len(lens)
+    o = Opts(device, 0, 0, 0)
+    out = P()
+    olen = u64()
+    rc = _L.hbam_bgzf_compress(C.byref(o), ptr, n, lens.ctypes.data if nl else None, nl, block_size, level,
+                               BGZF_EOF if eof else 0, C.byref(out), C.byref(olen))
+    if rc != OK:
+        raise HbamError(rc, _L.hbam_gpu_error(None).decode())
+    try:
+        return C.string_at(out, olen.value)
+    finally:
+        _L.hbam_free(out)
 
 
 def get_key0(ref_idx, start0):
@@ -445,6 +479,23 @@ class Gpu:
         if rc != OK:
             raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
         return buf.raw[:length]
+
+    def bgzf_compress(self, level=5, eof=True, iters=0):
+        """BGZF-compress the last run's inflated stream with the loaded file's
+        block boundaries (hbam_gpu_bgzf_compress): (ms per compress, bytes)."""
+        ms = C.c_float()
+        nb = u64()
+        rc = _L.hbam_gpu_bgzf_compress(self._h, level, BGZF_EOF if eof else 0, iters, C.byref(ms), C.byref(nb))
+        if rc != OK:
+            raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
+        return ms.value, nb.value
+
+    def fetch_compressed(self, pos, length):
+        buf = np.empty(max(length, 1), np.uint8)
+        rc = _L.hbam_gpu_fetch_compressed(self._h, pos, length, buf.ctypes.data)
+        if rc != OK:
+            raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
+        return buf[:length]
 
     def fetch(self, n):
         keys = np.zeros(max(n, 1), np.int64)

@@ -156,6 +156,22 @@ int hbam_decode_writables(hbam_ctx *ctx, const void *buf, uint64_t len, const ui
  * hbam_decode_writables. */
 int hbam_open_codec(const hbam_opts *opts, hbam_ctx **out);
 
+/* ---- BGZF write path ---- */
+#define HBAM_BGZF_EOF 1 /* append the 28-byte BGZF EOF terminator (BlockCompressedOutputStream.close) */
+/* [htsjdk] BlockCompressedOutputStream.write + deflateBlock + writeGzipBlock
+ * (the compressor BAMRecordWriter.java:131-149 writes through) for a whole
+ * payload stream, every block DEFLATEd on the GPU in one launch: one
+ * java.util.zip.Deflater(level, nowrap) reset per block, output
+ * byte-identical to zlib 1.2.11 (levels 4..9; htsjdk's default is 5); a block
+ * that does not fit the 65518-byte compressed buffer is written by the
+ * NO_COMPRESSION fallback (one stored block).  Blocks: block_lens[0..n_blocks)
+ * (each <= 65536, as BlockCompressedOutputStream.flush cuts them), or when
+ * block_lens is NULL, len cut every block_size bytes.  *out (BGZF file bytes)
+ * is released with hbam_free. */
+int hbam_bgzf_compress(const hbam_opts *opts, const void *data, uint64_t len, const uint32_t *block_lens,
+                       uint64_t n_blocks, int32_t block_size, int32_t level, int32_t flags, uint8_t **out,
+                       uint64_t *out_len);
+
 /* BGZF block table (coff, csize, isize, ustart) and inflated bytes: used by
  * tests and by the BGZF text formats. */
 int hbam_blocks(hbam_ctx *ctx, uint64_t *coff, uint32_t *csize, uint32_t *isize, uint64_t *ustart,
@@ -221,6 +237,14 @@ int hbam_gpu_d2d_bandwidth(hbam_gpu *g, uint64_t bytes, int32_t iters, float *gb
  * hbam_gpu_fetch_encoded copies [pos, pos+len) of the result to the host. */
 int hbam_gpu_encode_writables(hbam_gpu *g, int32_t iters, float *ms_per_iter, uint64_t *bytes);
 int hbam_gpu_fetch_encoded(hbam_gpu *g, uint64_t pos, uint64_t len, uint8_t *dst);
+/* BGZF-compress the inflated stream of the last run on the GPU with the
+ * loaded file's block boundaries (hbam_bgzf_compress semantics; iters timed
+ * repetitions, HIP events); the result stays in HBM, hbam_gpu_fetch_compressed
+ * copies [pos, pos+len) of it to the host.  Recompressing a file written by
+ * zlib at the same level reproduces it byte for byte. */
+int hbam_gpu_bgzf_compress(hbam_gpu *g, int32_t level, int32_t flags, int32_t iters, float *ms_per_iter,
+                           uint64_t *out_len);
+int hbam_gpu_fetch_compressed(hbam_gpu *g, uint64_t pos, uint64_t len, uint8_t *dst);
 /* Copy results of the last run to the host (any pointer may be NULL). */
 int hbam_gpu_fetch(hbam_gpu *g, int64_t *keys, uint64_t *voffs, uint64_t cap);
 int32_t hbam_device_count(void);

@@ -107,6 +107,68 @@ static int inflate_block(orc_stream *s, const uint8_t *f, const orc_block *b, ui
 
 uint32_t orc_crc32(const uint8_t *p, uint64_t n) { return (uint32_t)crc32(0L, p, (uInt)n); }
 
+/* [htsjdk] BlockCompressedOutputStream.deflateBlock / writeGzipBlock (not
+ * vendored in the reference; restated from htsjdk 2.13.2's published
+ * behaviour): the BGZF writer under BAMRecordWriter.java:131-149. */
+uint64_t orc_bgzf_compress(const uint8_t *data, uint64_t len, const uint32_t *block_lens,
+                           uint64_t nblk, int level, int eof, uint8_t *out) {
+  enum { kCap = 65536 - 18 };
+  static const uint8_t eofb[28] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43,
+                                   2, 0, 0x1b, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  z_stream z, z0;
+  memset(&z, 0, sizeof z);
+  memset(&z0, 0, sizeof z0);
+  if (deflateInit2(&z, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return UINT64_MAX;
+  if (deflateInit2(&z0, 0, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return UINT64_MAX;
+  uint8_t *cbuf = (uint8_t *)malloc(kCap);
+  uint64_t o = 0, pos = 0;
+  (void)len;
+  for (uint64_t b = 0; b < nblk; ++b) {
+    const uint32_t n = block_lens[b];
+    deflateReset(&z);
+    z.next_in = (Bytef *)(data + pos);
+    z.avail_in = n;
+    z.next_out = cbuf;
+    z.avail_out = kCap;
+    int rc = deflate(&z, Z_FINISH);
+    uint32_t cn = kCap - z.avail_out;
+    if (rc != Z_STREAM_END) { /* deflater.finished() false -> NO_COMPRESSION deflater */
+      deflateReset(&z0);
+      z0.next_in = (Bytef *)(data + pos);
+      z0.avail_in = n;
+      z0.next_out = cbuf;
+      z0.avail_out = kCap;
+      if (deflate(&z0, Z_FINISH) != Z_STREAM_END) {
+        o = UINT64_MAX;
+        break;
+      }
+      cn = kCap - z0.avail_out;
+    }
+    const uint32_t total = cn + 26;
+    if (out) {
+      static const uint8_t hdr[16] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C', 2, 0};
+      uint8_t *q = out + o;
+      memcpy(q, hdr, 16);
+      q[16] = (uint8_t)(total - 1);
+      q[17] = (uint8_t)((total - 1) >> 8);
+      memcpy(q + 18, cbuf, cn);
+      const uint32_t c = (uint32_t)crc32(0L, data + pos, n);
+      for (int k = 0; k < 4; ++k) q[18 + cn + k] = (uint8_t)(c >> (8 * k));
+      for (int k = 0; k < 4; ++k) q[22 + cn + k] = (uint8_t)(n >> (8 * k));
+    }
+    o += total;
+    pos += n;
+  }
+  if (o != UINT64_MAX && eof) {
+    if (out) memcpy(out + o, eofb, 28);
+    o += 28;
+  }
+  free(cbuf);
+  deflateEnd(&z);
+  deflateEnd(&z0);
+  return o;
+}
+
 /* logical stream helpers ------------------------------------------------- */
 
 /* first block index with ustart >= pos */

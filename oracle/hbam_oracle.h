@@ -121,6 +121,16 @@ int orc_get_splits(orc_stream *s, const uint8_t *file, uint64_t flen,
                    const uint8_t *sbi, uint64_t sbi_len, uint64_t *vstarts,
                    uint64_t *vends, uint64_t *nout);
 
+/* [htsjdk] BlockCompressedOutputStream (write + deflateBlock + writeGzipBlock,
+ * close() with the EOF terminator when eof != 0): one zlib raw deflater
+ * (level, windowBits -15, memLevel 8 -- java.util.zip.Deflater(level, true)),
+ * deflateReset per block, deflate(Z_FINISH) into a 65518-byte buffer; a block
+ * that does not finish there goes through the NO_COMPRESSION deflater.
+ * block_lens[0..nblk) cut data (their sum = len).  Returns the BGZF byte
+ * count (out == NULL only sizes; out needs len+64*nblk+28 bytes at most), or UINT64_MAX on a zlib error. */
+uint64_t orc_bgzf_compress(const uint8_t *data, uint64_t len, const uint32_t *block_lens,
+                           uint64_t nblk, int level, int eof, uint8_t *out);
+
 /* zlib crc32, for tests */
 uint32_t orc_crc32(const uint8_t *p, uint64_t n);
 

@@ -51,6 +51,8 @@ def lib():
         L.orc_guess_next_bgzf_block_start.argtypes = [P, u64, u64, u64]
         L.orc_guess_next_bgzf_block_start.restype = i64
         L.orc_get_splits.argtypes = [P, P, u64, P, P, u64, P, u64, P, P, C.POINTER(u64)]
+        L.orc_bgzf_compress.argtypes = [P, u64, P, u64, C.c_int, C.c_int, P]
+        L.orc_bgzf_compress.restype = u64
         L.orc_crc32.argtypes = [P, u64]
         L.orc_crc32.restype = u32
         L.orc_writable_encode.argtypes = [P, P, P, P]
@@ -241,3 +243,19 @@ def guess_next_bgzf_block_start(file: bytes, beg, end):
 
 def crc32(b: bytes):
     return lib().orc_crc32(C.c_char_p(bytes(b)), len(b))
+
+
+def bgzf_compress(data: bytes, block_lens, level=5, eof=True) -> bytes:
+    """[htsjdk] BlockCompressedOutputStream over `data` cut into block_lens
+    (zlib raw deflater reset per block; see orc_bgzf_compress)."""
+    L = lib()
+    lens = np.ascontiguousarray(np.asarray(block_lens, dtype=np.uint32))
+    assert int(lens.sum()) == len(data)
+    buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    cap = len(data) + 64 * len(lens) + 28 + 16  # stored sub-blocks: <= 5 x 5 B + 26 B framing per block
+    out = np.empty(cap, dtype=np.uint8)
+    n = L.orc_bgzf_compress(buf.ctypes.data, len(data), lens.ctypes.data if len(lens) else None, len(lens),
+                            level, 1 if eof else 0, out.ctypes.data)
+    if n == (1 << 64) - 1:
+        raise OracleError(4, "zlib deflate failed")
+    return out[:n].tobytes()
