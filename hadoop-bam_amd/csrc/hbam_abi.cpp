@@ -148,7 +148,7 @@ int hbam_bgzf_compress(const hbam_opts* opts, const void* data, uint64_t len, co
   if (hipStreamCreate(&s) != hipSuccess) return HBAM_E_DEVICE;
   uint8_t* d_in = nullptr;
   int rc = HBAM_OK;
-  if (hipMalloc(reinterpret_cast<void**>(&d_in), len ? len : 1) != hipSuccess ||
+  if (hipMalloc(reinterpret_cast<void**>(&d_in), len + 64) != hipSuccess ||  // 64 B pad: deflate's 8-byte compares
       (len && hipMemcpyAsync(d_in, data, len, hipMemcpyHostToDevice, s) != hipSuccess)) {
     g_open_err = "device buffer for the payload";
     rc = HBAM_E_DEVICE;

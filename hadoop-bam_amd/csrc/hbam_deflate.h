@@ -21,11 +21,14 @@
 // k_deflate_blocks (hbam_deflate.hip).
 #pragma once
 #include <stdint.h>
+#include <string.h>
 
 #if defined(__HIPCC__)
 #define DFL_HD __host__ __device__
+#define DFL_NOINLINE __attribute__((noinline))
 #else
 #define DFL_HD
+#define DFL_NOINLINE
 #endif
 
 namespace hbam {
@@ -444,7 +447,7 @@ DFL_HD inline void compress_block(State& s, const CodeT* lcode, const LenT* llen
 }
 
 // _tr_flush_block (trees.c), level > 0
-DFL_HD inline void flush_block(State& s, bool has_buf, uint32_t buf_start, uint32_t stored_len, int last) {
+DFL_HD DFL_NOINLINE void flush_block(State& s, bool has_buf, uint32_t buf_start, uint32_t stored_len, int last) {
   build_tree(s, s.l);
   build_tree(s, s.d);
   // build_bl_tree
@@ -485,6 +488,22 @@ DFL_HD inline void flush_block(State& s, bool has_buf, uint32_t buf_start, uint3
   if (last) s.out.windup();
 }
 
+// 8 bytes at any address (device: two aligned loads + funnel shift; the
+// buffers carry >= 16 bytes of padding past the last payload)
+DFL_HD inline uint64_t ld8(const uint8_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uintptr_t a = (uintptr_t)p;
+  const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
+  const unsigned sh = (unsigned)(a & 7) * 8;
+  const uint64_t lo = q[0];
+  return sh ? (lo >> sh) | (q[1] << (64 - sh)) : lo;
+#else
+  uint64_t v;
+  memcpy(&v, p, 8);
+  return v;
+#endif
+}
+
 DFL_HD inline uint32_t longest_match(State& s, uint32_t cur_match) {
   unsigned chain_length = s.cfg.chain;
   const uint32_t scan = s.strstart;
@@ -496,6 +515,7 @@ DFL_HD inline uint32_t longest_match(State& s, uint32_t cur_match) {
   if (s.prev_length >= s.cfg.good) chain_length >>= 2;
   if ((uint32_t)nice_match > s.lookahead) nice_match = (int)s.lookahead;
   const uint8_t s0 = s.win(scan), s1 = s.win(scan + 1);
+  const bool fast = !s.slid && scan + kMaxMatch + 1 <= s.len;
   do {
     const uint32_t match = cur_match;
     if (s.win(match + best_len) != scan_end || s.win(match + best_len - 1) != scan_end1 || s.win(match) != s0 ||
@@ -503,7 +523,22 @@ DFL_HD inline uint32_t longest_match(State& s, uint32_t cur_match) {
       continue;
     // scan[2] == match[2] is assumed (equal hash, HASH_BITS >= 8)
     int len = 3;
-    while (len < kMaxMatch && s.win(scan + len) == s.win(match + len)) len++;
+    if (fast) {  // bytes 3..258 of both strings inside the payload, no remap
+      const uint8_t* ps = s.in + scan;
+      const uint8_t* pm = s.in + match;
+      for (;;) {
+        const uint64_t x = ld8(ps + len) ^ ld8(pm + len);
+        if (x) {
+          len += (int)(__builtin_ctzll(x) >> 3);
+          break;
+        }
+        len += 8;
+        if (len >= kMaxMatch) break;
+      }
+      if (len > kMaxMatch) len = kMaxMatch;
+    } else {
+      while (len < kMaxMatch && s.win(scan + len) == s.win(match + len)) len++;
+    }
     if (len > best_len) {
       s.match_start = cur_match;
       best_len = len;

@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -32,7 +33,7 @@ namespace {
 constexpr uint32_t kSlot = 65536;      // cdata slot per block
 constexpr uint32_t kMaxLanes = 65536;  // concurrent arenas (~184 KiB each)
 constexpr uint32_t kCrcPoly = 0xedb88320u;
-constexpr uint32_t kWavesTarget = 2048;
+constexpr uint32_t kWavesTarget = 8192;  // 8 waves per SIMD (57 VGPRs: occupancy 8)
 
 __device__ inline uint32_t crc_mul(uint32_t a, uint32_t b) {
   uint32_t m = 1u << 31, p = 0;
@@ -222,8 +223,12 @@ int BgzfCompressor::compress(const uint8_t* d_in, const std::vector<uint64_t>& u
     DCHK(hipMemcpyAsync(lens_, lens.data(), nb * 4, hipMemcpyHostToDevice, s));
     for (uint64_t b0 = 0; b0 < nb; b0 += lanes) {
       const uint32_t n = (uint32_t)std::min<uint64_t>(lanes, nb - b0);
-      // about kWavesTarget waves in flight (2 per SIMD on 256 CUs x 4 SIMDs)
-      const uint32_t lpw = std::max<uint32_t>(1, std::min<uint32_t>(64, (n + kWavesTarget - 1) / kWavesTarget));
+      // about kWavesTarget waves in flight over 256 CUs x 4 SIMDs
+      static const uint32_t waves = [] {
+        const char* e = getenv("HBAM_DFL_WAVES");  // experiment knob
+        return e ? (uint32_t)std::max(1, atoi(e)) : kWavesTarget;
+      }();
+      const uint32_t lpw = std::max<uint32_t>(1, std::min<uint32_t>(64, (n + waves - 1) / waves));
       hipLaunchKernelGGL(k_deflate_blocks, dim3((n + lpw - 1) / lpw), dim3(64), 0, s, d_in, ustart_, lens_,
                          (uint32_t)b0, n, level, tables_, arenas_, slots_, csize_, ovf_, lpw);
       DCHK(hipGetLastError());
