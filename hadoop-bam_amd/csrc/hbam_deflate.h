@@ -193,12 +193,35 @@ struct Out {  // pending output (send_bits / put_byte over a bounded buffer)
   }
 };
 
-struct State {
-  // input view
+// the emulated zlib window: a view over the payload
+struct Win {
   const uint8_t* in;
   uint32_t len;
-  bool slid;
   uint32_t copied;  // bytes moved down by the slide (len - wsize)
+  bool slid;
+  DFL_HD uint8_t pre(uint32_t y) const { return y < len ? in[y] : 0; }
+  DFL_HD uint8_t win(uint32_t x) const {
+    if (slid && x < copied) return pre(x + kWSize);
+    return pre(x);
+  }
+};
+
+// state touched only when a block is flushed (trees, bit writer): kept apart
+// from the hot matching state so the out-of-line flush_block does not force
+// the match loop's variables into scratch memory
+struct Cold {
+  Arena* a;
+  const Tables* t;
+  Win w;
+  uint32_t last_lit;
+  uint32_t opt_len, static_len;
+  Tree l, d, b;
+  Out out;
+  DFL_HD uint8_t win(uint32_t x) const { return w.win(x); }
+};
+
+struct State {
+  Win w;
   Arena* a;
   const Tables* t;
   Config cfg;
@@ -208,16 +231,8 @@ struct State {
   int match_available;
   uint32_t ins_h;
   uint32_t last_lit;
-  uint32_t opt_len, static_len;
-  Tree l, d, b;
-  Out out;
-
-  // window[x] of the emulated zlib window
-  DFL_HD uint8_t pre(uint32_t y) const { return y < len ? in[y] : 0; }
-  DFL_HD uint8_t win(uint32_t x) const {
-    if (slid && x < copied) return pre(x + kWSize);
-    return pre(x);
-  }
+  Cold* c;
+  DFL_HD uint8_t win(uint32_t x) const { return w.win(x); }
 };
 
 DFL_HD inline void insert_string(State& s, uint32_t str, uint32_t* match_head) {
@@ -226,7 +241,7 @@ DFL_HD inline void insert_string(State& s, uint32_t str, uint32_t* match_head) {
   s.a->head[s.ins_h] = (uint16_t)str;
 }
 
-DFL_HD inline void init_block(State& s) {
+DFL_HD inline void init_block(Cold& s) {
   for (int n = 0; n < kLCodes; n++) s.l.fc[n] = 0;
   for (int n = 0; n < kDCodes; n++) s.d.fc[n] = 0;
   for (int n = 0; n < kBlCodes; n++) s.b.fc[n] = 0;
@@ -239,7 +254,7 @@ DFL_HD inline bool smaller(const uint16_t* fc, const uint8_t* depth, int n, int 
   return fc[n] < fc[m] || (fc[n] == fc[m] && depth[n] <= depth[m]);
 }
 
-DFL_HD inline void pqdownheap(State& s, const uint16_t* fc, int k, int heap_len) {
+DFL_HD inline void pqdownheap(Cold& s, const uint16_t* fc, int k, int heap_len) {
   uint16_t* heap = s.a->heap;
   const uint8_t* depth = s.a->depth;
   int v = heap[k];
@@ -254,7 +269,7 @@ DFL_HD inline void pqdownheap(State& s, const uint16_t* fc, int k, int heap_len)
   heap[k] = (uint16_t)v;
 }
 
-DFL_HD inline void gen_bitlen(State& s, Tree& tr, int heap_max) {
+DFL_HD inline void gen_bitlen(Cold& s, Tree& tr, int heap_max) {
   uint16_t* fc = tr.fc;
   uint16_t* dl = tr.dl;
   uint16_t* bl_count = s.a->bl_count;
@@ -300,7 +315,7 @@ DFL_HD inline void gen_bitlen(State& s, Tree& tr, int heap_max) {
   }
 }
 
-DFL_HD inline void build_tree(State& s, Tree& tr) {
+DFL_HD inline void build_tree(Cold& s, Tree& tr) {
   uint16_t* fc = tr.fc;
   uint16_t* dl = tr.dl;
   uint16_t* heap = s.a->heap;
@@ -355,7 +370,7 @@ DFL_HD inline void build_tree(State& s, Tree& tr) {
   }
 }
 
-DFL_HD inline void scan_tree(State& s, Tree& tr, int max_code) {
+DFL_HD inline void scan_tree(Cold& s, Tree& tr, int max_code) {
   uint16_t* dl = tr.dl;
   uint16_t* bfc = s.b.fc;
   int prevlen = -1, curlen, nextlen = dl[0], count = 0, max_count = 7, min_count = 4;
@@ -379,11 +394,11 @@ DFL_HD inline void scan_tree(State& s, Tree& tr, int max_code) {
   }
 }
 
-DFL_HD inline void send_code(State& s, int c, const uint16_t* codes, const uint16_t* lens) {
+DFL_HD inline void send_code(Cold& s, int c, const uint16_t* codes, const uint16_t* lens) {
   s.out.bits(codes[c], lens[c]);
 }
 
-DFL_HD inline void send_tree(State& s, Tree& tr, int max_code) {
+DFL_HD inline void send_tree(Cold& s, Tree& tr, int max_code) {
   uint16_t* dl = tr.dl;
   int prevlen = -1, curlen, nextlen = dl[0], count = 0, max_count = 7, min_count = 4;
   if (nextlen == 0) max_count = 138, min_count = 3;
@@ -422,7 +437,7 @@ DFL_HD inline int d_code(const Tables* t, unsigned dist) {
 }
 
 template <typename CodeT, typename LenT>
-DFL_HD inline void compress_block(State& s, const CodeT* lcode, const LenT* llen, const CodeT* dcode,
+DFL_HD inline void compress_block(Cold& s, const CodeT* lcode, const LenT* llen, const CodeT* dcode,
                                   const LenT* dlen) {
   const Tables* t = s.t;
   unsigned lx = 0;
@@ -447,7 +462,7 @@ DFL_HD inline void compress_block(State& s, const CodeT* lcode, const LenT* llen
 }
 
 // _tr_flush_block (trees.c), level > 0
-DFL_HD DFL_NOINLINE void flush_block(State& s, bool has_buf, uint32_t buf_start, uint32_t stored_len, int last) {
+DFL_HD DFL_NOINLINE void flush_block(Cold& s, bool has_buf, uint32_t buf_start, uint32_t stored_len, int last) {
   build_tree(s, s.l);
   build_tree(s, s.d);
   // build_bl_tree
@@ -515,7 +530,7 @@ DFL_HD inline uint32_t longest_match(State& s, uint32_t cur_match) {
   if (s.prev_length >= s.cfg.good) chain_length >>= 2;
   if ((uint32_t)nice_match > s.lookahead) nice_match = (int)s.lookahead;
   const uint8_t s0 = s.win(scan), s1 = s.win(scan + 1);
-  const bool fast = !s.slid && scan + kMaxMatch + 1 <= s.len;
+  const bool fast = !s.w.slid && scan + kMaxMatch + 1 <= s.w.len;
   do {
     const uint32_t match = cur_match;
     if (s.win(match + best_len) != scan_end || s.win(match + best_len - 1) != scan_end1 || s.win(match) != s0 ||
@@ -524,8 +539,8 @@ DFL_HD inline uint32_t longest_match(State& s, uint32_t cur_match) {
     // scan[2] == match[2] is assumed (equal hash, HASH_BITS >= 8)
     int len = 3;
     if (fast) {  // bytes 3..258 of both strings inside the payload, no remap
-      const uint8_t* ps = s.in + scan;
-      const uint8_t* pm = s.in + match;
+      const uint8_t* ps = s.w.in + scan;
+      const uint8_t* pm = s.w.in + match;
       for (;;) {
         const uint64_t x = ld8(ps + len) ^ ld8(pm + len);
         if (x) {
@@ -554,21 +569,24 @@ DFL_HD inline uint32_t longest_match(State& s, uint32_t cur_match) {
 DFL_HD inline bool tally_lit(State& s, uint8_t c) {
   s.a->d_buf[s.last_lit] = 0;
   s.a->l_buf[s.last_lit++] = c;
-  s.l.fc[c]++;
+  s.a->lfc[c]++;
   return s.last_lit == kLitBufSize - 1;
 }
 DFL_HD inline bool tally_dist(State& s, unsigned dist, unsigned len) {
   s.a->d_buf[s.last_lit] = (uint16_t)dist;
   s.a->l_buf[s.last_lit++] = (uint8_t)len;
   dist--;
-  s.l.fc[s.t->length_code[len] + kLiterals + 1]++;
-  s.d.fc[d_code(s.t, dist)]++;
+  s.a->lfc[s.t->length_code[len] + kLiterals + 1]++;
+  s.a->dfc[d_code(s.t, dist)]++;
   return s.last_lit == kLitBufSize - 1;
 }
 
 DFL_HD inline void flush(State& s, int last) {
   const bool has = s.block_start >= 0;
-  flush_block(s, has, has ? (uint32_t)s.block_start : 0, (uint32_t)((int32_t)s.strstart - s.block_start), last);
+  s.c->w = s.w;
+  s.c->last_lit = s.last_lit;
+  s.last_lit = 0;
+  flush_block(*s.c, has, has ? (uint32_t)s.block_start : 0, (uint32_t)((int32_t)s.strstart - s.block_start), last);
   s.block_start = (int32_t)s.strstart;
 }
 
@@ -587,7 +605,7 @@ DFL_HD inline void slide_words(uint64_t* w, int nwords) {
 // fill_window after the first read: only the slide can happen
 DFL_HD inline void fill_window(State& s) {
   if (s.strstart >= (uint32_t)(kWSize + kMaxDist)) {
-    s.slid = true;  // [wsize, len) moved to [0, len - wsize)
+    s.w.slid = true;  // [wsize, len) moved to [0, len - wsize)
     s.match_start -= kWSize;
     s.strstart -= kWSize;
     s.block_start -= kWSize;
@@ -602,17 +620,22 @@ DFL_HD inline void fill_window(State& s) {
 DFL_HD inline uint32_t deflate_block(Arena* a, const Tables* t, int level, const uint8_t* in, uint32_t len,
                                      uint8_t* out, uint32_t cap, bool* overflow, bool head_cleared = false) {
   State s;
-  s.in = in;
-  s.len = len;
-  s.slid = false;
-  s.copied = len > (uint32_t)kWSize ? len - kWSize : 0;
+  Cold c;
+  s.w.in = in;
+  s.w.len = len;
+  s.w.slid = false;
+  s.w.copied = len > (uint32_t)kWSize ? len - kWSize : 0;
   s.a = a;
   s.t = t;
+  s.c = &c;
   s.cfg = level_config(level);
-  s.l = Tree{a->lfc, a->ldl, t->sl_len, 0, kLCodes, kMaxBits, kLiterals + 1, 0};
-  s.d = Tree{a->dfc, a->ddl, t->sd_len, 1, kDCodes, kMaxBits, 0, 0};
-  s.b = Tree{a->bfc, a->bdl, nullptr, 2, kBlCodes, kMaxBlBits, 0, 0};
-  s.out = Out{out, cap, 0, 0, 0, false};
+  c.a = a;
+  c.t = t;
+  c.w = s.w;
+  c.l = Tree{a->lfc, a->ldl, t->sl_len, 0, kLCodes, kMaxBits, kLiterals + 1, 0};
+  c.d = Tree{a->dfc, a->ddl, t->sd_len, 1, kDCodes, kMaxBits, 0, 0};
+  c.b = Tree{a->bfc, a->bdl, nullptr, 2, kBlCodes, kMaxBlBits, 0, 0};
+  c.out = Out{out, cap, 0, 0, 0, false};
   // lm_init: CLEAR_HASH (prev is not cleared by zlib; stale entries are never reached)
   if (!head_cleared)
     for (int n = 0; n < kHashSize; ++n) a->head[n] = 0;
@@ -624,7 +647,8 @@ DFL_HD inline uint32_t deflate_block(Arena* a, const Tables* t, int level, const
   s.match_start = 0;
   s.prev_match = 0;
   s.ins_h = 0;
-  init_block(s);
+  s.last_lit = 0;
+  init_block(c);
   // first fill_window: the whole payload is read
   s.lookahead = len;
   if (s.lookahead >= (uint32_t)kMinMatch) {
@@ -674,8 +698,8 @@ DFL_HD inline uint32_t deflate_block(Arena* a, const Tables* t, int level, const
     s.match_available = 0;
   }
   flush(s, 1);
-  *overflow = s.out.overflow || s.out.n >= cap;
-  return s.out.n;
+  *overflow = c.out.overflow || c.out.n >= cap;
+  return c.out.n;
 }
 
 }  // namespace dfl

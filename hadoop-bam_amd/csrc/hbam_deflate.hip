@@ -33,7 +33,7 @@ namespace {
 constexpr uint32_t kSlot = 65536;      // cdata slot per block
 constexpr uint32_t kMaxLanes = 65536;  // concurrent arenas (~184 KiB each)
 constexpr uint32_t kCrcPoly = 0xedb88320u;
-constexpr uint32_t kWavesTarget = 8192;  // 8 waves per SIMD (57 VGPRs: occupancy 8)
+constexpr uint32_t kWavesTarget = 5120;  // 5 waves per SIMD (84 VGPRs: occupancy 5; measured best)
 
 __device__ inline uint32_t crc_mul(uint32_t a, uint32_t b) {
   uint32_t m = 1u << 31, p = 0;
