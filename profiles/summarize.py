@@ -38,7 +38,7 @@ def _col(row, *cands):
 
 
 def short(name):
-    n = name.split("(")[0]
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     if "rocprim" in n:
         return "rocprim:" + ("scan" if "scan" in name else "sort" if "sort" in name else "other")
     return n.replace("void ", "").strip()
