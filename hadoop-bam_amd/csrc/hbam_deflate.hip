@@ -96,10 +96,21 @@ __global__ __launch_bounds__(256) void k_dfl_crc(const uint8_t* __restrict__ in,
     tab[threadIdx.x] = c;
   }
   __syncthreads();
-  const uint32_t slice = (len + 255) / 256;
+  // 8-byte slices per thread, read as whole words (byte loads strided by the
+  // slice length re-fetched each line ~48x)
+  const uint32_t slice = ((len + 255) / 256 + 7) & ~7u;
   const uint32_t s0 = min(len, threadIdx.x * slice), s1 = min(len, s0 + slice);
   uint32_t r = 0;
-  for (uint32_t i = s0; i < s1; ++i) r = tab[(r ^ p[i]) & 0xff] ^ (r >> 8);
+  uint32_t i = s0;
+  for (; i + 8 <= s1; i += 8) {
+    uint64_t v = dfl::ld8(p + i);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      r = tab[(r ^ (uint32_t)v) & 0xff] ^ (r >> 8);
+      v >>= 8;
+    }
+  }
+  for (; i < s1; ++i) r = tab[(r ^ p[i]) & 0xff] ^ (r >> 8);
   part[threadIdx.x] = r;
   __syncthreads();
   if (threadIdx.x == 0) {
