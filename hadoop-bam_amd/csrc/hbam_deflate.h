@@ -531,8 +531,12 @@ DFL_HD inline uint32_t longest_match(State& s, uint32_t cur_match) {
   if ((uint32_t)nice_match > s.lookahead) nice_match = (int)s.lookahead;
   const uint8_t s0 = s.win(scan), s1 = s.win(scan + 1);
   const bool fast = !s.w.slid && scan + kMaxMatch + 1 <= s.w.len;
+  uint32_t next;
   do {
     const uint32_t match = cur_match;
+    // the next chain link does not depend on this candidate: load it first so
+    // its miss overlaps the candidate's window reads
+    next = s.a->prev[cur_match & kWMask];
     if (s.win(match + best_len) != scan_end || s.win(match + best_len - 1) != scan_end1 || s.win(match) != s0 ||
         s.win(match + 1) != s1)
       continue;
@@ -561,7 +565,7 @@ DFL_HD inline uint32_t longest_match(State& s, uint32_t cur_match) {
       scan_end1 = s.win(scan + best_len - 1);
       scan_end = s.win(scan + best_len);
     }
-  } while ((cur_match = s.a->prev[cur_match & kWMask]) > limit && --chain_length != 0);
+  } while ((cur_match = next) > limit && --chain_length != 0);
   if ((uint32_t)best_len <= s.lookahead) return (uint32_t)best_len;
   return s.lookahead;
 }
