@@ -537,9 +537,14 @@ DFL_HD inline uint32_t longest_match(State& s, uint32_t cur_match) {
     // the next chain link does not depend on this candidate: load it first so
     // its miss overlaps the candidate's window reads
     next = s.a->prev[cur_match & kWMask];
-    if (s.win(match + best_len) != scan_end || s.win(match + best_len - 1) != scan_end1 || s.win(match) != s0 ||
-        s.win(match + 1) != s1)
+    if (fast) {  // all four bytes in the payload: issue the loads together
+      const uint8_t* pm = s.w.in + match;
+      const uint32_t m0 = pm[best_len], m1 = pm[best_len - 1], m2 = pm[0], m3 = pm[1];
+      if ((m0 ^ scan_end) | (m1 ^ scan_end1) | (m2 ^ s0) | (m3 ^ s1)) continue;
+    } else if (s.win(match + best_len) != scan_end || s.win(match + best_len - 1) != scan_end1 ||
+               s.win(match) != s0 || s.win(match + 1) != s1) {
       continue;
+    }
     // scan[2] == match[2] is assumed (equal hash, HASH_BITS >= 8)
     int len = 3;
     if (fast) {  // bytes 3..258 of both strings inside the payload, no remap
