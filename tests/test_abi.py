@@ -48,3 +48,17 @@ def test_no_gpu_fails_loudly(test_bam):
     assert e.value.code == hbam.E_DEVICE
     with pytest.raises(hbam.HbamError):
         hbam.Gpu(0)
+    # the BGZF write path has no CPU path either
+    with pytest.raises(hbam.HbamError) as e:
+        hbam.bgzf_compress(b"ACGT" * 1000)
+    assert e.value.code == hbam.E_DEVICE
+
+
+def test_bgzf_compress_argument_errors():
+    # checked before any device work: block_lens must cover the payload, block_size 1..65536
+    with pytest.raises(hbam.HbamError) as e:
+        hbam.bgzf_compress(b"ACGT" * 10, block_lens=[39])
+    assert e.value.code == hbam.E_ARG
+    with pytest.raises(hbam.HbamError) as e:
+        hbam.bgzf_compress(b"ACGT" * 10, block_size=65537)
+    assert e.value.code == hbam.E_ARG
