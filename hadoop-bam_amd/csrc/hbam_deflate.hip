@@ -77,7 +77,7 @@ __global__ __launch_bounds__(64) void k_deflate_blocks(const uint8_t* __restrict
   const uint4 z = make_uint4(0, 0, 0, 0);
   for (int k = 0; k < (int)(sizeof(a->head) / 16); ++k) h[k] = z;
   bool o = false;
-  const uint32_t n = dfl::deflate_block(a, tables, level, in + ustart[b], lens[b], slots + (uint64_t)b * kSlot,
+  const uint32_t n = dfl::deflate_block(a, tables, level, in + ustart[b], lens[b], slots + (uint64_t)i * kSlot,
                                         dfl::kOutCap, &o, true);
   csize[b] = n;
   ovf[b] = o ? 1 : 0;
@@ -131,8 +131,8 @@ __global__ __launch_bounds__(256) void k_dfl_frame(const uint8_t* __restrict__ i
                                                    const uint8_t* __restrict__ slots,
                                                    const uint32_t* __restrict__ csize, const uint8_t* __restrict__ ovf,
                                                    const uint32_t* __restrict__ crc, const uint64_t* __restrict__ offs,
-                                                   uint8_t* __restrict__ out) {
-  const uint32_t b = blockIdx.x;
+                                                   uint8_t* __restrict__ out, uint32_t b0) {
+  const uint32_t b = b0 + blockIdx.x;  // slots hold the current batch only
   const uint32_t len = lens[b];
   const bool stored = ovf[b] != 0;
   const uint32_t cn = stored ? len + 5 : csize[b];
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void k_dfl_frame(const uint8_t* __restrict__ i
   }
   uint8_t* c = o + 18;
   if (!stored) {
-    const uint8_t* s = slots + (uint64_t)b * kSlot;
+    const uint8_t* s = slots + (uint64_t)blockIdx.x * kSlot;
     for (uint32_t i = threadIdx.x; i < cn; i += 256) c[i] = s[i];
   } else {  // Deflater(NO_COMPRESSION): one final stored block
     if (threadIdx.x == 0) {
@@ -216,67 +216,80 @@ int BgzfCompressor::compress(const uint8_t* d_in, const std::vector<uint64_t>& u
     DCHK(hipMalloc(reinterpret_cast<void**>(&tables_), sizeof t));
     DCHK(hipMemcpy(tables_, &t, sizeof t, hipMemcpyHostToDevice));
   }
-  const uint32_t lanes = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(nb, 1), kMaxLanes);
+  // Blocks go through in batches of up to kMaxLanes: deflate (a lane and an
+  // arena per block, cdata into the batch's slots), sizes to the host, file
+  // offsets continued from the previous batch, framing.  Memory is bounded by
+  // one batch's arenas + slots whatever the stream length; the output is
+  // sized for the worst case: a compressed block is never larger than its
+  // stored form (len + 5 B per DEFLATE block, <= 5 blocks of 16,383 symbols),
+  // the fallback is len + 5, plus 26 B of framing.
+  const char* ml = getenv("HBAM_DFL_MAX_LANES");  // test knob: force several batches
+  const uint64_t max_lanes = ml ? (uint64_t)std::max(1, atoi(ml)) : kMaxLanes;
+  const uint32_t lanes = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(nb, 1), max_lanes);
+  uint64_t worst = eof ? 28 : 0;
+  for (uint32_t l : lens) worst += (uint64_t)l + 26 + 64;
   DCHK(grow_buf(&arenas_, &arenas_n_, (size_t)lanes * sizeof(dfl::Arena)));
-  DCHK(grow_buf(&slots_, &slots_n_, std::max<uint64_t>(nb, 1) * kSlot));
+  DCHK(grow_buf(&slots_, &slots_n_, (size_t)lanes * kSlot));
   DCHK(grow_buf(&csize_, &csize_n_, std::max<uint64_t>(nb, 1) * 4));
   DCHK(grow_buf(&ovf_, &ovf_n_, std::max<uint64_t>(nb, 1)));
   DCHK(grow_buf(&crc_, &crc_n_, std::max<uint64_t>(nb, 1) * 4));
   DCHK(grow_buf(&offs_, &offs_n_, (nb + 1) * 8));
   DCHK(grow_buf(&ustart_, &ustart_n_, std::max<uint64_t>(nb, 1) * 8));
   DCHK(grow_buf(&lens_, &lens_n_, std::max<uint64_t>(nb, 1) * 4));
+  DCHK(grow_buf(&out_, &out_n_, worst + 16));
   hipEvent_t e0, e1;
   DCHK(hipEventCreate(&e0));
   DCHK(hipEventCreate(&e1));
   DCHK(hipEventRecord(e0, s));
+  std::vector<uint32_t> cs(nb);
+  std::vector<uint8_t> ov(nb);
+  std::vector<uint64_t> offs(nb + 1);
+  uint64_t o = 0;
   if (nb) {
     DCHK(hipMemcpyAsync(ustart_, ustart.data(), nb * 8, hipMemcpyHostToDevice, s));
     DCHK(hipMemcpyAsync(lens_, lens.data(), nb * 4, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_dfl_crc, dim3((uint32_t)nb), dim3(256), 0, s, d_in, ustart_, lens_, crc_);
+    DCHK(hipGetLastError());
+    static const uint32_t waves = [] {
+      const char* e = getenv("HBAM_DFL_WAVES");  // experiment knob
+      return e ? (uint32_t)std::max(1, atoi(e)) : kWavesTarget;
+    }();
     for (uint64_t b0 = 0; b0 < nb; b0 += lanes) {
       const uint32_t n = (uint32_t)std::min<uint64_t>(lanes, nb - b0);
       // about kWavesTarget waves in flight over 256 CUs x 4 SIMDs
-      static const uint32_t waves = [] {
-        const char* e = getenv("HBAM_DFL_WAVES");  // experiment knob
-        return e ? (uint32_t)std::max(1, atoi(e)) : kWavesTarget;
-      }();
       const uint32_t lpw = std::max<uint32_t>(1, std::min<uint32_t>(64, (n + waves - 1) / waves));
       hipLaunchKernelGGL(k_deflate_blocks, dim3((n + lpw - 1) / lpw), dim3(64), 0, s, d_in, ustart_, lens_,
                          (uint32_t)b0, n, level, tables_, arenas_, slots_, csize_, ovf_, lpw);
       DCHK(hipGetLastError());
+      DCHK(hipMemcpyAsync(cs.data() + b0, csize_ + b0, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+      DCHK(hipMemcpyAsync(ov.data() + b0, ovf_ + b0, n, hipMemcpyDeviceToHost, s));
+      DCHK(hipStreamSynchronize(s));
+      for (uint64_t b = b0; b < b0 + n; ++b) {
+        offs[b] = o;
+        if (ov[b] && lens[b] + 5 > dfl::kOutCap) {
+          err_ = "incompressible BGZF payload does not fit one stored block";
+          (void)hipEventDestroy(e0);
+          (void)hipEventDestroy(e1);
+          return kFormatErr;
+        }
+        o += 26 + (ov[b] ? lens[b] + 5 : cs[b]);
+      }
+      if (o + (eof ? 28 : 0) > worst) {  // cannot happen (see the bound above); never write past out_
+        err_ = "BGZF output bound exceeded";
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        return kFormatErr;
+      }
+      DCHK(hipMemcpyAsync(offs_ + b0, offs.data() + b0, (size_t)n * 8, hipMemcpyHostToDevice, s));
+      hipLaunchKernelGGL(k_dfl_frame, dim3(n), dim3(256), 0, s, d_in, ustart_, lens_, slots_, csize_, ovf_, crc_,
+                         offs_, out_, (uint32_t)b0);
+      DCHK(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_dfl_crc, dim3((uint32_t)nb), dim3(256), 0, s, d_in, ustart_, lens_, crc_);
-    DCHK(hipGetLastError());
-  }
-  std::vector<uint32_t> cs(nb);
-  std::vector<uint8_t> ov(nb);
-  if (nb) {
-    DCHK(hipMemcpyAsync(cs.data(), csize_, nb * 4, hipMemcpyDeviceToHost, s));
-    DCHK(hipMemcpyAsync(ov.data(), ovf_, nb, hipMemcpyDeviceToHost, s));
-  }
-  DCHK(hipStreamSynchronize(s));
-  std::vector<uint64_t> offs(nb + 1);
-  uint64_t o = 0;
-  for (uint64_t b = 0; b < nb; ++b) {
-    offs[b] = o;
-    if (ov[b] && lens[b] + 5 > dfl::kOutCap) {
-      err_ = "incompressible BGZF payload does not fit one stored block";
-      (void)hipEventDestroy(e0);
-      (void)hipEventDestroy(e1);
-      return kFormatErr;
-    }
-    o += 26 + (ov[b] ? lens[b] + 5 : cs[b]);
   }
   offs[nb] = o;
   static const uint8_t kEof[28] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43,
                                    2,    0,    0x1b, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   out_len_ = o + (eof ? 28 : 0);
-  DCHK(grow_buf(&out_, &out_n_, out_len_ + 16));
-  if (nb) {
-    DCHK(hipMemcpyAsync(offs_, offs.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_dfl_frame, dim3((uint32_t)nb), dim3(256), 0, s, d_in, ustart_, lens_, slots_, csize_, ovf_,
-                       crc_, offs_, out_);
-    DCHK(hipGetLastError());
-  }
   if (eof) DCHK(hipMemcpyAsync(out_ + o, kEof, 28, hipMemcpyHostToDevice, s));
   DCHK(hipEventRecord(e1, s));
   DCHK(hipEventSynchronize(e1));

@@ -136,3 +136,14 @@ def test_gpu_recompress_synthetic_bam_full_roundtrip():
         assert n == data.nbytes and np.array_equal(got, data)
     finally:
         g.close()
+
+
+@pytest.mark.gpu
+def test_gpu_multi_batch_framing(monkeypatch):
+    """More blocks than one batch of arenas: offsets continue across batches."""
+    import hbam
+    d = _cases()["acgt"] + _cases()["bam"]
+    lens = [min(4097, len(d) - p) for p in range(0, len(d), 4097)]
+    want = orc.bgzf_compress(d, lens, level=5, eof=True)
+    monkeypatch.setenv("HBAM_DFL_MAX_LANES", "37")
+    assert hbam.bgzf_compress(d, block_lens=lens, level=5, eof=True) == want
