@@ -1,5 +1,5 @@
 // hbam_deflate.h -- raw DEFLATE of one BGZF block payload, restating zlib
-// 1.2.11's deflate_slow / trees.c (levels 4-9; zlib is what
+// 1.2.11's deflate_fast / deflate_slow / trees.c (levels 1-9; zlib is what
 // java.util.zip.Deflater wraps) so that the output is byte-identical to
 // [htsjdk] BlockCompressedOutputStream.deflateBlock: one Deflater(level,
 // nowrap=true), reset() per block, setInput + finish + deflate(buf, 0, 65518).
@@ -50,9 +50,12 @@ constexpr uint32_t kOutCap = 65536 - 18;  // htsjdk compressedBuffer (MAX_COMPRE
 struct Config {
   uint16_t good, lazy, nice, chain;
 };
-// deflate.c configuration_table, levels 4..9 (deflate_slow)
+// deflate.c configuration_table: levels 1..3 run deflate_fast, 4..9 deflate_slow
 DFL_HD inline Config level_config(int level) {
   switch (level) {
+    case 1: return {4, 4, 8, 4};
+    case 2: return {4, 5, 16, 8};
+    case 3: return {4, 6, 32, 32};
     case 4: return {4, 4, 16, 16};
     case 5: return {8, 16, 32, 32};
     case 6: return {8, 16, 128, 128};
@@ -663,6 +666,44 @@ DFL_HD inline uint32_t deflate_block(Arena* a, const Tables* t, int level, const
   if (s.lookahead >= (uint32_t)kMinMatch) {
     s.ins_h = s.win(0);
     s.ins_h = ((s.ins_h << kHashShift) ^ s.win(1)) & kHashMask;
+  }
+  if (level <= 3) {
+    // deflate_fast: no lazy evaluation; max_insert_length = max_lazy
+    for (;;) {
+      if (s.lookahead < (uint32_t)kMinLookahead) {
+        fill_window(s);
+        if (s.lookahead == 0) break;
+      }
+      uint32_t hash_head = 0;
+      if (s.lookahead >= (uint32_t)kMinMatch) insert_string(s, s.strstart, &hash_head);
+      if (hash_head != 0 && s.strstart - hash_head <= (uint32_t)kMaxDist) s.match_length = longest_match(s, hash_head);
+      bool bflush;
+      if (s.match_length >= (uint32_t)kMinMatch) {
+        bflush = tally_dist(s, s.strstart - s.match_start, s.match_length - kMinMatch);
+        s.lookahead -= s.match_length;
+        if (s.match_length <= s.cfg.lazy && s.lookahead >= (uint32_t)kMinMatch) {
+          s.match_length--;
+          do {
+            s.strstart++;
+            insert_string(s, s.strstart, &hash_head);
+          } while (--s.match_length != 0);
+          s.strstart++;
+        } else {
+          s.strstart += s.match_length;
+          s.match_length = 0;
+          s.ins_h = s.win(s.strstart);
+          s.ins_h = ((s.ins_h << kHashShift) ^ s.win(s.strstart + 1)) & kHashMask;
+        }
+      } else {
+        bflush = tally_lit(s, s.win(s.strstart));
+        s.lookahead--;
+        s.strstart++;
+      }
+      if (bflush) flush(s, 0);
+    }
+    flush(s, 1);
+    *overflow = c.out.overflow || c.out.n >= cap;
+    return c.out.n;
   }
   // deflate_slow
   for (;;) {

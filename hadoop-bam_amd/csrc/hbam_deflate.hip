@@ -3,8 +3,8 @@
 // of a payload stream at once (the compressor behind BAMRecordWriter /
 // KeyIgnoringBAMRecordWriter output, BAMRecordWriter.java:131-149).
 //
-//   k_deflate_blocks  one lane per BGZF block: zlib 1.2.11 deflate_slow +
-//                     trees.c restated in hbam_deflate.h (byte-identical
+//   k_deflate_blocks  one lane per BGZF block: zlib 1.2.11 deflate_fast
+//                     (levels 1-3) / deflate_slow (4-9) + trees.c restated in hbam_deflate.h (byte-identical
 //                     output), hash chains / symbol buffer / trees in a
 //                     per-lane arena in HBM, cdata into a 64 KiB slot.
 //   k_dfl_crc         one workgroup per block: CRC-32 of the payload
@@ -77,6 +77,11 @@ __global__ __launch_bounds__(64) void k_deflate_blocks(const uint8_t* __restrict
   const uint4 z = make_uint4(0, 0, 0, 0);
   for (int k = 0; k < (int)(sizeof(a->head) / 16); ++k) h[k] = z;
   bool o = false;
+  if (level == 0) {  // Deflater(NO_COMPRESSION): one stored block, written by k_dfl_frame
+    csize[b] = 0;
+    ovf[b] = 1;
+    return;
+  }
   const uint32_t n = dfl::deflate_block(a, tables, level, in + ustart[b], lens[b], slots + (uint64_t)i * kSlot,
                                         dfl::kOutCap, &o, true);
   csize[b] = n;
@@ -199,8 +204,8 @@ static hipError_t grow_buf(T** p, size_t* have, size_t need) {
 int BgzfCompressor::compress(const uint8_t* d_in, const std::vector<uint64_t>& ustart,
                              const std::vector<uint32_t>& lens, int level, bool eof, hipStream_t s, float* ms) {
   const int kDeviceErr = 5, kArgErr = 3, kFormatErr = 1;
-  if (level < 4 || level > 9) {
-    err_ = "level must be 4..9 (deflate_slow levels; htsjdk default 5)";
+  if (level < 0 || level > 9) {
+    err_ = "level must be 0..9 (htsjdk default 5)";
     return kArgErr;
   }
   const uint64_t nb = lens.size();

@@ -135,7 +135,7 @@ int main(int argc, char** argv) {
       sz.push_back(l);
       tot += l;
     }
-    for (int level : {5, 9}) {
+    for (int level : {1, 5, 9}) {
       bad += run_case("ac-sliders", ab, sz, level, false);
       bad += run_case("ac-sliders", ab, sz, level, true);
     }
@@ -153,12 +153,12 @@ int main(int argc, char** argv) {
     uint64_t tot = 0;
     for (uint32_t v : rag) tot += v;
     if (d.size() >= tot) {
-      for (int level : {4, 5, 6, 9}) {
+      for (int level : {1, 3, 4, 5, 6, 9}) {
         bad += run_case((in.first + "/ragged").c_str(), d, rag, level, false);
         bad += run_case((in.first + "/ragged").c_str(), d, rag, level, true);
       }
     }
-    for (int level : {4, 6, 7, 8, 9}) bad += run_case(in.first.c_str(), d, cut(d.size() < 400000 ? d.size() : 400000, 65498), level, false);
+    for (int level : {1, 2, 3, 4, 6, 7, 8, 9}) bad += run_case(in.first.c_str(), d, cut(d.size() < 400000 ? d.size() : 400000, 65498), level, false);
   }
   printf(bad ? "FAILED (%d)\n" : "ALL OK\n", bad);
   return bad ? 1 : 0;

@@ -162,7 +162,7 @@ int hbam_open_codec(const hbam_opts *opts, hbam_ctx **out);
  * (the compressor BAMRecordWriter.java:131-149 writes through) for a whole
  * payload stream, every block DEFLATEd on the GPU in one launch: one
  * java.util.zip.Deflater(level, nowrap) reset per block, output
- * byte-identical to zlib 1.2.11 (levels 4..9; htsjdk's default is 5); a block
+ * byte-identical to zlib 1.2.11 (levels 0..9; htsjdk's default is 5); a block
  * that does not fit the 65518-byte compressed buffer is written by the
  * NO_COMPRESSION fallback (one stored block).  Blocks: block_lens[0..n_blocks)
  * (each <= 65536, as BlockCompressedOutputStream.flush cuts them), or when
