@@ -3,9 +3,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
-#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -13,28 +13,36 @@
 
 #include "hbam_deflate_api.h"
 #include "hbam_host.h"
+#include "hbam_launch.h"
 
 using hadoop_bam::BAMInputFormat;
 using hadoop_bam::BamFile;
 using hadoop_bam::BAMRecordReader;
+using hadoop_bam::Carry;
 using hadoop_bam::FileSplit;
 using hadoop_bam::FileVirtualSplit;
+using hadoop_bam::HostBatch;
+using hadoop_bam::OpenOptions;
+using hadoop_bam::SpanCursor;
 using hadoop_bam::SplittingBAMIndexer;
+using hadoop_bam::Step;
 
 struct hbam_ctx {
   std::unique_ptr<BamFile> f;
   std::unique_ptr<hbam::Pipeline> codec;  // hbam_open_codec: a pipeline with no file
   std::string err;
-  BAMRecordReader::Host batch;
-  hbam::SpanDev span;  // device result of the last hbam_decode_span (valid until the next call)
-  std::string text;
+  SpanCursor cursor;
+  HostBatch batch;
+  hbam::SpanDev wspan;  // device result of the last hbam_decode_writables
+  bool last_is_writables = false;
 };
 
 struct hbam_gpu {
-  std::unique_ptr<hbam::Pipeline> p;
+  std::unique_ptr<BamFile> f;
+  int device = 0;
+  uint64_t window = hadoop_bam::kDefaultWindowBytes;
   std::string err;
-  uint64_t first_pos = 0;  // inflated-stream position of the first record
-  hbam::SpanDev span;
+  hbam::SpanDev span;  // last window of the last run
   hbam::DevBuf<uint8_t> enc;  // hbam_gpu_encode_writables output
   uint64_t enc_bytes = 0;
   std::unique_ptr<hbam::BgzfCompressor> bgzf;  // hbam_gpu_bgzf_compress
@@ -43,40 +51,130 @@ struct hbam_gpu {
 namespace {
 std::string g_open_err;
 
-int open_common(const void* data, uint64_t len, const hbam_opts* opts, bool header, hbam_ctx** out) {
-  *out = nullptr;
+OpenOptions options_of(const hbam_opts* opts, bool header) {
   hbam_opts o{};
   if (opts) o = *opts;
+  OpenOptions r;
+  r.device = o.device;
+  r.check_crc = o.check_crc != 0;
+  r.stringency = o.stringency;
+  r.window_bytes = o.window_bytes;
+  r.parse_header = header;
+  return r;
+}
+
+int finish_open(int rc, std::unique_ptr<BamFile>&& f, const std::string& err, hbam_ctx** out) {
   auto* c = new hbam_ctx();
-  std::string err;
-  int rc = BamFile::open(static_cast<const uint8_t*>(data), len, o.device, header, o.check_crc != 0, &c->f, &err);
+  *out = c;  // on failure the caller may read hbam_last_error, then must hbam_close
   if (rc != HBAM_OK) {
     g_open_err = err;
     c->err = err;
-    *out = c;  // caller may read hbam_last_error, then must hbam_close
     return rc;
   }
-  *out = c;
+  c->f = std::move(f);
   return HBAM_OK;
 }
 
-bool read_file(const char* path, std::vector<uint8_t>* buf, std::string* err) {
-  FILE* fp = fopen(path, "rb");
-  if (!fp) {
-    *err = std::string("cannot open ") + path;
-    return false;
+bool valid_stringency(const hbam_opts* o) { return !o || (o->stringency >= 0 && o->stringency <= 2); }
+
+void fill_batch(const HostBatch& h, hbam_batch* out) {
+  out->n = h.n;
+  out->ref_id = h.ref_id.data();
+  out->pos = h.pos.data();
+  out->l_seq = h.l_seq.data();
+  out->next_ref_id = h.next_ref_id.data();
+  out->next_pos = h.next_pos.data();
+  out->tlen = h.tlen.data();
+  out->l_read_name = h.l_read_name.data();
+  out->mapq = h.mapq.data();
+  out->bin = h.bin.data();
+  out->n_cigar = h.n_cigar.data();
+  out->flag = h.flag.data();
+  out->key = h.key.data();
+  out->voff = h.voff.data();
+  out->rest_off = h.rest_off.data();
+  out->rest_len = h.rest_len.data();
+  out->data = h.data.data();
+  out->data_len = h.data_len;
+}
+
+// The decode of FileVirtualSplit [vstart, vend) window by window with the
+// records left in HBM; stats accumulate over windows.  *last = the last
+// window's span (C2-sized files: the whole split).
+int decode_device(BamFile& f, uint64_t vstart, uint64_t vend, int32_t flags, hbam_gpu_stats* st,
+                  hbam::SpanDev* last, std::string* err) {
+  memset(st, 0, sizeof *st);
+  hbam::Pipeline& p = f.pipe();
+  p.timing = (flags & 1) != 0;
+  const bool decode = (flags & 2) == 0, digest = (flags & 4) != 0;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, p.stream());
+  const uint64_t lf0 = p.link_fallbacks(), il0 = p.inflate_launches(), lr0 = p.link_rewalks();
+  f.invalidate_window();  // a timed pass locates and inflates afresh
+  Carry c{vstart >> 16, vstart & 0xffff};
+  bool cont = false;
+  int rc = HBAM_OK;
+  bool first = true;
+  for (;;) {
+    Step step;
+    rc = f.decode_step(c, vend, hbam::kReader, decode, cont, &step);
+    if (rc != HBAM_OK) {
+      *err = f.error();
+      break;
+    }
+    const hbam::SpanDev& s = step.span;
+    st->windows += 1;
+    st->records += s.n;
+    st->n_blocks += p.blocks().size();
+    st->compressed_bytes += p.window_end() - p.base();
+    st->inflated_bytes += p.total_u();
+    if (p.timing) {
+      st->ms_locate += p.times.locate;
+      st->ms_inflate += p.times.inflate;
+      st->ms_huff += p.times.huff;
+      st->ms_lz77 += p.times.lz77;
+      st->ms_chain += p.times.chain;
+      st->ms_decode += p.times.decode;
+    }
+    if (s.n) {
+      if (first) (void)hipMemcpy(&st->first_voff, s.rec_voff, 8, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(&st->last_voff, s.rec_voff + s.n - 1, 8, hipMemcpyDeviceToHost);
+      first = false;
+      if (digest) {
+        uint64_t kx = 0, vs = 0;
+        hbam::SpanDev d = s;
+        if (!decode) d.col.key = nullptr;
+        rc = p.span_digest(d, &kx, &vs);
+        if (rc != HBAM_OK) {
+          *err = p.error();
+          break;
+        }
+        st->key_xor ^= kx;
+        st->voff_sum += vs;
+      }
+    }
+    if (last) *last = s;
+    if (step.status != HBAM_OK) {
+      st->status = step.status;
+      *err = step.error;
+      break;
+    }
+    if (step.ended) break;
+    c = step.next;
+    cont = true;
   }
-  fseek(fp, 0, SEEK_END);
-  long n = ftell(fp);
-  fseek(fp, 0, SEEK_SET);
-  buf->resize(n > 0 ? (size_t)n : 0);
-  size_t got = n > 0 ? fread(buf->data(), 1, (size_t)n, fp) : 0;
-  fclose(fp);
-  if ((long)got != n) {
-    *err = std::string("short read on ") + path;
-    return false;
-  }
-  return true;
+  (void)hipEventRecord(e1, p.stream());
+  (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&st->ms_total, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  st->link_fallbacks = (int32_t)(p.link_fallbacks() - lf0);
+  st->inflate_launches = (int32_t)(p.inflate_launches() - il0);
+  st->link_rewalks = (int32_t)(p.link_rewalks() - lr0);
+  if (rc != HBAM_OK) st->status = rc;
+  return rc != HBAM_OK ? rc : st->status;
 }
 }  // namespace
 
@@ -85,22 +183,26 @@ extern "C" {
 int32_t hbam_abi_version(void) { return HBAM_ABI_VERSION; }
 
 int hbam_open_mem(const void* data, uint64_t len, const hbam_opts* opts, hbam_ctx** out) {
-  return open_common(data, len, opts, true, out);
+  if (!valid_stringency(opts)) return finish_open(HBAM_E_ARG, nullptr, "unknown validation stringency", out);
+  std::unique_ptr<BamFile> f;
+  std::string err;
+  int rc = BamFile::open_memory(static_cast<const uint8_t*>(data), len, options_of(opts, true), &f, &err);
+  return finish_open(rc, std::move(f), err, out);
 }
 
 int hbam_open_bgzf(const void* data, uint64_t len, const hbam_opts* opts, hbam_ctx** out) {
-  return open_common(data, len, opts, false, out);
+  std::unique_ptr<BamFile> f;
+  std::string err;
+  int rc = BamFile::open_memory(static_cast<const uint8_t*>(data), len, options_of(opts, false), &f, &err);
+  return finish_open(rc, std::move(f), err, out);
 }
 
 int hbam_open(const char* path, const hbam_opts* opts, hbam_ctx** out) {
-  std::vector<uint8_t> buf;
+  if (!valid_stringency(opts)) return finish_open(HBAM_E_ARG, nullptr, "unknown validation stringency", out);
+  std::unique_ptr<BamFile> f;
   std::string err;
-  if (!read_file(path, &buf, &err)) {
-    *out = new hbam_ctx();
-    (*out)->err = err;
-    return HBAM_E_IO;
-  }
-  return open_common(buf.data(), buf.size(), opts, true, out);
+  int rc = BamFile::open_path(path, options_of(opts, true), &f, &err);
+  return finish_open(rc, std::move(f), err, out);
 }
 
 void hbam_close(hbam_ctx* ctx) { delete ctx; }
@@ -184,8 +286,6 @@ int hbam_header(hbam_ctx* ctx, hbam_header_info* out) {
   out->l_text = f.l_text();
   out->first_record_voff = f.first_record_voff();
   out->file_size = f.file_size();
-  out->n_blocks = f.pipe().blocks().size();
-  out->uncompressed_size = f.pipe().total_u();
   out->text = f.text().c_str();
   return HBAM_OK;
 }
@@ -201,50 +301,64 @@ int hbam_ref(hbam_ctx* ctx, int32_t i, const char** name, int32_t* length) {
   return HBAM_OK;
 }
 
-namespace {
-void fill_batch(hbam_ctx* ctx, const hbam::SpanDev& span, hbam_batch* out) {
-  auto& h = ctx->batch;
-  out->n = span.n;
-  out->ref_id = h.ref_id.data();
-  out->pos = h.pos.data();
-  out->l_seq = h.l_seq.data();
-  out->next_ref_id = h.next_ref_id.data();
-  out->next_pos = h.next_pos.data();
-  out->tlen = h.tlen.data();
-  out->l_read_name = h.l_read_name.data();
-  out->mapq = h.mapq.data();
-  out->bin = h.bin.data();
-  out->n_cigar = h.n_cigar.data();
-  out->flag = h.flag.data();
-  out->key = h.key.data();
-  out->voff = h.voff.data();
-  out->rest_off = h.rest_off.data();
-  out->rest_len = h.rest_len.data();
-  out->data = h.data.data();
-  out->data_len = h.data.size();
-  out->status = span.status;
-}
-}  // namespace
-
-int hbam_decode_span(hbam_ctx* ctx, uint64_t vstart, uint64_t vend, hbam_batch* out) {
-  memset(out, 0, sizeof *out);
+int hbam_file_stats(hbam_ctx* ctx, uint64_t* n_blocks, uint64_t* uncompressed_size) {
   if (!ctx || !ctx->f) return HBAM_E_STATE;
-  ctx->span = hbam::SpanDev();
-  hbam::SpanDev& span = ctx->span;
-  int rc = ctx->f->pipe().decode_span(vstart, vend, hbam::kReader, true, &span);
+  const std::vector<hbam::BlockInfo>* B = nullptr;
+  int rc = ctx->f->all_blocks(&B);
   if (rc != HBAM_OK) {
-    ctx->err = ctx->f->pipe().error();
-    span = hbam::SpanDev();
+    ctx->err = ctx->f->error();
     return rc;
   }
-  rc = hadoop_bam::fetch_span(ctx->f->pipe(), span, &ctx->batch, &ctx->err);
-  if (rc != HBAM_OK) return rc;
-  fill_batch(ctx, span, out);
-  if (span.status != HBAM_OK) {
-    ctx->err = span.error;
-    return span.status;
-  }
+  *n_blocks = B->size();
+  *uncompressed_size = B->empty() ? 0 : B->back().ustart + B->back().isize;
   return HBAM_OK;
+}
+
+int hbam_bytes_read(hbam_ctx* ctx, uint64_t* bytes) {
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  *bytes = ctx->f->bytes_read();
+  return HBAM_OK;
+}
+
+int hbam_prefetch(hbam_ctx* ctx, uint64_t lo, uint64_t hi) {
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  if (hi < lo) {
+    ctx->err = "prefetch range end before its start";
+    return HBAM_E_ARG;
+  }
+  ctx->cursor.reset();
+  int rc = ctx->f->prefetch(lo, hi);
+  if (rc != HBAM_OK) ctx->err = ctx->f->error();
+  return rc;
+}
+
+int hbam_decode_span(hbam_ctx* ctx, uint64_t vstart, uint64_t vend, uint64_t max_records, hbam_batch* out) {
+  memset(out, 0, sizeof *out);
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  ctx->last_is_writables = false;
+  uint64_t next = vend;
+  int rc = ctx->cursor.next_batch(*ctx->f, vstart, vend, max_records, &ctx->batch, &next, &ctx->err);
+  fill_batch(ctx->batch, out);
+  out->next_voff = next;
+  out->status = rc;
+  if (rc == HBAM_E_DEVICE || rc == HBAM_E_STATE || rc == HBAM_E_NOMEM) out->n = 0;
+  return rc;
+}
+
+int hbam_reader_position(hbam_ctx* ctx, uint64_t i, uint64_t* pos) {
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  if (i >= ctx->batch.n) {
+    ctx->err = "record index outside the last batch";
+    return HBAM_E_ARG;
+  }
+  *pos = ctx->cursor.reader_position(*ctx->f, i);
+  return HBAM_OK;
+}
+
+int hbam_decode_span_device(hbam_ctx* ctx, uint64_t vstart, uint64_t vend, int32_t flags, hbam_gpu_stats* st) {
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  ctx->cursor.reset();
+  return decode_device(*ctx->f, vstart, vend, flags, st, nullptr, &ctx->err);
 }
 
 int hbam_open_codec(const hbam_opts* opts, hbam_ctx** out) {
@@ -269,21 +383,22 @@ int hbam_encode_writables(hbam_ctx* ctx, uint8_t* out, uint64_t cap, uint64_t* o
   *len = 0;
   if (!ctx || !ctx->f) return HBAM_E_STATE;
   hbam::Pipeline& p = ctx->f->pipe();
-  const hbam::SpanDev& span = ctx->span;
-  if (span.data) {
-    ctx->err = "hbam_encode_writables needs a span from hbam_decode_span";
+  hbam::SpanDev span;
+  if (ctx->last_is_writables || (ctx->batch.n && !ctx->cursor.last_batch_span(&span))) {
+    ctx->err = "hbam_encode_writables needs a one-window batch from hbam_decode_span";
     return HBAM_E_STATE;
   }
   uint64_t bytes = 0;
-  int rc = p.encoded_bytes(span, &bytes);
+  int rc = ctx->batch.n ? p.encoded_bytes(span, &bytes) : HBAM_OK;
   if (rc != HBAM_OK) {
     ctx->err = p.error();
     return rc;
   }
   *len = bytes;
   if (offs) {  // encodings have the records' own lengths: record i starts where its bytes did
-    for (uint64_t i = 0; i < span.n; ++i) offs[i] = ctx->batch.rest_off[i] - 36;
-    offs[span.n] = bytes;
+    const HostBatch& h = ctx->batch;
+    for (uint64_t i = 0; i < h.n; ++i) offs[i] = h.rest_off[i] - 36 - (h.rest_off[0] - 36);
+    offs[h.n] = bytes;
   }
   if (!out) return HBAM_OK;
   if (cap < bytes) {
@@ -314,17 +429,24 @@ int hbam_decode_writables(hbam_ctx* ctx, const void* buf, uint64_t len, const ui
   memset(out, 0, sizeof *out);
   if (!ctx || (!ctx->f && !ctx->codec)) return HBAM_E_STATE;
   hbam::Pipeline& p = ctx->f ? ctx->f->pipe() : *ctx->codec;
-  ctx->span = hbam::SpanDev();
-  hbam::SpanDev& span = ctx->span;
+  ctx->cursor.reset();
+  ctx->last_is_writables = true;
+  hbam::SpanDev& span = ctx->wspan;
+  span = hbam::SpanDev();
   int rc = p.decode_writables(static_cast<const uint8_t*>(buf), len, offs, n, &span);
   if (rc != HBAM_OK) {
     ctx->err = p.error();
     span = hbam::SpanDev();
     return rc;
   }
-  rc = hadoop_bam::fetch_span(p, span, &ctx->batch, &ctx->err);
+  HostBatch& h = ctx->batch;
+  h.n = 0;
+  h.data_len = 0;
+  h.window_pos.clear();
+  rc = hadoop_bam::fetch_span(p, span, 0, span.n, &h, &ctx->err);
   if (rc != HBAM_OK) return rc;
-  fill_batch(ctx, span, out);
+  fill_batch(h, out);
+  out->status = span.status;
   if (span.status != HBAM_OK) {
     ctx->err = span.error;
     return span.status;
@@ -336,6 +458,7 @@ int hbam_build_splitting_index(hbam_ctx* ctx, int32_t granularity, uint8_t** buf
   *buf = nullptr;
   *len = 0;
   if (!ctx || !ctx->f) return HBAM_E_STATE;
+  ctx->cursor.reset();
   std::vector<uint8_t> out;
   int rc = SplittingBAMIndexer::index(*ctx->f, granularity, &out);
   if (rc != HBAM_OK) {
@@ -349,8 +472,59 @@ int hbam_build_splitting_index(hbam_ctx* ctx, int32_t granularity, uint8_t** buf
   return HBAM_OK;
 }
 
+int hbam_splitting_index_for_records(const hbam_opts* opts, const uint64_t* voffs, uint64_t n, int32_t granularity,
+                                     uint64_t file_size, uint8_t** buf, uint64_t* len) {
+  *buf = nullptr;
+  *len = 0;
+  if (granularity <= 0) {
+    g_open_err = "Granularity must be a positive integer";
+    return HBAM_E_ARG;
+  }
+  hbam_opts o{};
+  if (opts) o = *opts;
+  if (o.device < 0 || o.device >= hbam_device_count()) {
+    g_open_err = "no HIP device " + std::to_string(o.device);
+    return HBAM_E_DEVICE;
+  }
+  // processAlignment (SplittingBAMIndexer.java:197-202): record 0, then every
+  // record whose ordinal + 1 is a multiple of g; finish writes size << 16
+  hbam::Pipeline p(o.device);
+  if (!p.error().empty()) {
+    g_open_err = p.error();
+    return HBAM_E_DEVICE;
+  }
+  hbam::DevBuf<uint64_t> dv;
+  std::vector<uint64_t> ent;
+  hbam::SpanDev span;
+  if (n) {
+    if (dv.reserve(n) != hipSuccess || hipMemcpy(dv.p, voffs, n * 8, hipMemcpyHostToDevice) != hipSuccess) {
+      g_open_err = "device buffer for the voffs";
+      return HBAM_E_DEVICE;
+    }
+    span.n = n;
+    span.rec_voff = dv.p;
+    int rc = p.splitting_entries(span, (uint32_t)granularity, 0, &ent);
+    if (rc != HBAM_OK) {
+      g_open_err = p.error();
+      return rc;
+    }
+  }
+  std::vector<uint64_t> all;
+  if (n) all.push_back(voffs[0]);
+  if (granularity == 1 && n) ent.erase(ent.begin());  // record 0 is written once
+  all.insert(all.end(), ent.begin(), ent.end());
+  all.push_back(file_size << 16);
+  *len = all.size() * 8;
+  *buf = static_cast<uint8_t*>(malloc(*len));
+  if (!*buf) return HBAM_E_NOMEM;
+  for (size_t i = 0; i < all.size(); ++i)
+    for (int b = 0; b < 8; ++b) (*buf)[8 * i + b] = (uint8_t)(all[i] >> (56 - 8 * b));
+  return HBAM_OK;
+}
+
 int hbam_guess_record_starts(hbam_ctx* ctx, const uint64_t* begs, const uint64_t* ends, uint64_t n, uint64_t* out) {
   if (!ctx || !ctx->f) return HBAM_E_STATE;
+  ctx->cursor.reset();
   std::vector<uint64_t> b(begs, begs + n), e(ends, ends + n), r;
   hadoop_bam::BAMSplitGuesser g(*ctx->f);
   int rc = g.guessNextBAMRecordStarts(b, e, &r);
@@ -358,13 +532,14 @@ int hbam_guess_record_starts(hbam_ctx* ctx, const uint64_t* begs, const uint64_t
     ctx->err = ctx->f->error();
     return rc;
   }
-  memcpy(out, r.data(), n * 8);
+  if (n) memcpy(out, r.data(), n * 8);
   return HBAM_OK;
 }
 
 int hbam_guess_bgzf_block_starts(hbam_ctx* ctx, const uint64_t* begs, const uint64_t* ends, uint64_t n,
                                  uint64_t* out) {
   if (!ctx || !ctx->f) return HBAM_E_STATE;
+  ctx->cursor.reset();
   std::vector<uint64_t> b(begs, begs + n), e(ends, ends + n), r;
   int rc = hadoop_bam::guess_bgzf_batch(*ctx->f, b, e, &r, &ctx->err);
   if (rc != HBAM_OK) return rc;
@@ -376,6 +551,7 @@ int hbam_get_splits(hbam_ctx* ctx, const uint64_t* starts, const uint64_t* lengt
                     uint64_t sbi_len, uint64_t* vstarts, uint64_t* vends, uint64_t* nout) {
   *nout = 0;
   if (!ctx || !ctx->f) return HBAM_E_STATE;
+  ctx->cursor.reset();
   std::vector<FileSplit> sp(n);
   for (uint64_t i = 0; i < n; ++i) {
     sp[i].path = "bam";
@@ -399,30 +575,37 @@ int hbam_get_splits(hbam_ctx* ctx, const uint64_t* starts, const uint64_t* lengt
 int hbam_blocks(hbam_ctx* ctx, uint64_t* coff, uint32_t* csize, uint32_t* isize, uint64_t* ustart, uint64_t cap,
                 uint64_t* n) {
   if (!ctx || !ctx->f) return HBAM_E_STATE;
-  const auto& b = ctx->f->pipe().blocks();
-  *n = b.size();
-  for (size_t i = 0; i < b.size() && i < cap; ++i) {
-    if (coff) coff[i] = b[i].coff;
-    if (csize) csize[i] = b[i].csize;
-    if (isize) isize[i] = b[i].isize;
-    if (ustart) ustart[i] = b[i].ustart;
+  ctx->cursor.reset();
+  const std::vector<hbam::BlockInfo>* B = nullptr;
+  int rc = ctx->f->all_blocks(&B);
+  if (rc != HBAM_OK) {
+    ctx->err = ctx->f->error();
+    return rc;
+  }
+  *n = B->size();
+  for (size_t i = 0; i < B->size() && i < cap; ++i) {
+    if (coff) coff[i] = (*B)[i].coff;
+    if (csize) csize[i] = (*B)[i].csize;
+    if (isize) isize[i] = (*B)[i].isize;
+    if (ustart) ustart[i] = (*B)[i].ustart;
   }
   return HBAM_OK;
 }
 
 int hbam_read_inflated(hbam_ctx* ctx, uint64_t pos, uint64_t len, uint8_t* dst) {
   if (!ctx || !ctx->f) return HBAM_E_STATE;
+  ctx->cursor.reset();
   std::vector<uint8_t> v;
-  int rc = ctx->f->pipe().read_stream(pos, len, &v);
+  int rc = ctx->f->read_inflated(pos, len, &v);
   if (rc != HBAM_OK) {
-    ctx->err = ctx->f->pipe().error();
+    ctx->err = ctx->f->error();
     return rc;
   }
   if (v.size() != len) {
     ctx->err = "range beyond the inflated stream";
     return HBAM_E_ARG;
   }
-  memcpy(dst, v.data(), len);
+  if (len) memcpy(dst, v.data(), len);
   return HBAM_OK;
 }
 
@@ -436,7 +619,7 @@ int64_t hbam_murmurhash3(const void* key, uint64_t len, int32_t seed) {
   return hadoop_bam::murmurhash3(static_cast<const uint8_t*>(key), len, seed);
 }
 
-// ---- device-resident pipeline ------------------------------------------------
+// ---- device-resident decode --------------------------------------------------
 int32_t hbam_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -451,12 +634,7 @@ int hbam_gpu_create(int32_t device, hbam_gpu** out) {
     return HBAM_E_DEVICE;
   }
   auto* g = new hbam_gpu();
-  g->p.reset(new hbam::Pipeline(device));
-  if (!g->p->error().empty()) {
-    g_open_err = g->p->error();
-    delete g;
-    return HBAM_E_DEVICE;
-  }
+  g->device = device;
   *out = g;
   return HBAM_OK;
 }
@@ -465,88 +643,93 @@ void hbam_gpu_destroy(hbam_gpu* g) { delete g; }
 
 const char* hbam_gpu_error(hbam_gpu* g) { return g ? g->err.c_str() : g_open_err.c_str(); }
 
-int hbam_gpu_load(hbam_gpu* g, const void* data, uint64_t len, uint64_t base_offset, int32_t n_ref,
-                  uint64_t first_pos) {
-  int rc = g->p->load(static_cast<const uint8_t*>(data), len, base_offset);
-  if (rc == HBAM_OK) rc = g->p->locate();
-  if (rc != HBAM_OK) {
-    g->err = g->p->error();
-    return rc;
-  }
-  if (first_pos == UINT64_MAX) {
-    // whole file: parse the header with the same GPU-backed reader
-    std::unique_ptr<BamFile> tmp;
-    std::string err;
-    rc = BamFile::open(static_cast<const uint8_t*>(data), len, g->p->device(), true, false, &tmp, &err);
-    if (rc != HBAM_OK) {
-      g->err = err;
-      return rc;
-    }
-    g->p->set_n_ref(tmp->n_ref());
-    g->first_pos = tmp->header_end();
-  } else {
-    g->p->set_n_ref(n_ref);
-    g->first_pos = first_pos;
-  }
+int hbam_gpu_load(hbam_gpu* g, const void* data, uint64_t len) {
+  OpenOptions o;
+  o.device = g->device;
+  o.window_bytes = g->window;
+  g->f.reset();
+  g->span = hbam::SpanDev();
+  std::string err;
+  int rc = BamFile::open_device_copy(static_cast<const uint8_t*>(data), len, o, &g->f, &err);
+  if (rc != HBAM_OK) g->err = err;
+  return rc;
+}
+
+int hbam_gpu_set_window(hbam_gpu* g, uint64_t window_bytes) {
+  g->window = window_bytes ? window_bytes : hadoop_bam::kDefaultWindowBytes;
+  if (g->f) g->f->set_window_bytes(g->window);
   return HBAM_OK;
 }
 
 int hbam_gpu_run(hbam_gpu* g, int32_t flags, hbam_gpu_stats* st) {
   memset(st, 0, sizeof *st);
-  hbam::Pipeline& p = *g->p;
-  p.timing = (flags & 1) != 0;
+  if (!g->f) {
+    g->err = "hbam_gpu_run needs a loaded file";
+    return HBAM_E_STATE;
+  }
+  return decode_device(*g->f, g->f->first_record_voff(), ~0ull, flags, st, &g->span, &g->err);
+}
+
+int hbam_gpu_index(hbam_gpu* g, int32_t granularity, uint8_t** buf, uint64_t* len, float* ms) {
+  *buf = nullptr;
+  *len = 0;
+  *ms = 0;
+  if (!g->f) return HBAM_E_STATE;
+  hbam::Pipeline& p = g->f->pipe();
+  p.timing = false;
+  g->f->invalidate_window();
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   (void)hipEventRecord(e0, p.stream());
-  const uint64_t lf0 = p.link_fallbacks(), il0 = p.inflate_launches(), lr0 = p.link_rewalks();
-  int rc = p.locate();
-  if (rc == HBAM_OK) rc = p.inflate(0, (uint32_t)p.blocks().size(), true);
-  float ms_inflate = p.times.inflate, ms_huff = p.times.huff, ms_lz = p.times.lz77;
-  if (rc == HBAM_OK) {
-    rc = p.decode_span(p.voff_of(g->first_pos), ~0ull, hbam::kReader, (flags & 2) == 0, &g->span);
-  }
+  std::vector<uint8_t> out;
+  int rc = SplittingBAMIndexer::index(*g->f, granularity, &out);
   (void)hipEventRecord(e1, p.stream());
   (void)hipEventSynchronize(e1);
-  (void)hipEventElapsedTime(&st->ms_total, e0, e1);
+  (void)hipEventElapsedTime(ms, e0, e1);
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
+  g->span = hbam::SpanDev();
   if (rc != HBAM_OK) {
-    g->err = p.error();
-    st->status = rc;
+    g->err = g->f->error();
     return rc;
   }
-  st->n_blocks = p.blocks().size();
-  st->compressed_bytes = p.file_len();
-  st->inflated_bytes = p.total_u();
-  st->records = g->span.n;
-  st->status = g->span.status;
-  st->link_fallbacks = (int32_t)(p.link_fallbacks() - lf0);
-  st->inflate_launches = (int32_t)(p.inflate_launches() - il0);
-  st->link_rewalks = (int32_t)(p.link_rewalks() - lr0);
-  if (p.timing) {
-    st->ms_locate = p.times.locate;
-    st->ms_inflate = ms_inflate;
-    st->ms_huff = ms_huff;
-    st->ms_lz77 = ms_lz;
-    st->ms_chain = p.times.chain;
-    st->ms_decode = p.times.decode;
-  }
-  if (g->span.n) {
-    (void)hipMemcpy(&st->first_voff, g->span.rec_voff, 8, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(&st->last_voff, g->span.rec_voff + g->span.n - 1, 8, hipMemcpyDeviceToHost);
-  }
-  if (g->span.status != HBAM_OK) g->err = g->span.error;
-  return g->span.status;
+  *buf = static_cast<uint8_t*>(malloc(out.size() ? out.size() : 1));
+  if (!*buf) return HBAM_E_NOMEM;
+  memcpy(*buf, out.data(), out.size());
+  *len = out.size();
+  return HBAM_OK;
 }
 
 int hbam_gpu_run_streamed(hbam_gpu* g, const void* data, uint64_t len, uint64_t piece_bytes, hbam_gpu_stats* st) {
   memset(st, 0, sizeof *st);
-  hbam::Pipeline& p = *g->p;
+  if (!g->f || len != g->f->file_size()) {
+    g->err = "hbam_gpu_run_streamed needs the loaded file's bytes";
+    return HBAM_E_STATE;
+  }
+  hbam::Pipeline& p = g->f->pipe();
   p.timing = false;
+  g->f->invalidate_window();
+  // one window holding the whole file in the pipeline's own buffer (untimed)
+  int rc = p.load(static_cast<const uint8_t*>(data), len, 0, true);
+  if (rc != HBAM_OK) {
+    g->err = p.error();
+    return rc;
+  }
   const uint64_t il0 = p.inflate_launches();
   g->span = hbam::SpanDev();
-  int rc = p.run_streamed(static_cast<const uint8_t*>(data), len, piece_bytes, g->first_pos, &g->span, &st->ms_total);
+  // first record: the header end (the same position the resident pass starts at)
+  std::unique_ptr<BamFile>& f = g->f;
+  rc = p.locate();
+  uint64_t first_pos = 0;
+  if (rc == HBAM_OK) {
+    const int64_t fp = p.pos_of_voff(f->first_record_voff());
+    if (fp < 0) rc = HBAM_E_STATE;
+    first_pos = (uint64_t)std::max<int64_t>(fp, 0);
+  }
+  if (rc == HBAM_OK)
+    rc = p.run_streamed(static_cast<const uint8_t*>(data), len, piece_bytes, first_pos, &g->span, &st->ms_total);
+  g->f->invalidate_window();
   if (rc != HBAM_OK) {
     g->err = p.error();
     st->status = rc;
@@ -557,6 +740,7 @@ int hbam_gpu_run_streamed(hbam_gpu* g, const void* data, uint64_t len, uint64_t 
   st->inflated_bytes = p.total_u();
   st->records = g->span.n;
   st->status = g->span.status;
+  st->windows = 1;
   st->inflate_launches = (int32_t)(p.inflate_launches() - il0);
   if (g->span.n) {
     (void)hipMemcpy(&st->first_voff, g->span.rec_voff, 8, hipMemcpyDeviceToHost);
@@ -578,21 +762,28 @@ void hbam_host_free(void* p) {
 
 int hbam_gpu_reload(hbam_gpu* g, const void* data, uint64_t len, int32_t pinned, float* ms) {
   *ms = 0;
-  int rc = g->p->reload(static_cast<const uint8_t*>(data), len, pinned != 0, ms);
-  if (rc != HBAM_OK) g->err = g->p->error();
+  if (!g->f) return HBAM_E_STATE;
+  hbam::Pipeline& p = g->f->pipe();
+  g->f->invalidate_window();
+  int rc = p.load(static_cast<const uint8_t*>(data), len, 0, true);  // the copy target (untimed)
+  if (rc == HBAM_OK) rc = p.reload(static_cast<const uint8_t*>(data), len, pinned != 0, ms);
+  if (rc != HBAM_OK) g->err = p.error();
+  g->span = hbam::SpanDev();
   return rc;
 }
 
 int hbam_gpu_d2d_bandwidth(hbam_gpu* g, uint64_t bytes, int32_t iters, float* gbps) {
-  int rc = g->p->d2d_bandwidth(bytes, iters, gbps);
-  if (rc != HBAM_OK) g->err = g->p->error();
+  if (!g->f) return HBAM_E_STATE;
+  int rc = g->f->pipe().d2d_bandwidth(bytes, iters, gbps);
+  if (rc != HBAM_OK) g->err = g->f->pipe().error();
   return rc;
 }
 
 int hbam_gpu_encode_writables(hbam_gpu* g, int32_t iters, float* ms_per_iter, uint64_t* bytes) {
   *ms_per_iter = 0;
   *bytes = 0;
-  hbam::Pipeline& p = *g->p;
+  if (!g->f) return HBAM_E_STATE;
+  hbam::Pipeline& p = g->f->pipe();
   uint64_t nb = 0;
   int rc = p.encoded_bytes(g->span, &nb);
   if (rc != HBAM_OK) {
@@ -640,16 +831,27 @@ int hbam_gpu_bgzf_compress(hbam_gpu* g, int32_t level, int32_t flags, int32_t it
                            uint64_t* out_len) {
   *ms_per_iter = 0;
   *out_len = 0;
-  hbam::Pipeline& p = *g->p;
-  if (!p.d_u()) {
-    g->err = "hbam_gpu_bgzf_compress needs a run (inflated stream) first";
+  if (!g->f) return HBAM_E_STATE;
+  hbam::Pipeline& p = g->f->pipe();
+  if (!p.d_u() || p.base() != 0 || !p.at_eof() || p.blocks().empty()) {
+    g->err = "hbam_gpu_bgzf_compress needs a one-window run (inflated stream) first";
     return HBAM_E_STATE;
   }
   std::vector<uint64_t> ustart;
   std::vector<uint32_t> lens;
-  for (const auto& b : p.blocks()) {
-    ustart.push_back(b.ustart);
-    lens.push_back(b.isize);
+  const auto& B = p.blocks();
+  // the input's EOF terminator is re-added by HBAM_BGZF_EOF, not recompressed
+  size_t nb = B.size();
+  if ((flags & HBAM_BGZF_EOF) && nb && B[nb - 1].isize == 0) --nb;
+  for (size_t i = 0; i < nb; ++i) {
+    ustart.push_back(B[i].ustart);
+    lens.push_back(B[i].isize);
+  }
+  // the run inflated the blocks from the first record on; the header's too
+  int rc0 = p.inflate(0, (uint32_t)B.size());
+  if (rc0 != HBAM_OK) {
+    g->err = p.error();
+    return rc0;
   }
   if (!g->bgzf) g->bgzf.reset(new hbam::BgzfCompressor(p.device()));
   float ms = 0, tot = 0;

@@ -435,164 +435,194 @@ __global__ void k_guess_bgzf_starts(GuessEnv E, const uint64_t* __restrict__ beg
 }  // namespace hbam
 
 // ---------------------------------------------------------------------------
-// host driver: hadoop_bam::guess_batch
+// host drivers: hadoop_bam::guess_batch / guess_bgzf_batch
 // ---------------------------------------------------------------------------
+// Each split point reads at most a few hundred KB after its start
+// (BAMSplitGuesser.java:127-138 MAX_BYTES_READ; BGZFSplitGuesser.java:74), so
+// the points are grouped into windows of nearby ranges; a window is loaded
+// from its first point's offset (free start: the block chain begins at the
+// first header candidate whose BSIZE chain runs through the window, a byte
+// offset need not be a block start), every block in it is inflated and CRC
+// checked, and one launch guesses all of its points.  One extra 64 KiB keeps
+// a block that straddles a point's read limit in the table, so the limit
+// checks see it exactly as over the whole file.
 namespace hadoop_bam {
 
-int guess_batch(BamFile& f, const std::vector<uint64_t>& begs, const std::vector<uint64_t>& ends,
-                std::vector<uint64_t>* out, std::string* err) {
+namespace {
+struct GuessPoint {
+  uint64_t beg, end, lim;  // lim: end of the bytes the guesser may read
+  size_t slot;
+};
+
+// Windows over sorted points: [lo, hi) covering points [a, b).
+template <typename F>
+int for_each_window(BamFile& f, std::vector<GuessPoint>& pts, F&& body) {
+  std::sort(pts.begin(), pts.end(), [](const GuessPoint& x, const GuessPoint& y) { return x.beg < y.beg; });
+  const uint64_t size = f.file_size(), cap = std::max<uint64_t>(f.window_bytes(), 1ull << 20);
+  for (size_t a = 0; a < pts.size();) {
+    const uint64_t lo = pts[a].beg;
+    uint64_t hi = std::min(size, pts[a].lim + 0x10000);
+    size_t b = a + 1;
+    while (b < pts.size() && pts[b].beg <= hi + (1ull << 20)) {
+      const uint64_t h2 = std::max(hi, std::min(size, pts[b].lim + 0x10000));
+      if (h2 - lo > cap) break;
+      hi = h2;
+      ++b;
+    }
+    int rc = body(lo, hi, a, b);
+    if (rc != hbam::kOk) return rc;
+    a = b;
+  }
+  return hbam::kOk;
+}
+
+// Load + locate + inflate + CRC-check the window; *valid[k] per block.
+int prepare_window(BamFile& f, uint64_t lo, uint64_t hi, hbam::DevBuf<uint8_t>* dvalid, std::string* err) {
   using namespace hbam;
+  int rc = f.load_window(lo, hi, /*free_start=*/true);
+  if (rc != kOk) {
+    *err = f.error();
+    return rc;
+  }
   Pipeline& p = f.pipe();
-  const size_t n = begs.size();
-  out->assign(n, 0);
   const auto& blk = p.blocks();
   const uint32_t nblk = (uint32_t)blk.size();
-  // blocks any window can read: coff in [beg, beg + MAX_BYTES_READ)
-  std::vector<uint8_t> need(nblk, 0);
-  std::vector<uint32_t> dev_idx;
-  std::vector<uint64_t> db, de;
-  std::vector<size_t> dev_slot;
-  for (size_t i = 0; i < n; ++i) {
-    if (begs[i] == 0) {  // :115-123
-      (*out)[i] = f.first_record_voff();
-      continue;
-    }
-    dev_slot.push_back(i);
-    db.push_back(begs[i]);
-    de.push_back(ends[i]);
-    const uint64_t W = std::min<uint64_t>(begs[i] + std::min<uint64_t>(ends[i] - begs[i], kMaxBytesRead), f.file_size());
-    auto it = std::lower_bound(blk.begin(), blk.end(), begs[i], [](const BlockInfo& b, uint64_t c) { return b.coff < c; });
-    for (; it != blk.end() && it->coff < W; ++it) need[it - blk.begin()] = 1;
-  }
-  if (dev_slot.empty()) return kOk;
-  // inflate the needed ranges (inflate errors mark blocks invalid, as a failed seek would)
   std::vector<uint8_t> valid(nblk, 0);
-  for (uint32_t k = 0; k < nblk;) {
-    if (!need[k]) { ++k; continue; }
-    uint32_t e = k;
-    while (e < nblk && need[e]) ++e;
-    // inflate block by block ranges; a bad block fails the range -> retry per block
-    if (p.inflate(k, e) == kOk) {
-      for (uint32_t j = k; j < e; ++j) valid[j] = 1;
+  std::vector<uint32_t> dev_idx;
+  if (nblk) {
+    // inflate errors mark blocks invalid, as a failed seek would
+    if (p.inflate(0, nblk) == kOk) {
+      for (uint32_t j = 0; j < nblk; ++j) valid[j] = 1;
     } else {
-      for (uint32_t j = k; j < e; ++j) valid[j] = p.inflate(j, j + 1) == kOk;
+      for (uint32_t j = 0; j < nblk; ++j) valid[j] = p.inflate(j, j + 1) == kOk;
     }
-    for (uint32_t j = k; j < e; ++j)
+    for (uint32_t j = 0; j < nblk; ++j)
       if (valid[j] && blk[j].isize > 0) dev_idx.push_back(j);
-    k = e;
   }
-  DevBuf<uint8_t> dvalid, dok;
   DevBuf<uint32_t> dlist;
-  DevBuf<uint64_t> dbeg, dend, dout;
-  DevBuf<int32_t> dst;
-  const uint32_t m = (uint32_t)dev_slot.size();
   hipStream_t s = p.stream();
   auto chk = [&](hipError_t e) {
     if (e != hipSuccess) *err = std::string("HIP: ") + hipGetErrorString(e);
     return e == hipSuccess;
   };
-  if (!chk(dvalid.reserve(nblk + 1)) || !chk(dlist.reserve(dev_idx.size() + 1)) || !chk(dbeg.reserve(m)) ||
-      !chk(dend.reserve(m)) || !chk(dout.reserve(m)) || !chk(dst.reserve(m)))
-    return kErrDevice;
-  if (!chk(hipMemcpyAsync(dvalid.p, valid.data(), nblk, hipMemcpyHostToDevice, s))) return kErrDevice;
-  if (!dev_idx.empty()) {
+  if (!chk(dvalid->reserve(nblk + 1)) || !chk(dlist.reserve(dev_idx.size() + 1))) return kErrDevice;
+  if (nblk && !chk(hipMemcpyAsync(dvalid->p, valid.data(), nblk, hipMemcpyHostToDevice, s))) return kErrDevice;
+  if (!dev_idx.empty()) {  // setCheckCrcs(true): valid[k] = CRC ok
     if (!chk(hipMemcpyAsync(dlist.p, dev_idx.data(), dev_idx.size() * 4, hipMemcpyHostToDevice, s))) return kErrDevice;
-    // CRC check of every needed, inflated block: valid[k] = crc ok
     hipLaunchKernelGGL(k_block_crc, dim3((uint32_t)dev_idx.size()), dim3(256), 0, s, p.d_blocks(), dlist.p,
-                       (uint32_t)dev_idx.size(), p.d_u(), dvalid.p);
+                       (uint32_t)dev_idx.size(), p.d_u(), dvalid->p);
     if (!chk(hipGetLastError())) return kErrDevice;
   }
-  if (!chk(hipMemcpyAsync(dbeg.p, db.data(), m * 8, hipMemcpyHostToDevice, s)) ||
-      !chk(hipMemcpyAsync(dend.p, de.data(), m * 8, hipMemcpyHostToDevice, s)))
+  if (!chk(hipStreamSynchronize(s))) return kErrDevice;
+  return kOk;
+}
+
+// points [a, b) through kernel K; results into out by slot
+template <typename Launch>
+int run_points(BamFile& f, const std::vector<GuessPoint>& pts, size_t a, size_t b, const hbam::DevBuf<uint8_t>& dvalid,
+               std::vector<uint64_t>* out, std::string* err, Launch&& launch) {
+  using namespace hbam;
+  Pipeline& p = f.pipe();
+  const uint32_t m = (uint32_t)(b - a);
+  std::vector<uint64_t> hb(m), he(m), res(m);
+  for (uint32_t j = 0; j < m; ++j) {
+    hb[j] = pts[a + j].beg;
+    he[j] = pts[a + j].end;
+  }
+  DevBuf<uint64_t> dbeg, dend, dout;
+  DevBuf<int32_t> dst;
+  hipStream_t s = p.stream();
+  auto chk = [&](hipError_t e) {
+    if (e != hipSuccess) *err = std::string("HIP: ") + hipGetErrorString(e);
+    return e == hipSuccess;
+  };
+  if (!chk(dbeg.reserve(m)) || !chk(dend.reserve(m)) || !chk(dout.reserve(m)) || !chk(dst.reserve(m)))
+    return kErrDevice;
+  if (!chk(hipMemcpyAsync(dbeg.p, hb.data(), m * 8, hipMemcpyHostToDevice, s)) ||
+      !chk(hipMemcpyAsync(dend.p, he.data(), m * 8, hipMemcpyHostToDevice, s)))
     return kErrDevice;
   GuessEnv E;
-  E.file = p.d_file();
+  E.file = p.d_file() - p.base();  // absolute file coordinates (the window covers every point's bytes)
   E.flen = f.file_size();
   E.blocks = p.d_blocks();
-  E.nblk = nblk;
+  E.nblk = (uint32_t)p.blocks().size();
   E.u = p.d_u();
   E.valid = dvalid.p;
   E.n_ref = f.n_ref();
-  hipLaunchKernelGGL(k_guess_splits, dim3((m + 63) / 64), dim3(64), 0, s, E, dbeg.p, dend.p, m, dout.p, dst.p);
+  launch(E, dbeg.p, dend.p, m, dout.p, dst.p, s);
   if (!chk(hipGetLastError())) return kErrDevice;
-  std::vector<uint64_t> res(m);
   if (!chk(hipMemcpyAsync(res.data(), dout.p, m * 8, hipMemcpyDeviceToHost, s)) || !chk(hipStreamSynchronize(s)))
     return kErrDevice;
-  for (uint32_t j = 0; j < m; ++j) (*out)[dev_slot[j]] = res[j];
+  for (uint32_t j = 0; j < m; ++j) (*out)[pts[a + j].slot] = res[j];
   return kOk;
+}
+}  // namespace
+
+int guess_batch(BamFile& f, const std::vector<uint64_t>& begs, const std::vector<uint64_t>& ends,
+                std::vector<uint64_t>* out, std::string* err) {
+  using namespace hbam;
+  const size_t n = begs.size();
+  out->assign(n, 0);
+  std::vector<GuessPoint> pts;
+  for (size_t i = 0; i < n; ++i) {
+    if (ends[i] < begs[i]) {
+      *err = "split end before its start";
+      return kErrArg;
+    }
+    if (begs[i] == 0) {  // :115-123 the header gives the first record
+      (*out)[i] = f.first_record_voff();
+      continue;
+    }
+    if (begs[i] >= f.file_size()) {  // nothing to read: no record start
+      (*out)[i] = ends[i];
+      continue;
+    }
+    const uint64_t lim = std::min<uint64_t>(begs[i] + std::min<uint64_t>(ends[i] - begs[i], kMaxBytesRead), f.file_size());
+    pts.push_back({begs[i], ends[i], lim, i});
+  }
+  DevBuf<uint8_t> dvalid;
+  return for_each_window(f, pts, [&](uint64_t lo, uint64_t hi, size_t a, size_t b) {
+    int rc = prepare_window(f, lo, hi, &dvalid, err);
+    if (rc != kOk) return rc;
+    return run_points(f, pts, a, b, dvalid, out, err,
+                      [](const GuessEnv& E, const uint64_t* db, const uint64_t* de, uint32_t m, uint64_t* dout,
+                         int32_t* dst, hipStream_t s) {
+                        hipLaunchKernelGGL(k_guess_splits, dim3((m + 63) / 64), dim3(64), 0, s, E, db, de, m, dout,
+                                           dst);
+                      });
+  });
 }
 
 int guess_bgzf_batch(BamFile& f, const std::vector<uint64_t>& begs, const std::vector<uint64_t>& ends,
                      std::vector<uint64_t>* out, std::string* err) {
   using namespace hbam;
-  Pipeline& p = f.pipe();
   const size_t n = begs.size();
   out->assign(n, 0);
-  if (n == 0) return kOk;
-  const auto& blk = p.blocks();
-  const uint32_t nblk = (uint32_t)blk.size();
-  for (size_t i = 0; i < n; ++i)
+  std::vector<GuessPoint> pts;
+  for (size_t i = 0; i < n; ++i) {
     if (ends[i] < begs[i]) {
       *err = "split end before its start";
       return kErrArg;
     }
-  // blocks a window can accept: coff in [beg, beg + firstBGZFEnd)
-  std::vector<uint8_t> need(nblk, 0);
-  for (size_t i = 0; i < n; ++i) {
-    const uint64_t lim = begs[i] + std::min<uint64_t>(ends[i] - begs[i], 0xffff);
-    auto it = std::lower_bound(blk.begin(), blk.end(), begs[i], [](const BlockInfo& b, uint64_t c) { return b.coff < c; });
-    for (; it != blk.end() && it->coff < lim; ++it) need[it - blk.begin()] = 1;
-  }
-  std::vector<uint8_t> valid(nblk, 0);
-  std::vector<uint32_t> dev_idx;
-  for (uint32_t k = 0; k < nblk;) {
-    if (!need[k]) { ++k; continue; }
-    uint32_t e = k;
-    while (e < nblk && need[e]) ++e;
-    if (p.inflate(k, e) == kOk) {
-      for (uint32_t j = k; j < e; ++j) valid[j] = 1;
-    } else {  // a bad block fails the range: per block, as a failed seek would
-      for (uint32_t j = k; j < e; ++j) valid[j] = p.inflate(j, j + 1) == kOk;
+    if (begs[i] >= f.file_size()) {
+      (*out)[i] = ends[i];
+      continue;
     }
-    for (uint32_t j = k; j < e; ++j)
-      if (valid[j] && blk[j].isize > 0) dev_idx.push_back(j);
-    k = e;
+    const uint64_t lim =
+        std::min<uint64_t>(begs[i] + std::min<uint64_t>(ends[i] - begs[i], kBgzfGuessWindow), f.file_size());
+    pts.push_back({begs[i], ends[i], lim, i});
   }
   DevBuf<uint8_t> dvalid;
-  DevBuf<uint32_t> dlist;
-  DevBuf<uint64_t> dbeg, dend, dout;
-  hipStream_t s = p.stream();
-  auto chk = [&](hipError_t e) {
-    if (e != hipSuccess) *err = std::string("HIP: ") + hipGetErrorString(e);
-    return e == hipSuccess;
-  };
-  if (!chk(dvalid.reserve(nblk + 1)) || !chk(dlist.reserve(dev_idx.size() + 1)) || !chk(dbeg.reserve(n)) ||
-      !chk(dend.reserve(n)) || !chk(dout.reserve(n)))
-    return kErrDevice;
-  if (!chk(hipMemcpyAsync(dvalid.p, valid.data(), nblk, hipMemcpyHostToDevice, s))) return kErrDevice;
-  if (!dev_idx.empty()) {  // setCheckCrcs(true) (:89)
-    if (!chk(hipMemcpyAsync(dlist.p, dev_idx.data(), dev_idx.size() * 4, hipMemcpyHostToDevice, s))) return kErrDevice;
-    hipLaunchKernelGGL(k_block_crc, dim3((uint32_t)dev_idx.size()), dim3(256), 0, s, p.d_blocks(), dlist.p,
-                       (uint32_t)dev_idx.size(), p.d_u(), dvalid.p);
-    if (!chk(hipGetLastError())) return kErrDevice;
-  }
-  if (!chk(hipMemcpyAsync(dbeg.p, begs.data(), n * 8, hipMemcpyHostToDevice, s)) ||
-      !chk(hipMemcpyAsync(dend.p, ends.data(), n * 8, hipMemcpyHostToDevice, s)))
-    return kErrDevice;
-  GuessEnv E;
-  E.file = p.d_file();
-  E.flen = f.file_size();
-  E.blocks = p.d_blocks();
-  E.nblk = nblk;
-  E.u = p.d_u();
-  E.valid = dvalid.p;
-  E.n_ref = f.n_ref();
-  hipLaunchKernelGGL(k_guess_bgzf_starts, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s, E, dbeg.p, dend.p,
-                     (uint32_t)n, dout.p);
-  if (!chk(hipGetLastError())) return kErrDevice;
-  if (!chk(hipMemcpyAsync(out->data(), dout.p, n * 8, hipMemcpyDeviceToHost, s)) || !chk(hipStreamSynchronize(s)))
-    return kErrDevice;
-  return kOk;
+  return for_each_window(f, pts, [&](uint64_t lo, uint64_t hi, size_t a, size_t b) {
+    int rc = prepare_window(f, lo, hi, &dvalid, err);
+    if (rc != kOk) return rc;
+    return run_points(f, pts, a, b, dvalid, out, err,
+                      [](const GuessEnv& E, const uint64_t* db, const uint64_t* de, uint32_t m, uint64_t* dout,
+                         int32_t*, hipStream_t s) {
+                        hipLaunchKernelGGL(k_guess_bgzf_starts, dim3((m + 63) / 64), dim3(64), 0, s, E, db, de, m,
+                                           dout);
+                      });
+  });
 }
 
 }  // namespace hadoop_bam

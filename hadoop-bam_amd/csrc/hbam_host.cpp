@@ -1,61 +1,214 @@
 // hbam_host.cpp -- C++ mirror of org.seqdoop.hadoop_bam's BAM read path
-// classes on top of the gfx950 pipeline.  Host code here plans, validates
-// headers and copies results; every per-record / per-byte loop of the hot path
-// runs in hbam_kernels.hip.
+// classes on top of the gfx950 pipeline.  Host code here plans windows,
+// parses the header and copies results; every per-record / per-byte loop of
+// the hot path runs in hbam_kernels.hip.
 #include "hbam_host.h"
 
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstring>
 
 namespace hadoop_bam {
 
+using hbam::BlockInfo;
 using hbam::kErrArg;
 using hbam::kErrDevice;
 using hbam::kErrFormat;
 using hbam::kErrIO;
+using hbam::kErrNoMem;
 using hbam::kErrState;
 using hbam::kErrTrunc;
 using hbam::kOk;
 
 // ---------------------------------------------------------------------------
+// PinnedVec / Source
+// ---------------------------------------------------------------------------
+template <typename T>
+bool PinnedVec<T>::resize(size_t n) {
+  if (n <= cap_) {
+    n_ = n;
+    return true;
+  }
+  size_t c = std::max(n, cap_ + cap_ / 2);
+  T* q = nullptr;
+  if (hipHostMalloc(reinterpret_cast<void**>(&q), std::max<size_t>(c, 1) * sizeof(T), hipHostMallocDefault) !=
+      hipSuccess)
+    return false;
+  if (p_ && n_) memcpy(q, p_, n_ * sizeof(T));
+  if (p_) (void)hipHostFree(p_);
+  p_ = q;
+  cap_ = c;
+  n_ = n;
+  return true;
+}
+template <typename T>
+void PinnedVec<T>::release() {
+  if (p_) (void)hipHostFree(p_);
+  p_ = nullptr;
+  n_ = cap_ = 0;
+}
+template class PinnedVec<int32_t>;
+template class PinnedVec<uint8_t>;
+template class PinnedVec<uint16_t>;
+template class PinnedVec<int64_t>;
+template class PinnedVec<uint64_t>;
+template class PinnedVec<uint32_t>;
+
+Source::~Source() {
+  if (map) munmap(map, map_len);
+}
+
+// ---------------------------------------------------------------------------
 // BamFile
 // ---------------------------------------------------------------------------
-int BamFile::open(const uint8_t* data, uint64_t len, int device, bool parse_header, bool check_crc,
-                  std::unique_ptr<BamFile>* out, std::string* err) {
-  (void)check_crc;  // CRC checking is opt-in in htsjdk's reader (off by default)
+int BamFile::open_memory(const uint8_t* data, uint64_t len, const OpenOptions& o, std::unique_ptr<BamFile>* out,
+                         std::string* err) {
   std::unique_ptr<BamFile> f(new BamFile());
-  f->file_.assign(data, data + len);
+  f->src_.owned.assign(data, data + len);
+  f->src_.host = f->src_.owned.data();
+  f->src_.size = len;
+  int rc = f->init(o, err);
+  if (rc == kOk) *out = std::move(f);
+  return rc;
+}
+
+int BamFile::open_path(const char* path, const OpenOptions& o, std::unique_ptr<BamFile>* out, std::string* err) {
+  std::unique_ptr<BamFile> f(new BamFile());
+  const int fd = ::open(path, O_RDONLY);
+  if (fd < 0) {
+    *err = std::string("cannot open ") + path;
+    return kErrIO;
+  }
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    ::close(fd);
+    *err = std::string("cannot stat ") + path;
+    return kErrIO;
+  }
+  f->src_.size = (uint64_t)st.st_size;
+  if (st.st_size > 0) {
+    // pages are read only when a window copies them (WrapSeekable seeks)
+    void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
+    if (m == MAP_FAILED) {
+      ::close(fd);
+      *err = std::string("cannot map ") + path;
+      return kErrIO;
+    }
+    f->src_.map = m;
+    f->src_.map_len = (size_t)st.st_size;
+    f->src_.host = static_cast<const uint8_t*>(m);
+  } else {
+    static const uint8_t empty = 0;
+    f->src_.host = &empty;
+  }
+  ::close(fd);
+  int rc = f->init(o, err);
+  if (rc == kOk) *out = std::move(f);
+  return rc;
+}
+
+int BamFile::open_device_copy(const uint8_t* data, uint64_t len, const OpenOptions& o, std::unique_ptr<BamFile>* out,
+                              std::string* err) {
+  std::unique_ptr<BamFile> f(new BamFile());
+  f->src_.size = len;
   int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) {
-    *err = "no HIP device " + std::to_string(device) + " (libhbam has no CPU path)";
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= o.device || o.device < 0) {
+    *err = "no HIP device " + std::to_string(o.device) + " (libhbam has no CPU path)";
     return kErrDevice;
   }
-  f->pipe_.reset(new hbam::Pipeline(device));
-  if (!f->pipe_->error().empty()) {
-    *err = f->pipe_->error();
+  if (hipSetDevice(o.device) != hipSuccess || f->src_.dev.reserve(len + hbam::kFilePad) != hipSuccess ||
+      (len && hipMemcpy(f->src_.dev.p, data, len, hipMemcpyHostToDevice) != hipSuccess) ||
+      hipMemset(f->src_.dev.p + len, 0, hbam::kFilePad) != hipSuccess) {
+    *err = "cannot make the file resident in HBM";
     return kErrDevice;
   }
-  int rc = f->pipe_->load(f->file_.data(), len, 0);
-  if (rc == kOk) rc = f->pipe_->locate();
+  f->src_.dev_lo = 0;
+  f->src_.dev_hi = len;
+  f->src_.bytes_read = len;
+  int rc = f->init(o, err);
+  if (rc == kOk) *out = std::move(f);
+  return rc;
+}
+
+int BamFile::init(const OpenOptions& o, std::string* err) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= o.device || o.device < 0) {
+    *err = "no HIP device " + std::to_string(o.device) + " (libhbam has no CPU path)";
+    return kErrDevice;
+  }
+  pipe_.reset(new hbam::Pipeline(o.device));
+  if (!pipe_->error().empty()) {
+    *err = pipe_->error();
+    return kErrDevice;
+  }
+  pipe_->set_stringency(o.stringency);
+  set_window_bytes(o.window_bytes ? o.window_bytes : kDefaultWindowBytes);
+  int rc;
+  if (o.parse_header) {
+    rc = parse_header();
+  } else {  // plain BGZF: the first window's framing is checked at open
+    rc = load_window(0, std::min<uint64_t>(src_.size, window_bytes_));
+  }
+  if (rc != kOk) *err = err_;
+  return rc;
+}
+
+int BamFile::prefetch(uint64_t lo, uint64_t hi) {
+  hi = std::min(hi, src_.size);
+  if (lo >= hi) return kOk;
+  if (!src_.host) {
+    err_ = "prefetch needs a host copy of the file";
+    return kErrState;
+  }
+  if (hipSetDevice(pipe_->device()) != hipSuccess || src_.dev.reserve(hi - lo + hbam::kFilePad) != hipSuccess ||
+      hipMemcpy(src_.dev.p, src_.host + lo, hi - lo, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(src_.dev.p + (hi - lo), 0, hbam::kFilePad) != hipSuccess) {
+    err_ = "prefetch: HIP copy failed";
+    return kErrDevice;
+  }
+  src_.dev_lo = lo;
+  src_.dev_hi = hi;
+  src_.bytes_read += hi - lo;
+  win_lo_ = ~0ull;  // the loaded window may point at the old copy
+  return kOk;
+}
+
+int BamFile::load_window(uint64_t lo, uint64_t hi, bool free_start, bool host_only) {
+  hi = std::min(hi, src_.size);
+  if (hi < lo) hi = lo;
+  const bool dev = !host_only && src_.dev.p && lo >= src_.dev_lo && lo < src_.dev_hi;
+  if (dev) hi = std::min(hi, src_.dev_hi);
+  if (lo == win_lo_ && hi == win_hi_ && free_start == win_free_) return kOk;  // already loaded and located
+  win_lo_ = ~0ull;
+  int rc;
+  if (dev) {
+    rc = pipe_->attach_device(src_.dev.p + (lo - src_.dev_lo), hi - lo, lo, hi == src_.size);
+  } else {
+    if (!src_.host) {
+      err_ = "file bytes [" + std::to_string(lo) + ", " + std::to_string(hi) + ") are not resident in HBM";
+      return kErrState;
+    }
+    rc = pipe_->load(src_.host + lo, hi - lo, lo, hi == src_.size);
+    src_.bytes_read += hi - lo;
+  }
+  if (rc == kOk) rc = pipe_->locate(free_start);
   if (rc != kOk) {
-    *err = f->pipe_->error();
+    err_ = pipe_->error();
     return rc;
   }
-  if (parse_header) {
-    rc = f->parse_header();
-    if (rc != kOk) {
-      *err = f->err_;
-      return rc;
-    }
-  }
-  *out = std::move(f);
+  win_lo_ = lo;
+  win_hi_ = hi;
+  win_free_ = free_start;
   return kOk;
 }
 
 namespace {
-// Sequential reader over the GPU-inflated stream (header parsing only).
+// Sequential reader over the current window's inflated stream (header parse).
 struct StreamCursor {
   hbam::Pipeline& p;
   uint64_t pos = 0;
@@ -88,78 +241,236 @@ int32_t rd_i32(const uint8_t* p) {
 }  // namespace
 
 // [htsjdk] BAMFileReader.readHeader: magic, l_text, text, n_ref, refs; text
-// @SQ lines, when present, must agree with the binary dictionary.
+// @SQ lines, when present, must agree with the binary dictionary.  Read from
+// a window at the start of the file that grows until the header fits.
 int BamFile::parse_header() {
-  StreamCursor c(*pipe_);
-  uint8_t b4[4];
-  uint64_t got;
-  int rc;
-  if ((rc = c.read(b4, 4, &got)) != kOk) { err_ = pipe_->error(); return rc; }
-  if (got < 4 || memcmp(b4, "BAM\1", 4) != 0) { err_ = "Invalid BAM file header"; return kErrIO; }
-  if ((rc = c.read(b4, 4, &got)) != kOk) { err_ = pipe_->error(); return rc; }
-  if (got < 4) { err_ = "Premature EOF in BAM header"; return kErrTrunc; }
-  const int32_t l_text = rd_i32(b4);
-  if (l_text < 0) { err_ = "Invalid BAM header: negative SAM header length " + std::to_string(l_text); return kErrIO; }
-  text_.assign((size_t)l_text, '\0');
-  if ((rc = c.read(reinterpret_cast<uint8_t*>(&text_[0]), (uint64_t)l_text, &got)) != kOk) { err_ = pipe_->error(); return rc; }
-  if (got < (uint64_t)l_text) { err_ = "Premature EOF in BAM header text"; return kErrTrunc; }
-  if ((rc = c.read(b4, 4, &got)) != kOk) { err_ = pipe_->error(); return rc; }
-  if (got < 4) { err_ = "Invalid BAM header: too short, no reference sequence count"; return kErrTrunc; }
-  const int32_t n_ref = rd_i32(b4);
-  if (n_ref < 0) { err_ = "Invalid BAM header: negative reference count"; return kErrIO; }
-  for (int32_t i = 0; i < n_ref; ++i) {
-    if ((rc = c.read(b4, 4, &got)) != kOk) { err_ = pipe_->error(); return rc; }
-    if (got < 4) { err_ = "Invalid reference list: EOF before reference " + std::to_string(i + 1); return kErrTrunc; }
-    const int32_t l_name = rd_i32(b4);
-    if (l_name < 0) { err_ = "negative reference name length"; return kErrIO; }
-    std::string name((size_t)l_name, '\0');
-    if ((rc = c.read(reinterpret_cast<uint8_t*>(&name[0]), (uint64_t)l_name, &got)) != kOk) { err_ = pipe_->error(); return rc; }
-    if (got < (uint64_t)l_name) { err_ = "Premature EOF in reference name"; return kErrTrunc; }
-    if (!name.empty() && name.back() == '\0') name.pop_back();
-    if ((rc = c.read(b4, 4, &got)) != kOk) { err_ = pipe_->error(); return rc; }
-    if (got < 4) { err_ = "Premature EOF in reference length"; return kErrTrunc; }
-    ref_names_.push_back(name);
-    ref_lens_.push_back(rd_i32(b4));
-  }
-  n_ref_ = n_ref;
-  header_end_ = c.pos;
-  // text @SQ lines vs binary dictionary
-  std::vector<std::pair<std::string, int64_t>> sq;
-  size_t s = 0;
-  while (s < text_.size()) {
-    size_t e = text_.find('\n', s);
-    if (e == std::string::npos) e = text_.size();
-    if (text_.compare(s, 3, "@SQ") == 0) {
-      std::string sn;
-      int64_t ln = -1;
-      size_t f = s;
-      while (f < e) {
-        size_t t = text_.find('\t', f);
-        if (t == std::string::npos || t > e) t = e;
-        if (text_.compare(f, 3, "SN:") == 0) sn = text_.substr(f + 3, t - f - 3);
-        if (text_.compare(f, 3, "LN:") == 0) ln = strtoll(text_.c_str() + f + 3, nullptr, 10);
-        f = t + 1;
+  uint64_t w = std::min<uint64_t>(src_.size, std::min<uint64_t>(window_bytes_, 1ull << 20));
+  for (;;) {
+    int rc = load_window(0, w);
+    if (rc != kOk) return rc;
+    const bool whole = pipe_->at_eof();
+    StreamCursor c(*pipe_);
+    uint8_t b4[4];
+    uint64_t got;
+    auto more = [&](int code, const char* msg) {  // a short read in an open window: grow it
+      if (!whole) return -1;
+      err_ = msg;
+      return code;
+    };
+    text_.clear();
+    ref_names_.clear();
+    ref_lens_.clear();
+    rc = [&]() -> int {
+      int r;
+      if ((r = c.read(b4, 4, &got)) != kOk) { err_ = pipe_->error(); return r; }
+      if (got < 4) return more(kErrIO, "Invalid BAM file header");
+      if (memcmp(b4, "BAM\1", 4) != 0) { err_ = "Invalid BAM file header"; return kErrIO; }
+      if ((r = c.read(b4, 4, &got)) != kOk) { err_ = pipe_->error(); return r; }
+      if (got < 4) return more(kErrTrunc, "Premature EOF in BAM header");
+      const int32_t l_text = rd_i32(b4);
+      if (l_text < 0) { err_ = "Invalid BAM header: negative SAM header length " + std::to_string(l_text); return kErrIO; }
+      text_.assign((size_t)l_text, '\0');
+      if ((r = c.read(reinterpret_cast<uint8_t*>(&text_[0]), (uint64_t)l_text, &got)) != kOk) { err_ = pipe_->error(); return r; }
+      if (got < (uint64_t)l_text) return more(kErrTrunc, "Premature EOF in BAM header text");
+      if ((r = c.read(b4, 4, &got)) != kOk) { err_ = pipe_->error(); return r; }
+      if (got < 4) return more(kErrTrunc, "Invalid BAM header: too short, no reference sequence count");
+      const int32_t n_ref = rd_i32(b4);
+      if (n_ref < 0) { err_ = "Invalid BAM header: negative reference count"; return kErrIO; }
+      for (int32_t i = 0; i < n_ref; ++i) {
+        if ((r = c.read(b4, 4, &got)) != kOk) { err_ = pipe_->error(); return r; }
+        if (got < 4) return more(kErrTrunc, "Invalid reference list: EOF before reference");
+        const int32_t l_name = rd_i32(b4);
+        if (l_name < 0) { err_ = "negative reference name length"; return kErrIO; }
+        std::string name((size_t)l_name, '\0');
+        if ((r = c.read(reinterpret_cast<uint8_t*>(&name[0]), (uint64_t)l_name, &got)) != kOk) { err_ = pipe_->error(); return r; }
+        if (got < (uint64_t)l_name) return more(kErrTrunc, "Premature EOF in reference name");
+        if (!name.empty() && name.back() == '\0') name.pop_back();
+        if ((r = c.read(b4, 4, &got)) != kOk) { err_ = pipe_->error(); return r; }
+        if (got < 4) return more(kErrTrunc, "Premature EOF in reference length");
+        ref_names_.push_back(name);
+        ref_lens_.push_back(rd_i32(b4));
       }
-      sq.emplace_back(sn, ln);
+      n_ref_ = n_ref;
+      return kOk;
+    }();
+    if (rc == -1) {  // the header runs past this window
+      if (w >= src_.size) return kErrTrunc;
+      w = std::min<uint64_t>(src_.size, 2 * w);
+      continue;
     }
-    s = e + 1;
-  }
-  if (!sq.empty()) {
-    if ((int32_t)sq.size() != n_ref) {
-      err_ = "Number of sequences in text header (" + std::to_string(sq.size()) +
-             ") != number of sequences in binary header (" + std::to_string(n_ref) + ")";
-      return kErrFormat;
+    if (rc != kOk) return rc;
+    const uint64_t header_end = c.pos;
+    // text @SQ lines vs binary dictionary
+    std::vector<std::pair<std::string, int64_t>> sq;
+    size_t s = 0;
+    while (s < text_.size()) {
+      size_t e = text_.find('\n', s);
+      if (e == std::string::npos) e = text_.size();
+      if (text_.compare(s, 3, "@SQ") == 0) {
+        std::string sn;
+        int64_t ln = -1;
+        size_t f = s;
+        while (f < e) {
+          size_t t = text_.find('\t', f);
+          if (t == std::string::npos || t > e) t = e;
+          if (text_.compare(f, 3, "SN:") == 0) sn = text_.substr(f + 3, t - f - 3);
+          if (text_.compare(f, 3, "LN:") == 0) ln = strtoll(text_.c_str() + f + 3, nullptr, 10);
+          f = t + 1;
+        }
+        sq.emplace_back(sn, ln);
+      }
+      s = e + 1;
     }
-    for (int32_t i = 0; i < n_ref; ++i) {
-      if (sq[i].first != ref_names_[i] || sq[i].second != ref_lens_[i]) {
-        err_ = "Sequence " + std::to_string(i) + " in text header does not match binary header";
+    if (!sq.empty()) {
+      if ((int32_t)sq.size() != n_ref_) {
+        err_ = "Number of sequences in text header (" + std::to_string(sq.size()) +
+               ") != number of sequences in binary header (" + std::to_string(n_ref_) + ")";
         return kErrFormat;
       }
+      for (int32_t i = 0; i < n_ref_; ++i) {
+        if (sq[i].first != ref_names_[i] || sq[i].second != ref_lens_[i]) {
+          err_ = "Sequence " + std::to_string(i) + " in text header does not match binary header";
+          return kErrFormat;
+        }
+      }
     }
+    pipe_->set_n_ref(n_ref_);
+    rc = pipe_->set_ref_lengths(ref_lens_);
+    if (rc != kOk) {
+      err_ = pipe_->error();
+      return rc;
+    }
+    first_voff_ = pipe_->voff_of(header_end);
+    return kOk;
   }
-  pipe_->set_n_ref(n_ref_);
-  first_voff_ = pipe_->voff_of(header_end_);
+}
+
+int BamFile::decode_step(const Carry& from, uint64_t vend, hbam::ChainMode mode, bool decode, bool continuation,
+                         Step* out) {
+  *out = Step();
+  Carry c = from;
+  uint64_t span_w = window_bytes_;
+  bool host_only = false;
+  for (int guard = 0; guard < 96; ++guard) {
+    out->next = c;
+    if (c.upos <= 0xffff && c.voff() >= vend) return kOk;  // the split ends here
+    if (c.coff >= src_.size) return kOk;                    // past the last block: end of stream
+    int rc = load_window(c.coff, c.coff + span_w, false, host_only);
+    if (rc != kOk) return rc;
+    hbam::Pipeline& p = *pipe_;
+    const auto& B = p.blocks();
+    if (B.empty()) {
+      if (p.at_eof()) return kOk;  // no complete block left
+      span_w *= 2;                 // a block longer than the window
+      continue;
+    }
+    if (B[0].coff != c.coff || (!continuation && c.upos > B[0].isize)) {
+      err_ = "Invalid file pointer: " + std::to_string(c.voff());
+      return kErrIO;
+    }
+    // [htsjdk] an empty block right after an exhausted one reads as EOF
+    if (continuation && c.upos == 0 && B[0].isize == 0) return kOk;
+    const uint64_t p0 = c.upos;
+    if (p0 > p.total_u() || (p0 == p.total_u() && !p.at_eof())) {
+      // the indexer skipped past this window (a record longer than it)
+      if (p.at_eof()) {
+        out->status = kErrIO;
+        out->error = "Skip failed: record runs past the end of the file";
+        return kOk;
+      }
+      c = Carry{p.window_end(), p0 - p.total_u()};
+      continuation = true;
+      continue;
+    }
+    SpanDev s;
+    rc = p.decode_span_pos(p0, vend, mode, decode, &s);
+    if (rc != kOk) {
+      err_ = p.error();
+      return rc;
+    }
+    if (s.status == kOk && s.n == 0 && s.next_pos == p0 && p0 < s.q_end && !p.at_eof()) {
+      // the first record does not end inside this window: a bigger one
+      if (win_hi_ < std::min(src_.size, c.coff + span_w)) host_only = true;  // clipped by the HBM-resident range
+      else span_w *= 2;
+      continue;
+    }
+    out->span = s;
+    out->status = s.status;
+    out->error = s.error;
+    const uint64_t np = s.next_pos;
+    if (np < p.total_u()) {
+      const uint64_t v = p.voff_of(np);
+      out->next = Carry{v >> 16, v & 0xffff};
+    } else {
+      out->next = Carry{p.window_end(), np - p.total_u()};
+    }
+    bool ended = s.status != kOk || np >= s.q_end || (p.at_eof() && np >= p.total_u());
+    if (!ended) {  // stopped at a dead position: an empty block k >= 1 starts there (finish_blocks)
+      auto it = std::lower_bound(B.begin(), B.end(), np, [](const BlockInfo& b, uint64_t x) { return b.ustart < x; });
+      for (; it != B.end() && it->ustart == np && !ended; ++it)
+        if (it != B.begin() && it->isize == 0) ended = true;
+    }
+    out->ended = ended;
+    return kOk;
+  }
+  err_ = "window planning did not converge";
+  return kErrState;
+}
+
+int BamFile::all_blocks(const std::vector<BlockInfo>** out) {
+  if (!have_all_blocks_) {
+    all_blocks_.clear();
+    uint64_t lo = 0, ubase = 0, w = window_bytes_;
+    while (lo < src_.size) {
+      int rc = load_window(lo, lo + w);
+      if (rc != kOk) return rc;
+      const auto& B = pipe_->blocks();
+      if (B.empty() && !pipe_->at_eof()) {
+        w *= 2;
+        continue;
+      }
+      for (BlockInfo b : B) {
+        b.ustart += ubase;
+        all_blocks_.push_back(b);
+      }
+      ubase += pipe_->total_u();
+      if (pipe_->at_eof()) break;
+      lo = pipe_->window_end();
+      w = window_bytes_;
+    }
+    have_all_blocks_ = true;
+  }
+  *out = &all_blocks_;
   return kOk;
+}
+
+int BamFile::read_inflated(uint64_t pos, uint64_t len, std::vector<uint8_t>* out) {
+  out->clear();
+  const std::vector<BlockInfo>* B = nullptr;
+  int rc = all_blocks(&B);
+  if (rc != kOk) return rc;
+  if (len == 0 || B->empty()) return kOk;
+  const BlockInfo& last = B->back();
+  const uint64_t total = last.ustart + last.isize;
+  if (pos >= total) return kOk;
+  len = std::min(len, total - pos);
+  auto first_ending_after = [&](uint64_t q) {
+    return std::lower_bound(B->begin(), B->end(), q,
+                            [](const BlockInfo& b, uint64_t x) { return b.ustart + b.isize <= x; });
+  };
+  auto a = first_ending_after(pos), e = first_ending_after(pos + len - 1);
+  rc = load_window(a->coff, e->coff + e->csize);
+  if (rc != kOk) return rc;
+  rc = pipe_->read_stream(pos - a->ustart, len, out);
+  if (rc != kOk) err_ = pipe_->error();
+  return rc;
+}
+
+uint64_t BamFile::block_end_of(uint64_t pos) const {
+  const auto& B = pipe_->blocks();
+  const uint32_t k = pipe_->block_containing(pos);
+  if (k >= B.size()) return pipe_->window_end();
+  return B[k].coff + B[k].csize;
 }
 
 // ---------------------------------------------------------------------------
@@ -215,27 +526,34 @@ int SplittingBAMIndexer::index(BamFile& f, int32_t g, std::vector<uint8_t>* out)
     f.error() = "Granularity must be a positive integer";
     return kErrArg;
   }
-  SpanDev span;
-  // the chain starts at the header end (skipToAlignmentList :292-328)
-  int rc = f.pipe().decode_span(f.first_record_voff(), ~0ull, hbam::kIndexer, false, &span);
-  if (rc != kOk) {
-    f.error() = f.pipe().error();
-    return rc;
-  }
-  if (span.status != kOk) {
-    f.error() = span.error;
-    return span.status;
-  }
+  put_be64(out, f.first_record_voff());  // :262-264
+  // the chain starts at the header end (skipToAlignmentList :292-328) and
+  // runs window by window; record ordinals continue across windows
+  const uint64_t fv = f.first_record_voff();
+  Carry c{fv >> 16, fv & 0xffff};
+  bool cont = false;
+  uint64_t ordinal = 0;
   std::vector<uint64_t> ent;
-  rc = f.pipe().splitting_entries(span, (uint32_t)g, &ent);
-  if (rc != kOk) {
-    f.error() = f.pipe().error();
-    return rc;
+  for (;;) {
+    Step st;
+    int rc = f.decode_step(c, ~0ull, hbam::kIndexer, false, cont, &st);
+    if (rc != kOk) return rc;
+    if (st.status != kOk) {
+      f.error() = st.error;
+      return st.status;
+    }
+    rc = f.pipe().splitting_entries(st.span, (uint32_t)g, ordinal, &ent);
+    if (rc != kOk) {
+      f.error() = f.pipe().error();
+      return rc;
+    }
+    for (uint64_t v : ent) put_be64(out, v);  // :273-277
+    ordinal += st.span.n;
+    if (st.ended) break;
+    c = st.next;
+    cont = true;
   }
-  out->reserve(8 * (ent.size() + 2));
-  put_be64(out, f.first_record_voff());       // :262-264
-  for (uint64_t v : ent) put_be64(out, v);     // :273-277
-  put_be64(out, f.file_size() << 16);          // :286
+  put_be64(out, f.file_size() << 16);  // :286
   return kOk;
 }
 
@@ -342,106 +660,249 @@ int BAMInputFormat::getSplits(BamFile& f, const std::vector<FileSplit>& splits, 
 }
 
 // ---------------------------------------------------------------------------
-// BAMRecordReader
+// Host batches, the span cursor, BAMRecordReader
 // ---------------------------------------------------------------------------
-int fetch_span(hbam::Pipeline& p, const SpanDev& s, BAMRecordReader::Host* h, std::string* err) {
-  const uint64_t n = s.n;
-  auto cp = [&](auto& vec, const auto* src) -> int {
-    vec.resize(n);
-    if (n == 0) return kOk;
-    if (hipMemcpyAsync(vec.data(), src, n * sizeof(vec[0]), hipMemcpyDeviceToHost, p.stream()) != hipSuccess) {
-      *err = "hipMemcpy D2H failed";
-      return kErrDevice;
-    }
-    return kOk;
-  };
+int HostBatch::reserve(uint64_t nn, uint64_t bytes) {
+  bool ok = ref_id.resize(nn) && pos.resize(nn) && l_seq.resize(nn) && next_ref_id.resize(nn) &&
+            next_pos.resize(nn) && tlen.resize(nn) && l_read_name.resize(nn) && mapq.resize(nn) && bin.resize(nn) &&
+            n_cigar.resize(nn) && flag.resize(nn) && key.resize(nn) && voff.resize(nn) && rest_off.resize(nn) &&
+            rest_len.resize(nn) && data.resize(bytes);
+  return ok ? kOk : kErrNoMem;
+}
+
+int fetch_span(hbam::Pipeline& p, const SpanDev& s, uint64_t k, uint64_t m, HostBatch* h, std::string* err) {
+  if (m == 0) return kOk;
+  const hipStream_t st = p.stream();
   const hbam::Columns& c = s.col;
-  int rc = kOk;
-  rc |= cp(h->ref_id, c.ref_id);
-  rc |= cp(h->pos, c.pos);
-  rc |= cp(h->l_seq, c.l_seq);
-  rc |= cp(h->next_ref_id, c.next_ref_id);
-  rc |= cp(h->next_pos, c.next_pos);
-  rc |= cp(h->tlen, c.tlen);
-  rc |= cp(h->l_read_name, c.l_read_name);
-  rc |= cp(h->mapq, c.mapq);
-  rc |= cp(h->bin, c.bin);
-  rc |= cp(h->n_cigar, c.n_cigar);
-  rc |= cp(h->flag, c.flag);
-  rc |= cp(h->key, c.key);
-  rc |= cp(h->voff, c.voff);
-  rc |= cp(h->rest_off, c.rest_off);
-  rc |= cp(h->rest_len, c.rest_len);
-  if (rc != kOk) return kErrDevice;
-  if (hipStreamSynchronize(p.stream()) != hipSuccess) {
-    *err = "hipStreamSynchronize failed";
+  uint64_t lo = 0, last_off = 0;
+  uint32_t last_len = 0;
+  if (hipMemcpyAsync(&lo, s.rec_pos + k, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(&last_off, c.rest_off + k + m - 1, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(&last_len, c.rest_len + k + m - 1, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    *err = "hipMemcpy D2H failed";
     return kErrDevice;
   }
-  // inflated bytes of the span: [p0, end of the last record)
-  uint64_t lo = s.p0, hi = s.p0;
-  if (n) hi = h->rest_off[n - 1] + h->rest_len[n - 1];
-  h->data.resize(hi - lo);
-  if (hi > lo) {
-    if (hipMemcpy(h->data.data(), (s.data ? s.data : p.d_u()) + lo, hi - lo, hipMemcpyDeviceToHost) != hipSuccess) {
+  const uint64_t hi = last_off + last_len, n0 = h->n, d0 = h->data_len;
+  if (h->reserve(n0 + m, d0 + (hi - lo)) != kOk) {
+    *err = "page-locked host memory for the batch";
+    return kErrNoMem;
+  }
+  bool ok = true;
+  auto cp = [&](auto& vec, const auto* src) {
+    ok = ok && hipMemcpyAsync(vec.data() + n0, src + k, m * sizeof(vec[0]), hipMemcpyDeviceToHost, st) == hipSuccess;
+  };
+  cp(h->ref_id, c.ref_id);
+  cp(h->pos, c.pos);
+  cp(h->l_seq, c.l_seq);
+  cp(h->next_ref_id, c.next_ref_id);
+  cp(h->next_pos, c.next_pos);
+  cp(h->tlen, c.tlen);
+  cp(h->l_read_name, c.l_read_name);
+  cp(h->mapq, c.mapq);
+  cp(h->bin, c.bin);
+  cp(h->n_cigar, c.n_cigar);
+  cp(h->flag, c.flag);
+  cp(h->key, c.key);
+  cp(h->voff, c.voff);
+  cp(h->rest_off, c.rest_off);
+  cp(h->rest_len, c.rest_len);
+  const uint8_t* src = s.data ? s.data : p.d_u();
+  if (hi > lo)
+    ok = ok && hipMemcpyAsync(h->data.data() + d0, src + lo, hi - lo, hipMemcpyDeviceToHost, st) == hipSuccess;
+  if (!ok || hipStreamSynchronize(st) != hipSuccess) {
+    *err = "hipMemcpy D2H failed";
+    return kErrDevice;
+  }
+  for (uint64_t i = n0; i < n0 + m; ++i) h->rest_off[i] = h->rest_off[i] - lo + d0;
+  h->window_pos.push_back(lo - d0);  // window position = rest_off + this (segment base)
+  h->n = n0 + m;
+  h->data_len = d0 + (hi - lo);
+  return kOk;
+}
+
+static hbam::Columns offset_columns(const hbam::Columns& c, uint64_t k) {
+  hbam::Columns o = c;
+  o.ref_id += k;
+  o.pos += k;
+  o.l_seq += k;
+  o.next_ref_id += k;
+  o.next_pos += k;
+  o.tlen += k;
+  o.l_read_name += k;
+  o.mapq += k;
+  o.bin += k;
+  o.n_cigar += k;
+  o.flag += k;
+  o.key += k;
+  o.voff += k;
+  o.rest_off += k;
+  o.rest_len += k;
+  return o;
+}
+
+int SpanCursor::next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t max_records, HostBatch* h,
+                           uint64_t* next_voff, std::string* err) {
+  h->n = 0;
+  h->data_len = 0;
+  h->window_pos.clear();
+  batch_one_window_ = false;
+  batch_end_pos_.clear();
+  const bool cont = valid_ && vend == vend_ && vstart == next_voff_;
+  if (!cont) {  // a seek to the split start (or anywhere in it)
+    valid_ = true;
+    vend_ = vend;
+    k_ = 0;
+    const int rc = f.decode_step(Carry{vstart >> 16, vstart & 0xffff}, vend, hbam::kReader, true, false, &step_);
+    if (rc != kOk) {
+      valid_ = false;
+      *err = f.error();
+      return rc;
+    }
+  }
+  int status = kOk;
+  for (;;) {
+    const uint64_t avail = step_.span.n - k_;
+    if (avail == 0) {
+      if (step_.ended) {
+        status = step_.status;
+        if (status != kOk) *err = step_.error;
+        break;
+      }
+      if (h->n && max_records) break;  // bounded batches stay inside one window
+      const int rc = f.decode_step(step_.next, vend, hbam::kReader, true, true, &step_);
+      k_ = 0;
+      if (rc != kOk) {
+        valid_ = false;
+        *err = f.error();
+        return rc;
+      }
+      continue;
+    }
+    const uint64_t m = max_records ? std::min(max_records - h->n, avail) : avail;
+    const bool first_segment = h->n == 0;
+    int rc = fetch_span(f.pipe(), step_.span, k_, m, h, err);
+    if (rc != kOk) return rc;
+    if (first_segment) {
+      batch_k0_ = k_;
+      batch_n_ = m;
+      batch_one_window_ = true;
+    } else {
+      batch_one_window_ = false;
+    }
+    k_ += m;
+    if (max_records && h->n >= max_records) break;
+  }
+  if (k_ < step_.span.n) {
+    uint64_t v = 0;
+    if (hipMemcpy(&v, step_.span.rec_voff + k_, 8, hipMemcpyDeviceToHost) != hipSuccess) {
       *err = "hipMemcpy D2H failed";
       return kErrDevice;
     }
+    *next_voff = v;
+  } else if (!step_.ended || status != kOk) {
+    *next_voff = step_.next.voff();
+  } else {
+    *next_voff = vend;
   }
-  for (uint64_t i = 0; i < n; ++i) h->rest_off[i] -= lo;
-  return kOk;
+  next_voff_ = *next_voff;
+  if (batch_one_window_) {  // last byte of each record (+ the read-ahead one) for reader_position
+    const uint64_t base = h->window_pos.empty() ? 0 : h->window_pos[0];
+    batch_end_pos_.resize(h->n + 1);
+    for (uint64_t i = 0; i < h->n; ++i) batch_end_pos_[i] = base + h->rest_off[i] + h->rest_len[i] - 1;
+    batch_end_pos_[h->n] = ~0ull;
+    if (k_ < step_.span.n) {
+      uint64_t ro = 0;
+      uint32_t rl = 0;
+      if (hipMemcpy(&ro, step_.span.col.rest_off + k_, 8, hipMemcpyDeviceToHost) == hipSuccess &&
+          hipMemcpy(&rl, step_.span.col.rest_len + k_, 4, hipMemcpyDeviceToHost) == hipSuccess)
+        batch_end_pos_[h->n] = ro + rl - 1;
+    }
+  }
+  return status;
+}
+
+bool SpanCursor::last_batch_span(SpanDev* out) const {
+  if (!valid_ || !batch_one_window_) return false;
+  *out = step_.span;
+  out->n = batch_n_;
+  out->rec_pos = step_.span.rec_pos + batch_k0_;
+  out->rec_voff = step_.span.rec_voff + batch_k0_;
+  out->col = offset_columns(step_.span.col, batch_k0_);
+  return true;
+}
+
+uint64_t SpanCursor::reader_position(BamFile& f, uint64_t i) const {
+  // BAMRecordReader.getProgress (:209-219) reads in.position(): htsjdk's
+  // iterator has already read the record after the one just returned (when
+  // the split holds one), so the stream stands at the end of the block
+  // holding that record's last byte.
+  if (batch_end_pos_.empty()) return 0;
+  uint64_t pos = i + 1 < batch_end_pos_.size() ? batch_end_pos_[i + 1] : ~0ull;
+  if (pos == ~0ull) pos = batch_end_pos_[std::min<uint64_t>(i, batch_end_pos_.size() - 2)];
+  return f.block_end_of(pos);
 }
 
 int BAMRecordReader::initialize(BamFile& f, const FileVirtualSplit& split) {
   // :131-133 re-entrant initialize
-  *this = BAMRecordReader();
-  const uint64_t vs = split.getStartVirtualOffset();
-  fileStart_ = vs >> 16;                     // :153
-  virtualEnd_ = split.getEndVirtualOffset(); // :154
-  SpanDev span;
-  int rc = f.pipe().decode_span(vs, virtualEnd_, hbam::kReader, true, &span);
-  if (rc != kOk) {
-    err_ = f.pipe().error();
-    status_ = rc;
-    return rc;
-  }
-  rc = fetch_span(f.pipe(), span, &h_, &err_);
-  if (rc != kOk) {
-    status_ = rc;
-    return rc;
-  }
-  n_ = span.n;
-  status_ = span.status;
-  if (status_ != kOk) err_ = span.error;
-  return kOk;
+  f_ = &f;
+  cur_span_.reset();
+  b_.n = 0;
+  cur_ = 0;
+  started_ = reached_end_ = have_batch_ = false;
+  status_ = kOk;
+  err_.clear();
+  fileStart_ = split.getStartVirtualOffset() >> 16;  // :153
+  virtualEnd_ = split.getEndVirtualOffset();         // :154
+  next_voff_ = split.getStartVirtualOffset();
+  // the iterator reads its first record in initialize (htsjdk's
+  // BAMFileIndexIterator constructor advances once)
+  fill();
+  return status_ == kOk || b_.n > 0 ? kOk : status_;
+}
+
+bool BAMRecordReader::fill() {
+  if (have_batch_ && (status_ != kOk || next_voff_ >= virtualEnd_)) return false;
+  const int rc = cur_span_.next_batch(*f_, next_voff_, virtualEnd_, kBatchRecords, &b_, &next_voff_, &err_);
+  have_batch_ = true;
+  cur_ = 0;
+  if (rc != kOk) status_ = rc;
+  return b_.n > 0;
 }
 
 bool BAMRecordReader::nextKeyValue() {
+  if (reached_end_) return false;
   if (started_) ++cur_;
   started_ = true;
-  if (cur_ >= n_) return false;  // status() tells a clean end from an error
-  view_.refID = h_.ref_id[cur_];
-  view_.pos = h_.pos[cur_];
-  view_.l_seq = h_.l_seq[cur_];
-  view_.next_refID = h_.next_ref_id[cur_];
-  view_.next_pos = h_.next_pos[cur_];
-  view_.tlen = h_.tlen[cur_];
-  view_.l_read_name = h_.l_read_name[cur_];
-  view_.mapq = h_.mapq[cur_];
-  view_.bin = h_.bin[cur_];
-  view_.n_cigar = h_.n_cigar[cur_];
-  view_.flag = h_.flag[cur_];
-  view_.voff = h_.voff[cur_];
-  view_.rest = h_.data.data() + h_.rest_off[cur_];
-  view_.rest_len = h_.rest_len[cur_];
-  lastVoff_ = view_.voff;
+  if (cur_ >= b_.n && !fill()) {
+    reached_end_ = true;
+    return false;  // status() tells a clean end from an error
+  }
+  view_.refID = b_.ref_id[cur_];
+  view_.pos = b_.pos[cur_];
+  view_.l_seq = b_.l_seq[cur_];
+  view_.next_refID = b_.next_ref_id[cur_];
+  view_.next_pos = b_.next_pos[cur_];
+  view_.tlen = b_.tlen[cur_];
+  view_.l_read_name = b_.l_read_name[cur_];
+  view_.mapq = b_.mapq[cur_];
+  view_.bin = b_.bin[cur_];
+  view_.n_cigar = b_.n_cigar[cur_];
+  view_.flag = b_.flag[cur_];
+  view_.voff = b_.voff[cur_];
+  view_.rest = b_.data.data() + b_.rest_off[cur_];
+  view_.rest_len = b_.rest_len[cur_];
   return true;
 }
 
 float BAMRecordReader::getProgress() const {
-  if (started_ && cur_ >= n_) return 1.0f;
-  const uint64_t filePos = lastVoff_ >> 16, fileEnd = virtualEnd_ >> 16;
-  if (filePos < fileStart_) return 0.0f;
-  return (float)(filePos - fileStart_) / (float)(fileEnd - fileStart_ + 1);
+  if (reached_end_) return 1.0f;
+  const uint64_t fileEnd = virtualEnd_ >> 16;
+  if (b_.n == 0) return 0.0f;
+  // before the first nextKeyValue the iterator has read record 0
+  const uint64_t filePos = started_ ? cur_span_.reader_position(*f_, cur_) : f_->block_end_of(
+      b_.window_pos.empty() ? 0 : b_.window_pos[0] + b_.rest_off[0] + b_.rest_len[0] - 1);
+  return (float)((double)((int64_t)filePos - (int64_t)fileStart_) / (double)(fileEnd - fileStart_ + 1));
 }
 
 // ---------------------------------------------------------------------------

@@ -11,6 +11,14 @@
 // Names, argument meaning and error behaviour follow the Java classes; Java
 // exceptions become status codes (hbam.h) and the message is kept in
 // BamFile::error().
+//
+// A BamFile reads its compressed bytes the way BAMRecordReader reads a split
+// through WrapSeekable (WrapSeekable.java:42-87): only the byte ranges a
+// decode touches are copied into an HBM window (or attached from a
+// device-resident copy), never the whole file up front.  A span is decoded
+// window by window; the next record's position is carried from one window to
+// the next, so device memory is bounded by the window size whatever the file
+// size.
 #pragma once
 #include <stdint.h>
 
@@ -26,15 +34,84 @@ namespace hadoop_bam {
 
 using hbam::SpanDev;
 
-// One opened BAM (or BGZF) file: host bytes + the device pipeline + header.
+constexpr uint64_t kDefaultWindowBytes = 4ull << 30;  // hadoopbam.gpu.window-bytes default
+
+// Page-locked host array (batch columns handed to a JNI caller as direct
+// ByteBuffers; D2H copies into it run at the PCIe rate).
+template <typename T>
+class PinnedVec {
+ public:
+  PinnedVec() = default;
+  PinnedVec(const PinnedVec&) = delete;
+  PinnedVec& operator=(const PinnedVec&) = delete;
+  ~PinnedVec() { release(); }
+  bool resize(size_t n);  // contents not kept on growth
+  size_t size() const { return n_; }
+  T* data() { return p_; }
+  const T* data() const { return p_; }
+  T& operator[](size_t i) { return p_[i]; }
+  const T& operator[](size_t i) const { return p_[i]; }
+  void release();
+
+ private:
+  T* p_ = nullptr;
+  size_t n_ = 0, cap_ = 0;
+};
+
+// Where a BamFile's compressed bytes come from.
+struct Source {
+  const uint8_t* host = nullptr;  // the whole file in host address space (copy or mmap); nullptr: device only
+  uint64_t size = 0;              // file length
+  std::vector<uint8_t> owned;     // hbam_open_mem copy
+  void* map = nullptr;            // hbam_open: read-only mmap of the path
+  size_t map_len = 0;
+  hbam::DevBuf<uint8_t> dev;      // device-resident bytes [dev_lo, dev_hi) (+ kFilePad zeros)
+  uint64_t dev_lo = 0, dev_hi = 0;
+  uint64_t bytes_read = 0;        // host -> HBM bytes copied so far (window loads + prefetch)
+  ~Source();
+};
+
+// Where a span continues: the block at file offset coff, stream offset upos
+// from its start (a voff when upos <= 0xffff; the indexer's skip of a record
+// longer than a window may carry further).
+struct Carry {
+  uint64_t coff = 0, upos = 0;
+  uint64_t voff() const { return (coff << 16) | (upos & 0xffff); }
+};
+
+// One window's part of a span.
+struct Step {
+  SpanDev span;             // records of this window (device)
+  Carry next;               // where the span continues
+  bool ended = true;        // span exhausted (span end, end of stream, error)
+  int status = 0;           // status of the record that ended the span early
+  std::string error;
+};
+
+struct OpenOptions {
+  int device = 0;
+  bool parse_header = true;
+  bool check_crc = false;
+  int stringency = hbam::kStrict;
+  uint64_t window_bytes = kDefaultWindowBytes;
+};
+
+// One opened BAM (or BGZF) file on one GPU.
 class BamFile {
  public:
-  static int open(const uint8_t* data, uint64_t len, int device, bool parse_header, bool check_crc,
-                  std::unique_ptr<BamFile>* out, std::string* err);
+  // whole-file sources: an in-memory copy, an mmap of a path, or a device
+  // copy of host bytes (hbam_gpu: the file resident in HBM)
+  static int open_memory(const uint8_t* data, uint64_t len, const OpenOptions& o, std::unique_ptr<BamFile>* out,
+                         std::string* err);
+  static int open_path(const char* path, const OpenOptions& o, std::unique_ptr<BamFile>* out, std::string* err);
+  static int open_device_copy(const uint8_t* data, uint64_t len, const OpenOptions& o, std::unique_ptr<BamFile>* out,
+                              std::string* err);
 
-  const std::vector<uint8_t>& bytes() const { return file_; }
   hbam::Pipeline& pipe() { return *pipe_; }
-  uint64_t file_size() const { return file_.size(); }
+  uint64_t file_size() const { return src_.size; }
+  uint64_t bytes_read() const { return src_.bytes_read; }
+  uint64_t window_bytes() const { return window_bytes_; }
+  void set_window_bytes(uint64_t w) { window_bytes_ = w < (1ull << 16) ? (1ull << 16) : w; }
 
   // [htsjdk] BAMFileReader.readHeader results
   int32_t n_ref() const { return n_ref_; }
@@ -42,20 +119,48 @@ class BamFile {
   const std::string& text() const { return text_; }
   const std::vector<std::string>& ref_names() const { return ref_names_; }
   const std::vector<int32_t>& ref_lens() const { return ref_lens_; }
-  uint64_t header_end() const { return header_end_; }
   uint64_t first_record_voff() const { return first_voff_; }
 
   std::string& error() { return err_; }
 
+  // Copy file bytes [lo, hi) into HBM now; windows inside the range then
+  // attach to it instead of reading the host (bench: inputs resident in HBM).
+  int prefetch(uint64_t lo, uint64_t hi);
+  // the next load re-attaches / re-copies and re-locates (timed passes)
+  void invalidate_window() { win_lo_ = ~0ull; }
+  // Load the window [lo, hi) (clipped to the file) and locate its blocks.
+  int load_window(uint64_t lo, uint64_t hi, bool free_start = false, bool host_only = false);
+
+  // Decode the part of FileVirtualSplit [.., vend) that starts at `from`
+  // and lies in one window.  continuation: `from` is the carry of the
+  // previous step (not a reader seek).
+  int decode_step(const Carry& from, uint64_t vend, hbam::ChainMode mode, bool decode, bool continuation,
+                  Step* out);
+
+  // Every BGZF block of the file (window by window; cached).  ustart is the
+  // offset in the whole inflated stream.
+  int all_blocks(const std::vector<hbam::BlockInfo>** out);
+  // Inflated bytes [pos, pos + len) of the whole stream.
+  int read_inflated(uint64_t pos, uint64_t len, std::vector<uint8_t>* out);
+  // file offset just past the block holding window position `pos` (window of the last step)
+  uint64_t block_end_of(uint64_t pos) const;
+
  private:
+  BamFile() = default;
+  int init(const OpenOptions& o, std::string* err);
   int parse_header();
-  std::vector<uint8_t> file_;
+  Source src_;
   std::unique_ptr<hbam::Pipeline> pipe_;
+  uint64_t win_lo_ = ~0ull, win_hi_ = 0;  // the loaded window
+  bool win_free_ = false;
+  uint64_t window_bytes_ = kDefaultWindowBytes;
   int32_t n_ref_ = 0;
   std::string text_;
   std::vector<std::string> ref_names_;
   std::vector<int32_t> ref_lens_;
-  uint64_t header_end_ = 0, first_voff_ = 0;
+  uint64_t first_voff_ = 0;
+  std::vector<hbam::BlockInfo> all_blocks_;
+  bool have_all_blocks_ = false;
   std::string err_;
 };
 
@@ -100,13 +205,14 @@ class SplittingBAMIndexer {
  public:
   static constexpr int DEFAULT_GRANULARITY = 4096;  // :70
   // index(in, out, inputSize, granularity) :248-290 -- GPU record chain under
-  // the indexer's read rules, entries emitted by sbi_emit.
+  // the indexer's read rules, window by window, entries by global ordinal.
   static int index(BamFile& f, int32_t granularity, std::vector<uint8_t>* out);
-  // write-time API :175-243
+  // write-time API :175-243 (BAMRecordWriter.java:145-149 drives it): the
+  // entries of a run of record voffs, computed on the GPU (k_sbi_emit)
   explicit SplittingBAMIndexer(int32_t granularity = DEFAULT_GRANULARITY) : granularity_(granularity) {}
-  void processAlignment(uint64_t virtualOffset);  // :197-202
+  void processAlignment(uint64_t virtualOffset);    // :197-202
   void writeVirtualOffset(uint64_t virtualOffset);  // :229-232
-  void finish(uint64_t inputSize);                   // :240-243
+  void finish(uint64_t inputSize);                  // :240-243
   const std::vector<uint8_t>& bytes() const { return out_; }
 
  private:
@@ -115,7 +221,8 @@ class SplittingBAMIndexer {
   std::vector<uint8_t> out_;
 };
 
-// BAMSplitGuesser (BAMSplitGuesser.java:69-339): batched on the GPU.
+// BAMSplitGuesser (BAMSplitGuesser.java:69-339): batched on the GPU over
+// windows around the split points.
 class BAMSplitGuesser {
  public:
   explicit BAMSplitGuesser(BamFile& f) : f_(f) {}
@@ -148,64 +255,96 @@ class BAMInputFormat {
                                     std::vector<FileVirtualSplit>* out);
 };
 
-// A decoded record handed out by BAMRecordReader: the LazyBAMRecordFactory
-// argument list + the variable-length block.
-struct RecordView {
-  int32_t refID, pos, l_seq, next_refID, next_pos, tlen;
-  uint8_t l_read_name, mapq;
-  uint16_t bin, n_cigar, flag;
-  uint64_t voff;
-  const uint8_t* rest;
-  uint32_t rest_len;
-  int32_t getAlignmentStart() const { return pos + 1; }
-  int32_t getMateAlignmentStart() const { return next_pos + 1; }
+// Host copy of a run of decoded records: the LazyBAMRecordFactory argument
+// list + key + voff + the variable-length block of each record.
+struct HostBatch {
+  PinnedVec<int32_t> ref_id, pos, l_seq, next_ref_id, next_pos, tlen;
+  PinnedVec<uint8_t> l_read_name, mapq;
+  PinnedVec<uint16_t> bin, n_cigar, flag;
+  PinnedVec<int64_t> key;
+  PinnedVec<uint64_t> voff, rest_off;
+  PinnedVec<uint32_t> rest_len;
+  PinnedVec<uint8_t> data;  // inflated bytes of the records; rest_off is relative to data
+  uint64_t n = 0, data_len = 0;
+  std::vector<uint64_t> window_pos;  // window position of data[0] per window segment (progress)
+  int reserve(uint64_t n, uint64_t bytes);
+};
+
+// Records [k, k + m) of a device span appended to h at record h->n (columns
+// and their bytes; D2H on the pipeline stream into page-locked memory).
+int fetch_span(hbam::Pipeline& p, const SpanDev& s, uint64_t k, uint64_t m, HostBatch* h, std::string* err);
+
+// A split being read in bounded batches (BAMRecordReader's iterator): the
+// current window's decoded span stays on the device and batches are copied
+// out of it; the next window is decoded when the batch reaches its end.
+class SpanCursor {
+ public:
+  // Up to max_records records (0 = the rest of the split) starting at vstart;
+  // *next_voff = where the next call continues (>= vend when the split is
+  // exhausted).  A vstart equal to the previous call's *next_voff continues
+  // the same split without re-decoding.
+  int next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t max_records, HostBatch* h,
+                 uint64_t* next_voff, std::string* err);
+  // device view of the records of the last batch when they lie in one window
+  bool last_batch_span(SpanDev* out) const;
+  // BAMRecordReader.getProgress's in.position() after record i of the last batch
+  uint64_t reader_position(BamFile& f, uint64_t i) const;
+  void reset() { valid_ = false; }
+
+ private:
+  bool valid_ = false;
+  uint64_t vend_ = 0, next_voff_ = 0;
+  Step step_;
+  uint64_t k_ = 0;                    // next record of step_ to hand out
+  uint64_t batch_k0_ = 0, batch_n_ = 0;  // the last batch within step_ (single window)
+  bool batch_one_window_ = false;
+  std::vector<uint64_t> batch_end_pos_;  // window position of each batch record's last byte (+1 read-ahead)
 };
 
 // BAMRecordReader (BAMRecordReader.java:63-233) over one FileVirtualSplit.
 class BAMRecordReader {
  public:
+  static constexpr uint64_t kBatchRecords = 1 << 20;  // records per device->host batch
   // static keys :81-121
   static int64_t getKey0(int32_t refIdx, int32_t alignmentStart0) {
     return (int64_t)(((uint64_t)(int64_t)refIdx << 32) | (uint64_t)(int64_t)alignmentStart0);
   }
   static int64_t getKey(int32_t refIdx, int32_t alignmentStart) { return getKey0(refIdx, alignmentStart - 1); }
 
-  // initialize :123-184 -- decodes the whole split on the GPU
+  // initialize :123-184 -- positions the cursor at the split start; records
+  // are decoded on the GPU in batches as nextKeyValue reaches them
   int initialize(BamFile& f, const FileVirtualSplit& split);
   // nextKeyValue :223-232; returns false at the end or on error (see status())
   bool nextKeyValue();
-  int64_t getCurrentKey() const { return h_.key[cur_]; }
+  int64_t getCurrentKey() const { return b_.key[cur_]; }
+  struct RecordView {
+    int32_t refID, pos, l_seq, next_refID, next_pos, tlen;
+    uint8_t l_read_name, mapq;
+    uint16_t bin, n_cigar, flag;
+    uint64_t voff;
+    const uint8_t* rest;
+    uint32_t rest_len;
+    int32_t getAlignmentStart() const { return pos + 1; }
+    int32_t getMateAlignmentStart() const { return next_pos + 1; }
+  };
   const RecordView& getCurrentValue() const { return view_; }
   float getProgress() const;  // :209-219
   int status() const { return status_; }
   const std::string& error() const { return err_; }
   void close() {}
 
-  // bulk access (what a JNI shim hands to Java as direct ByteBuffers)
-  uint64_t size() const { return n_; }
-  struct Host {
-    std::vector<int32_t> ref_id, pos, l_seq, next_ref_id, next_pos, tlen;
-    std::vector<uint8_t> l_read_name, mapq;
-    std::vector<uint16_t> bin, n_cigar, flag;
-    std::vector<int64_t> key;
-    std::vector<uint64_t> voff, rest_off;
-    std::vector<uint32_t> rest_len;
-    std::vector<uint8_t> data;  // inflated bytes of the span; rest_off is relative to data
-  };
-  const Host& host() const { return h_; }
-
  private:
-  Host h_;
-  uint64_t n_ = 0, cur_ = 0;
-  bool started_ = false;
+  bool fill();
+  BamFile* f_ = nullptr;
+  SpanCursor cur_span_;
+  HostBatch b_;
+  uint64_t cur_ = 0, next_voff_ = 0;
+  bool started_ = false, reached_end_ = false, have_batch_ = false;
   int status_ = 0;
   std::string err_;
   RecordView view_{};
-  uint64_t fileStart_ = 0, virtualEnd_ = 0, lastVoff_ = 0;
+  uint64_t fileStart_ = 0, virtualEnd_ = 0;
 };
-
-// Fetch a span decoded on the device into host vectors.
-int fetch_span(hbam::Pipeline& p, const SpanDev& s, BAMRecordReader::Host* h, std::string* err);
 
 // MurmurHash3.murmurhash3(byte[], int) (util/MurmurHash3.java:32-102) -- scalar
 int64_t murmurhash3(const uint8_t* key, uint64_t len, int32_t seed);

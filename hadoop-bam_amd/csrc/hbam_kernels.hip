@@ -197,19 +197,12 @@ __global__ void k_block_ustart(BlockInfo* __restrict__ blocks, uint32_t n, const
 // sub-table entries carry the full code length.
 // Tokens (u32): literal  bit31=0, [25:24] count (1..2), [15:0] bytes
 //               match    bit31=1, [30:16] dist-1, [15:0] length
-#ifndef HBAM_HUFF_THREADS
-#define HBAM_HUFF_THREADS 256
-#endif
-constexpr int kHuffThreads = HBAM_HUFF_THREADS;
+constexpr int kHuffThreads = 256;
 constexpr int kHuffWaves = kHuffThreads / 64;
-#ifndef HBAM_HUFF_STAGE
-#define HBAM_HUFF_STAGE 1
-#endif
 // Phase A reads the compressed block from an LDS copy (staged) or straight
-// from HBM/L2.  1 = per chunk: staged while the workgroup's LDS (tables +
-// the chunk's largest block) leaves room for 4 workgroups per CU, else
-// unstaged (C4: 7.4 -> 3.9 ms; C2: staged 7.6 vs 8.0 ms); 0 = never, 2 = always.
-constexpr int kHuffStageMode = HBAM_HUFF_STAGE;
+// from HBM/L2, per chunk: staged while the workgroup's LDS (tables + the
+// chunk's largest block) leaves room for 4 workgroups per CU, else unstaged
+// (C4: 7.4 -> 3.9 ms; C2: staged 7.6 vs 8.0 ms).
 constexpr uint32_t kHuffStageMaxLds = 40 * 1024;
 
 // Wave-local ordering of LDS traffic (code run by one wave only).
@@ -479,10 +472,7 @@ enum { LD_SPEC = 0, LD_SYNC = 1, LD_EMIT = 2 };
 
 // Boundaries of a lane's speculative walk: p[k] = bit position after symbol
 // kMergeFirst << k, b[k] = output bytes decoded up to there (~0u = not reached).
-#ifndef HBAM_MERGE_FIRST
-#define HBAM_MERGE_FIRST 4
-#endif
-constexpr uint32_t kMergeFirst = HBAM_MERGE_FIRST;  // power of two
+constexpr uint32_t kMergeFirst = 4;  // power of two
 struct MergePts {
   uint32_t p0, p1, p2, p3;
   uint32_t b0, b1, b2, b3;
@@ -1058,42 +1048,15 @@ constexpr uint32_t kHuffLdsBytes = (sizeof(HuffLds) + 15) & ~15u;
 constexpr uint32_t kHuffCtlBytes = (sizeof(HuffCtl) + 15) & ~15u;
 constexpr uint32_t kHuffStaticBytes = kHuffLdsBytes + kHuffCtlBytes;
 
-// Per-block cycle profiles (HBAM_HUFF_PROF=1 at run time) are compiled in only
-// with -DHBAM_KPROF=1: their accumulators would otherwise stay live (22 VGPRs
-// in phase A) for the whole kernel.
-#ifndef HBAM_KPROF
-#define HBAM_KPROF 0
-#endif
-constexpr bool kProf = HBAM_KPROF != 0;
-
-#ifndef HBAM_HUFF_WPE
-#define HBAM_HUFF_WPE 5  // waves per SIMD (VGPR cap 96; measured best on C2)
-#endif
+constexpr int kHuffWavesPerSimd = 5;  // VGPR cap 96; measured best on C2
 template <bool STAGE>
-__global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(const uint8_t* __restrict__ file,
+__global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huff(const uint8_t* __restrict__ file,
                                                                const BlockInfo* __restrict__ blocks, uint32_t b0,
                                                                uint64_t chunk_ustart, uint32_t* __restrict__ tokens,
                                                                HuffOut* __restrict__ hout,
                                                                const uint8_t* __restrict__ tables,
-                                                               const HuffTableInfo* __restrict__ tinfo,
-                                                               uint64_t* __restrict__ prof) {
+                                                               const HuffTableInfo* __restrict__ tinfo) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  // optional per-block cycle profile (prof != nullptr; thread 0's clock):
-  // [0] staging [1] wave-0 headers/tables/lookahead [2] spec pass (to the first
-  // exchange) [3] sync [4] end scan [5] emit [6] result hand-back
-  // [7] of [1]: dynamic litlen/dist table builds + literal pairing
-  // [8] all-lane passes [9] sync iterations [10] total
-  if (!kProf) prof = nullptr;
-  uint64_t pacc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t pt = prof ? clock64() : 0, pt0 = pt;
-#define PROF_T(i)                           \
-  do {                                      \
-    if (prof && threadIdx.x == 0) {         \
-      const uint64_t n_ = clock64();        \
-      pacc[i] += n_ - pt;                   \
-      pt = n_;                              \
-    }                                       \
-  } while (0)
   HuffLds& L = *reinterpret_cast<HuffLds*>(smem);
   HuffCtl& C = *reinterpret_cast<HuffCtl*>(smem + kHuffLdsBytes);
   uint4* s_in = reinterpret_cast<uint4*>(smem + kHuffStaticBytes);
@@ -1119,10 +1082,7 @@ __global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(co
     const uint4* __restrict__ src = reinterpret_cast<const uint4*>(file + abase);
     const uint4* __restrict__ tsrc = reinterpret_cast<const uint4*>(tables + (uint64_t)blockIdx.x * kTableImage);
     uint4* tdst = reinterpret_cast<uint4*>(&L);
-#ifndef HBAM_STAGE_BATCH
-#define HBAM_STAGE_BATCH 4
-#endif
-    constexpr int kStageBatch = HBAM_STAGE_BATCH;
+    constexpr int kStageBatch = 4;
     for (uint32_t i0 = tid; i0 < nq + nt; i0 += kStageBatch * kHuffThreads) {
       uint4 v[kStageBatch];
 #pragma unroll
@@ -1140,7 +1100,6 @@ __global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(co
     }
   }
   __syncthreads();
-  PROF_T(0);
   // compressed bits: the LDS copy, or (unstaged) the file in HBM
   const uint32_t* __restrict__ W =
       STAGE ? reinterpret_cast<const uint32_t*>(s_in) : reinterpret_cast<const uint32_t*>(file + abase);
@@ -1293,9 +1252,7 @@ __global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(co
             }
             pair_literals(L);
           } else {  // dynamic Huffman
-            const uint64_t tb0 = prof ? clock64() : 0;
             const int dh = dyn_header(L, R, E);
-            if (prof && threadIdx.x == 0) pacc[7] += clock64() - tb0;
             if (dh == DH_TRUNC) { if (!look) err = kErrFormat; break; }
             if (dh != DH_OK) { err = kErrIO; break; }
           }
@@ -1317,10 +1274,8 @@ __global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(co
       }
       if (lane == 0) C.act = act;
     }
-    PROF_T(1);
     __syncthreads();
     if (C.act != kActDecode) break;
-    if (prof) pacc[8]++;
 
     // ---- all-lane decode of this DEFLATE block's symbols
     const uint32_t B0 = C.B0, out0 = C.out0, tok0 = C.tok0;
@@ -1332,16 +1287,12 @@ __global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(co
     uint32_t mj = 0, x, nt, nb;
     uint32_t ev = lane_decode<LD_SPEC>(L, W, a, stop, E, x, nt, nb, mp, mj, nullptr, 0, 0);
     const uint32_t sx = x, snt = nt, snb = nb, sev = ev;
-    bool first_x = true;
     for (;;) {  // sync: restart each slice from its predecessor's exit
       if (lane == 63) {
         C.xx[wave] = x;
         C.xe[wave] = ev;
       }
       __syncthreads();
-      if (first_x) PROF_T(2);
-      first_x = false;
-      if (prof) pacc[9]++;
       uint32_t px = __shfl_up(x, 1, 64), pev = __shfl_up(ev, 1, 64);
       if (lane == 0 && wave > 0) {
         px = C.xx[wave - 1];
@@ -1367,18 +1318,15 @@ __global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(co
         }
       }
     }
-    PROF_T(3);
     const uint32_t lend0 = wg_min(ev != EV_STOP ? tid : 0xffffffffu, C.red);
     const uint32_t lend = lend0 == 0xffffffffu ? (uint32_t)kHuffThreads - 1 : lend0;
     const bool valid = tid <= lend;
     uint32_t toff, boff;
     wg_excl_scan2(valid ? nt : 0u, valid ? nb : 0u, C.red, toff, boff);
-    PROF_T(4);
     uint32_t x3 = a, nt3 = 0, nb3 = 0, ev3 = EV_STOP;
     if (valid)
       ev3 = lane_decode<LD_EMIT>(L, W, a, stop, E, x3, nt3, nb3, mp, mj, tok_out + tok0 + toff, out0 + boff, isize);
     const uint32_t m3 = wg_min((valid && ev3 != EV_STOP) ? tid : 0xffffffffu, C.red);
-    PROF_T(5);
     const uint32_t f = m3 != 0xffffffffu ? m3 : lend;
     if (tid == f) {
       C.fe = ev3;
@@ -1388,18 +1336,12 @@ __global__ __launch_bounds__(kHuffThreads, HBAM_HUFF_WPE) void k_inflate_huff(co
       C.m3any = m3 != 0xffffffffu;
     }
     __syncthreads();
-    PROF_T(6);
   }
   if (tid == 0) {
     if (err == kOk && outpos < isize) err = kErrFormat;  // "Did not inflate expected amount"
     hout[bi].ntok = ntok;
     hout[bi].status = err;
-    if (prof) {
-      pacc[10] = clock64() - pt0;
-      for (int i = 0; i < 11; ++i) prof[16ull * bi + i] = pacc[i];
-    }
   }
-#undef PROF_T
 }
 
 // ---------------------------------------------------------------------------
@@ -1419,27 +1361,7 @@ constexpr int kLzThreads = 1024;
 constexpr int kLzWaves = kLzThreads / 64;
 constexpr uint32_t kMapMax = 65280;
 constexpr uint32_t kLitTag = 0xFF00u;
-// phase-B resolve: raw entries loaded this many rounds ahead (1 measured best)
-#ifndef HBAM_LZ_PF
-#define HBAM_LZ_PF 1
-#endif
-[[maybe_unused]] constexpr int kLzPf = HBAM_LZ_PF;
-// phase-B fill: 64-token groups loaded ahead (4 vs 8 measured equal)
-#ifndef HBAM_LZ_RING
-#define HBAM_LZ_RING 4
-#endif
-[[maybe_unused]] constexpr int kLzRing = HBAM_LZ_RING;
-// phase-B fill: 64-token groups taken dynamically by waves (1) instead of
-// static token ranges (0).  Measured on C2: the waits vanish but the fill
-// itself doubles (the fill is issue-bound across all 16 waves, not
-// imbalanced): 7.91 vs 7.14 ms per pass.  Kept for reference, off.
-#ifndef HBAM_LZ_DYN
-#define HBAM_LZ_DYN 0
-#endif
-// phase-B resolve: two independent chases per thread per pass
-#ifndef HBAM_LZ_DUAL
-#define HBAM_LZ_DUAL 1
-#endif
+constexpr int kLzRing = 4;  // phase-B fill: 64-token groups loaded ahead (4 vs 8 measured equal)
 
 // exclusive scan over the workgroup; returns the prefix, *total = sum
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
@@ -1512,29 +1434,10 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
                                                              uint64_t chunk_ustart,
                                                              const uint32_t* __restrict__ tokens,
                                                              const HuffOut* __restrict__ hout,
-                                                             uint8_t* __restrict__ u,
-                                                             uint64_t* __restrict__ prof) {
+                                                             uint8_t* __restrict__ u) {
   // map index = o0 + position, so 16-byte output segments read 32 B-aligned LDS
   __shared__ __attribute__((aligned(16))) uint16_t map[kMapMax + 32];
   __shared__ uint32_t scratch[kLzWaves];
-#if HBAM_LZ_DYN
-  __shared__ uint16_t gpos[1024 + 2];  // output position of each 64-token group
-  __shared__ uint32_t gnext;           // next group to take
-#endif
-  // optional cycle profile (thread 0): [6] token loads [0] block scan
-  // [1] map fill (wave 0's own work) [2] fill barrier wait [3] resolve
-  // [4] store [5] total
-  if (!kProf) prof = nullptr;
-  uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t pt = prof ? clock64() : 0, pt0 = pt;
-#define LZ_T(i)                             \
-  do {                                      \
-    if (prof && threadIdx.x == 0) {         \
-      const uint64_t n_ = clock64();        \
-      pacc[i] += n_ - pt;                   \
-      pt = n_;                              \
-    }                                       \
-  } while (0)
   const BlockInfo blk = blocks[b0 + blockIdx.x];
   const HuffOut ho = hout[b0 + blockIdx.x];
   if (ho.status != kOk || blk.isize == 0) return;
@@ -1564,94 +1467,6 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
     return;
   }
 
-#if HBAM_LZ_DYN
-  // 1. per-group byte totals (a group = 64 consecutive tokens, one per lane;
-  //    G <= 1020 since every token emits >= 1 byte and isize <= 65280),
-  //    scanned over the workgroup into gpos[] (clamped to isize: u16).
-  const uint32_t wid = tid >> 6, lane = tid & 63;
-  const uint32_t G = (ntok + 63) >> 6;
-  for (uint32_t g0 = wid; g0 < G; g0 += 4 * kLzWaves) {  // 4 group loads in flight per wave
-    uint32_t tv[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t i = (g0 + k * kLzWaves) * 64 + lane;
-      tv[k] = i < ntok ? tk[i] : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t g = g0 + k * kLzWaves;
-      const uint32_t i = g * 64 + lane;
-      uint32_t v = i < ntok ? tok_len(tv[k]) : 0u;
-#pragma unroll
-      for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
-      if (lane == 0 && g < G) gpos[g] = (uint16_t)v;  // <= 64 * 258
-    }
-  }
-  if (tid == 0) gnext = kLzWaves;  // groups 0..15 are taken statically below
-  __syncthreads();
-  LZ_T(6);
-  {
-    uint32_t total;
-    const uint32_t v = tid < G ? gpos[tid] : 0u;
-    const uint32_t pre = block_excl_scan(v, scratch, &total);  // both barriers inside
-    if (tid < G) gpos[tid] = (uint16_t)min(pre, isize);
-    if (tid == 0) gpos[G] = (uint16_t)min(total, isize);
-  }
-  __syncthreads();
-  LZ_T(0);
-
-  // 2. map fill.  Waves take 64-token groups dynamically (LDS counter), so a
-  //    wave that drew long matches does not hold the others at the barrier.
-  //    A token is an arithmetic run of entries base + k*delta (match: source
-  //    position, 1; literal pair: tag|b0, b1-b0).  (i) every 8-entry aligned
-  //    chunk that starts inside a token is written whole by that token with
-  //    one ds_write_b128 -- entries past the token's end are wrong but belong
-  //    to later tokens of the same group; (ii) then each token writes its head
-  //    (its entries before its first chunk boundary) one by one, overwriting
-  //    them.  Chunks never cross the group's range end, so groups stay
-  //    disjoint.
-  uint16_t* m = map + o0;
-  uint32_t g = wid;
-  uint32_t tcur = g * 64 + lane < ntok ? tk[g * 64 + lane] : 0u;
-  while (g < G) {  // wave-uniform
-    uint32_t gn = 0;
-    if (lane == 0) gn = atomicAdd(&gnext, 1u);
-    gn = rfl(gn);
-    const uint32_t tnext = gn * 64 + lane < ntok && gn < G ? tk[gn * 64 + lane] : 0u;  // in flight meanwhile
-    const uint32_t i = g * 64 + lane;
-    const uint32_t t = tcur;
-    const uint32_t P = gpos[g], ghi = gpos[g + 1];
-    const uint32_t len = i < ntok ? tok_len(t) : 0u;
-    const uint32_t incl = wave_incl_scan_dpp(len);
-    const uint32_t pos = P + incl - len;
-    const uint32_t end = min(pos + len, ghi);
-    uint32_t base, delta;
-    if (t >> 31) {
-      base = pos - (((t >> 16) & 0x7fffu) + 1);  // dist <= pos: checked in phase A
-      delta = 1;
-    } else {
-      base = kLitTag | (t & 0xffu);
-      delta = (((t >> 8) & 0xffu) - (t & 0xffu)) & 0xffffu;
-    }
-    const uint32_t hb = min(end, ((o0 + pos + 7) & ~7u) - o0);  // head end = first chunk start
-    for (uint32_t q = hb; q < end; q += 8) {
-      const uint32_t v0 = base + (q - pos) * delta;
-      if (q + 8 <= ghi) {
-        const uint32_t d0 = (v0 & 0xffffu) | ((v0 + delta) << 16);
-        const uint32_t inc = (2u * delta) * 0x10001u;
-        *reinterpret_cast<uint4*>(m + q) = make_uint4(d0, d0 + inc, d0 + 2u * inc, d0 + 3u * inc);
-      } else {
-        uint32_t v = v0;
-        for (uint32_t r = q; r < ghi; ++r, v += delta) m[r] = (uint16_t)v;
-      }
-    }
-    wave_sync();  // (i) before (ii): they overlap across lanes
-    uint32_t v = base;
-    for (uint32_t r = pos; r < hb; ++r, v += delta) m[r] = (uint16_t)v;
-    g = gn;
-    tcur = tnext;
-  }
-#else
   // 1. wave w expands tokens [w*TW, (w+1)*TW); its output range starts at
   //    the byte total of the waves before it (coalesced token loads).
   const uint32_t wid = tid >> 6, lane = tid & 63;
@@ -1667,14 +1482,12 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
   }
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) wsum += __shfl_xor(wsum, d, 64);
-  LZ_T(6);
   if (lane == 0) scratch[wid] = wsum;
   __syncthreads();
   uint32_t P = 0;
 #pragma unroll
   for (int w = 0; w < kLzWaves; ++w) P += (uint32_t)w < wid ? scratch[w] : 0u;
   const uint32_t whi = min(P + wsum, isize);  // end of this wave's range (the last token may run past ISIZE)
-  LZ_T(0);
 
   // 2. map fill, 64 tokens (one per lane) at a time.  A token is an
   //    arithmetic run of entries base + k*delta (match: source position, 1;
@@ -1723,17 +1536,13 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
     uint32_t v = base;
     for (uint32_t r = pos; r < hb; ++r, v += delta) m[r] = (uint16_t)v;
   }
-#endif
-  LZ_T(1);
   __syncthreads();
-  LZ_T(2);
 
   // 3. resolve, increasing positions first; results written back in place
   //    (path compression).  Each round (1024 consecutive positions) costs one
   //    dependent LDS latency per chase step, so the raw entries of this
   //    thread's next positions (written by fill, rewritten only by this
   //    thread) are loaded kLzPf rounds ahead.
-#if HBAM_LZ_DUAL
   // two rounds per pass: the chases of positions q and q + 1024 are
   // independent, so their dependent LDS loads overlap (any visiting order is
   // correct: entries always point to smaller positions and a chase ends at a
@@ -1751,27 +1560,7 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
     m[q] = (uint16_t)v1;
     if (has2) m[q2] = (uint16_t)v2;
   }
-#else
-  {
-    uint32_t pre[kLzPf];
-#pragma unroll
-    for (int k = 0; k < kLzPf; ++k) {
-      const uint32_t q = tid + k * kLzThreads;
-      pre[k] = q < isize ? m[q] : kLitTag;
-    }
-    for (uint32_t q = tid; q < isize; q += kLzThreads) {
-      uint32_t v = pre[0];
-#pragma unroll
-      for (int k = 0; k + 1 < kLzPf; ++k) pre[k] = pre[k + 1];
-      const uint32_t qn = q + kLzPf * kLzThreads;
-      pre[kLzPf - 1] = qn < isize ? m[qn] : kLitTag;
-      while (v < kLitTag) v = m[v];
-      m[q] = (uint16_t)v;
-    }
-  }
-#endif
   __syncthreads();
-  LZ_T(3);
 
   // 4. 16 B stores; low bytes of 16 entries packed with v_perm
   for (uint32_t s = tid; s < nseg; s += kLzThreads) {
@@ -1792,12 +1581,6 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
       }
     }
   }
-  LZ_T(4);
-  if (prof && tid == 0) {
-    pacc[5] = clock64() - pt0;
-    for (int i = 0; i < 8; ++i) prof[8ull * (b0 + blockIdx.x) + i] = pacc[i];
-  }
-#undef LZ_T
 }
 
 // ---------------------------------------------------------------------------
@@ -1814,7 +1597,207 @@ struct ChainEnv {
   uint32_t ndead;
   int32_t n_ref;
   uint32_t k0, k1;         // block range [k0, k1)
+  int validate;            // reader mode: 0 SILENT (none), 1 LENIENT (decode structure), 2 STRICT (SAMRecord.isValid)
+  const int32_t* ref_len;  // n_ref reference lengths, or nullptr
 };
+
+// ---------------------------------------------------------------------------
+// [htsjdk] SAMRecord.isValid under ValidationStringency.STRICT.  BAMFileReader's
+// iterator validates every record it returns unless the stringency is SILENT
+// (BAMRecordReader.java:142,192-194 pass hadoopbam.samheaderreader.
+// validation-stringency through; htsjdk's default is STRICT) and STRICT turns
+// the first error into a SAMFormatException.  Restated subset (DESIGN.md
+// §2.1; oracle/hbam_oracle.c orc_strict_invalid is the same rule list):
+//   structure  read name, cigar, seq, qual inside the record; cigar op <= 8
+//   unpaired   no proper-pair / mate-unmapped / mate-reverse / first / second
+//              flag, mate refID == -1
+//   paired     mate refID/pos consistent (isValidReferenceIndexAndPosition),
+//              mate refID set unless mate-unmapped, first or second flag
+//   unmapped   not secondary / supplementary, MAPQ 0, no cigar
+//   mapped     cigar present, non-empty sequence dictionary
+//   position   refID/pos consistent, pos+1 <= reference length
+//   cigar      Cigar.isValid (zero-length ops, H/S/P placement, I/D pairs,
+//              a real operator) and M/=/X blocks inside the reference
+//   bin        == reg2bin(alignmentStart-1, alignmentEnd)
+//   seq        cigar read length == l_seq when both are non-zero;
+//              l_seq == 0 needs FZ, or CQ + CS (unless secondary)
+// The reader's IllegalArgumentException (refID out of range) is checked
+// before this, as the record factory raises it first.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int reg2bin_dev(int beg, int end) {  // GenomicIndexUtil.regionToBin
+  --end;
+  if (beg >> 14 == end >> 14) return ((1 << 15) - 1) / 7 + (beg >> 14);
+  if (beg >> 17 == end >> 17) return ((1 << 12) - 1) / 7 + (beg >> 17);
+  if (beg >> 20 == end >> 20) return ((1 << 9) - 1) / 7 + (beg >> 20);
+  if (beg >> 23 == end >> 23) return ((1 << 6) - 1) / 7 + (beg >> 23);
+  if (beg >> 26 == end >> 26) return ((1 << 3) - 1) / 7 + (beg >> 26);
+  return 0;
+}
+
+// aux tag t present (an l_seq == 0 record's FZ / CQ / CS lookup); *zlen = Z
+// string length
+__device__ bool aux_find(const uint8_t* u, uint64_t a, uint64_t e, uint16_t tag, int64_t* zlen) {
+  while (a + 3 <= e) {
+    const uint16_t t = (uint16_t)(u[a] | (u[a + 1] << 8));
+    const uint8_t ty = u[a + 2];
+    a += 3;
+    int64_t sz;
+    switch (ty) {
+      case 'A': case 'c': case 'C': sz = 1; break;
+      case 's': case 'S': sz = 2; break;
+      case 'i': case 'I': case 'f': sz = 4; break;
+      case 'Z': case 'H': {
+        uint64_t j = a;
+        while (j < e && u[j]) ++j;
+        if (t == tag) *zlen = (int64_t)(j - a);
+        sz = (int64_t)(j - a) + 1;
+        break;
+      }
+      case 'B': {
+        if (a + 5 > e) return false;
+        const uint8_t sub = u[a];
+        const int32_t cnt = (int32_t)ldu32(u, a + 1);
+        const int es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
+        if (cnt < 0) return false;
+        sz = 5 + (int64_t)cnt * es;
+        break;
+      }
+      default: return false;
+    }
+    if (t == tag) return true;
+    if ((uint64_t)sz > e - a) return false;  // a malformed aux block ends the lookup
+    a += (uint64_t)sz;
+  }
+  return false;
+}
+
+// true when the (fully inflated) record at q fails validation.  strict =
+// false keeps only the structural decode failures (LENIENT still decodes the
+// cigar for isValid and logs the rest).
+__device__ bool record_invalid(const ChainEnv& E, uint64_t q, int32_t bs, bool strict) {
+  const uint8_t* u = E.u;
+  const int32_t ref = (int32_t)ldu32(u, q + 4), pos = (int32_t)ldu32(u, q + 8);
+  const uint32_t w12 = ldu32(u, q + 12), w16 = ldu32(u, q + 16);
+  const uint32_t lrn = w12 & 0xffu, mapq = (w12 >> 8) & 0xffu, bin = w12 >> 16;
+  const uint32_t ncig = w16 & 0xffffu, flag = w16 >> 16;
+  const int32_t lseq = (int32_t)ldu32(u, q + 20), nref = (int32_t)ldu32(u, q + 24), npos = (int32_t)ldu32(u, q + 28);
+  // structure: the lazy fields isValid decodes must lie inside the record
+  if (lrn < 1 || lseq < 0) return true;
+  const int64_t need = 32 + (int64_t)lrn + 4 * (int64_t)ncig + ((int64_t)lseq + 1) / 2 + (int64_t)lseq;
+  if (need > (int64_t)bs) return true;
+  const uint64_t c0 = q + 36 + lrn;
+  uint32_t qlen = 0, rlen = 0;
+  for (uint32_t k = 0; k < ncig; ++k) {
+    const uint32_t op = ldu32(u, c0 + 4ull * k) & 0xfu;
+    if (op > 8) return true;
+  }
+  if (!strict) return false;
+  const bool paired = flag & 0x1, unmapped = flag & 0x4;
+  if (!paired) {
+    if (flag & (0x2 | 0x8 | 0x20 | 0x40 | 0x80)) return true;
+    if (nref != -1) return true;
+  } else {
+    if (nref == -1) {
+      if (npos != -1) return true;
+      if (!(flag & 0x8)) return true;  // "Mapped mate should have mate reference name"
+    } else {
+      if (npos == -1) return true;
+      if (E.ref_len && (int64_t)npos + 1 > (int64_t)E.ref_len[nref]) return true;
+    }
+    if (!(flag & 0xC0)) return true;  // neither first nor second of pair
+  }
+  if (unmapped) {
+    if (flag & (0x100 | 0x800)) return true;
+    if (mapq != 0) return true;  // (a cigar on an unmapped read is allowed: test.bam has them)
+  } else {
+    if (ncig == 0) return true;
+    if (E.n_ref == 0) return true;  // MISSING_SEQUENCE_DICTIONARY
+  }
+  if (ref == -1) {
+    if (pos != -1) return true;
+  } else {
+    if (pos == -1) return true;
+    if (E.ref_len && (int64_t)pos + 1 > (int64_t)E.ref_len[ref]) return true;
+  }
+  // cigar: Cigar.isValid + alignment blocks (mapped reads only)
+  bool real = false;
+  int64_t rpos = (int64_t)pos + 1, maxend = 0;
+  uint32_t prev_op = 99, first_op = 99, last_op = 99;
+  if (ncig) {
+    first_op = ldu32(u, c0) & 0xfu;
+    last_op = ldu32(u, c0 + 4ull * (ncig - 1)) & 0xfu;
+  }
+  // Cigar.isValid: between two separators (M/=/X/N or P) an I or a D may
+  // appear only once ("No M or N operator between pair of I/D operators")
+  bool seen_i = false, seen_d = false;
+  for (uint32_t k = 0; k < ncig; ++k) {
+    const uint32_t c = ldu32(u, c0 + 4ull * k), op = c & 0xfu, len = c >> 4;
+    const bool consumes_read = op == 0 || op == 1 || op == 4 || op == 7 || op == 8;
+    const bool consumes_ref = op == 0 || op == 2 || op == 3 || op == 7 || op == 8;
+    if (consumes_read) qlen += len;
+    if (consumes_ref) rlen += len;
+    if (!unmapped) {
+      if (len == 0) return true;
+      if (op == 5) {
+        if (k != 0 && k != ncig - 1) return true;
+      } else if (op == 4) {
+        if (k == 0 || k == ncig - 1) {
+        } else if (k == 1) {
+          if (!(ncig == 3 && last_op == 5) && first_op != 5) return true;
+        } else if (k == ncig - 2) {
+          if (last_op != 5) return true;
+        } else {
+          return true;
+        }
+      } else if (op == 6) {
+        if (k != 0) {
+          if (k == ncig - 1) return true;
+          const uint32_t nx = ldu32(u, c0 + 4ull * (k + 1)) & 0xfu;
+          const bool pr = prev_op <= 3 || prev_op == 7 || prev_op == 8, nr = nx <= 3 || nx == 7 || nx == 8;
+          if (!pr || !nr) return true;
+        }
+        seen_i = seen_d = false;
+      } else {  // real operator
+        real = true;
+        if (op == 1) {
+          if (seen_i) return true;
+          seen_i = true;
+        } else if (op == 2) {
+          if (seen_d) return true;
+          seen_d = true;
+        } else {
+          seen_i = seen_d = false;
+        }
+        if (op == 0 || op == 7 || op == 8) maxend = max(maxend, rpos + (int64_t)len - 1);
+      }
+    }
+    if (consumes_ref) rpos += len;
+    prev_op = op;
+  }
+  if (!unmapped) {
+    if (!real) return true;
+    if (ref >= 0 && E.ref_len && maxend > (int64_t)E.ref_len[ref]) return true;  // CIGAR_MAPS_OFF_REFERENCE
+  }
+  // bin: computeIndexingBin()
+  {
+    const int start0 = pos;  // getAlignmentStart() - 1
+    int end = unmapped ? 0 : (int)((int64_t)pos + 1 + (int64_t)rlen - 1);
+    if (end <= 0) end = start0 + 1;
+    if ((uint32_t)reg2bin_dev(start0, end) != bin) return true;
+  }
+  if (lseq != 0 && ncig != 0 && (int64_t)qlen != (int64_t)lseq) return true;  // MISMATCH_CIGAR_SEQ_LENGTH
+  if (lseq == 0 && !(flag & 0x100)) {  // EMPTY_READ unless FZ, or CQ and CS
+    const uint64_t a0 = c0 + 4ull * ncig, ae = q + 4 + (uint64_t)bs;
+    int64_t zl = -1;
+    if (!aux_find(u, a0, ae, (uint16_t)('F' | ('Z' << 8)), &zl)) {
+      int64_t cq = -1, cs = -1;
+      const bool hq = aux_find(u, a0, ae, (uint16_t)('C' | ('Q' << 8)), &cq);
+      const bool hs = aux_find(u, a0, ae, (uint16_t)('C' | ('S' << 8)), &cs);
+      if (!hq || !hs || cq <= 0 || cs <= 0) return true;
+    }
+  }
+  return false;
+}
 
 __device__ __forceinline__ bool is_dead(const ChainEnv& E, uint64_t q) {
   uint32_t lo = 0, hi = E.ndead;  // sorted; usually 0 or 1 entries (the EOF marker)
@@ -1884,51 +1867,6 @@ __device__ __forceinline__ bool chain_step(const ChainEnv& E, uint64_t q, uint64
     *nq = q + 4 + (bs > 0 ? (uint64_t)bs : 0);
   }
   return true;
-}
-
-// Per block guess of the first record start and the chain exit.  One wave per
-// block.  g = kNone when no candidate survives; exit < block end means the
-// walk stopped inside the block.
-template <int MODE>
-__global__ __launch_bounds__(64) void k_rec_guess(ChainEnv E, uint64_t* __restrict__ g_out,
-                                                  uint64_t* __restrict__ x_out) {
-  const uint32_t k = E.k0 + blockIdx.x;
-  const BlockInfo b = E.blocks[k];
-  const uint64_t bend = b.ustart + b.isize;
-  const uint32_t lane = lane_id();
-  uint64_t g = kNone, x = kNone;
-  if (bend > E.p0 && b.ustart < E.q_end && b.isize > 0) {
-    if (b.ustart <= E.p0) {  // the block holding the span start: entry is known
-      g = E.p0;
-      uint64_t q = g, nq;
-      while (q < bend && chain_step<MODE>(E, q, &nq)) q = nq;
-      x = q;
-    } else {
-      for (uint64_t c0 = b.ustart; c0 < bend && g == kNone; c0 += 64) {
-        uint64_t p = c0 + lane;
-        bool ok = p < bend && plausible(E, p);
-        uint64_t m = __ballot(ok);
-        while (m) {
-          uint64_t c = c0 + (uint64_t)(__ffsll((long long)m) - 1);
-          m &= m - 1;
-          uint64_t q = c;
-          bool valid = true;
-          while (q < bend) {
-            if (!plausible(E, q)) { valid = false; break; }
-            q += 4 + (uint64_t)(int32_t)ldu32(E.u, q);
-          }
-          // the exit must itself look like a record (or be the end / unreadable):
-          // rejects false starts whose garbage block_size jumps far ahead
-          if (valid && !(q == E.e_true || q + 36 > E.e_inf || plausible(E, q))) valid = false;
-          if (valid) { g = c; x = q; break; }
-        }
-      }
-    }
-  }
-  if (lane == 0) {
-    g_out[blockIdx.x] = g;
-    x_out[blockIdx.x] = x;
-  }
 }
 
 // Link the per-block guesses into the true chain (serial in block order, with
@@ -2008,39 +1946,6 @@ __global__ void k_rec_link_y(const uint64_t* __restrict__ g, const uint64_t* __r
   if (i < nb) y[i] = (g[i] != kNone && x[i] != kNone) ? x[i] : 0;
 }
 
-__global__ void k_rec_link_check(ChainEnv E, const uint64_t* __restrict__ g, const uint64_t* __restrict__ x,
-                                 const uint64_t* __restrict__ in_scan, uint64_t* __restrict__ entry,
-                                 uint32_t* __restrict__ fails) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t nb = E.k1 - E.k0;
-  if (i >= nb) return;
-  if (i == 0) {  // block of the span start: entry known
-    entry[0] = E.p0;
-    const BlockInfo b = E.blocks[E.k0];
-    if (x[0] < b.ustart + b.isize) atomicAdd(fails, 1u);  // chain stops in the first block: serial path
-    return;
-  }
-  const BlockInfo b = E.blocks[E.k0 + i];
-  const uint64_t bend = b.ustart + b.isize;
-  const uint64_t in = in_scan[i];
-  const uint64_t gi = g[i];
-  bool bad = false;
-  uint64_t e = kNone;
-  if (in >= E.q_end) {
-    e = kNone;                       // beyond the span
-  } else if (in >= bend || b.isize == 0) {
-    e = kNone;                       // no record starts here: pass-through
-    bad = gi != kNone && x[i] > in;  // a stray guess would corrupt later in[]
-  } else if (in < b.ustart) {
-    bad = true;                      // a block before had records but no guess
-  } else {
-    e = in;
-    bad = gi != in;                  // guess disagrees with the entering chain
-  }
-  entry[i] = e;
-  if (bad) atomicAdd(fails, 1u);
-}
-
 // Count (and validate) the records of each block of the span under the
 // reader / indexer rules.  One thread per block.
 //   cnt[i], err[i] = status code, errpos[i] = position of the failing record,
@@ -2075,6 +1980,7 @@ __global__ void k_rec_count(ChainEnv E, const uint64_t* __restrict__ entry, uint
         if (q + 4 + (uint64_t)bs > E.e_inf) { atomicMax(need, (unsigned long long)(q + 4 + (uint64_t)bs)); break; }
         const int32_t ref = (int32_t)ldu32(E.u, q + 4), nref = (int32_t)ldu32(E.u, q + 24);
         if (ref < -1 || ref >= E.n_ref || nref < -1 || nref >= E.n_ref) { st = kErrArg; break; }
+        if (E.validate && record_invalid(E, q, bs, E.validate == 2)) { st = kErrFormat; break; }
         ++n;
         q += 4 + (uint64_t)bs;
       } else {
@@ -2541,7 +2447,7 @@ __global__ __launch_bounds__(64) void k_rec_check(ChainEnv E, const uint64_t* __
     // a plausible() list on fully inflated data already satisfies every rule
     // that reads the record (block_size >= 32, refID / mate refID in range,
     // record inside the stream): only span end and dead positions remain
-    const bool light = (wc & kListPlausible) && E.e_inf == E.e_true;
+    const bool light = (wc & kListPlausible) && E.e_inf == E.e_true && (MODE != kReader || E.validate == 0);
     const uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
     count = n;
     for (uint32_t r0 = 0; r0 < n; r0 += 64) {
@@ -2581,6 +2487,9 @@ __global__ __launch_bounds__(64) void k_rec_check(ChainEnv E, const uint64_t* __
               if (ref < -1 || ref >= E.n_ref || nref < -1 || nref >= E.n_ref) {
                 stop = true;
                 s = kErrArg;
+              } else if (E.validate && record_invalid(E, q, bs, E.validate == 2)) {
+                stop = true;
+                s = kErrFormat;
               }
             }
           }
@@ -2656,11 +2565,49 @@ __global__ void k_truncate_counts(uint32_t* __restrict__ cnt, uint32_t nb, const
   if (i < nb && i > *cut) cnt[i] = 0;
 }
 
-// .splitting-bai: entry (o+1)/g = voff of record o when (o+1) % g == 0.
-__global__ void k_sbi_emit(const uint64_t* __restrict__ voff, uint64_t n, uint32_t g, uint64_t* __restrict__ ent) {
+// .splitting-bai (SplittingBAMIndexer.java:273-277): the voff of every record
+// whose global ordinal go = o0 + o satisfies (go + 1) % g == 0, at index
+// (go + 1) / g - 1 - o0 / g (entries of earlier windows come before).
+__global__ void k_sbi_emit(const uint64_t* __restrict__ voff, uint64_t n, uint32_t g, uint64_t o0,
+                           uint64_t* __restrict__ ent) {
+  const uint64_t k0 = o0 / g;
   for (uint64_t o = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; o < n;
        o += (uint64_t)gridDim.x * blockDim.x) {
-    if ((o + 1) % g == 0) ent[(o + 1) / g] = voff[o];
+    const uint64_t go = o0 + o;
+    if ((go + 1) % g == 0) ent[(go + 1) / g - 1 - k0] = voff[o];
+  }
+}
+
+// the chain successor of the last record of a span: where the next window
+// (or the next batch of a split) resumes
+__global__ void k_next_pos(const uint8_t* __restrict__ u, const uint64_t* __restrict__ rec_pos, uint64_t n,
+                           uint64_t p0, int mode, uint64_t* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (n == 0) {
+    *out = p0;
+    return;
+  }
+  const uint64_t q = rec_pos[n - 1];
+  const int32_t bs = (int32_t)ldu32(u, q);
+  *out = q + 4 + (uint64_t)(mode == kReader ? bs : (bs > 0 ? bs : 0));
+}
+
+// xor of the keys and sum of the voffs (order-independent digests)
+__global__ __launch_bounds__(256) void k_digest(const int64_t* __restrict__ keys, const uint64_t* __restrict__ voffs,
+                                                uint64_t n, unsigned long long* __restrict__ out) {
+  uint64_t kx = 0, vs = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (keys) kx ^= (uint64_t)keys[i];
+    vs += voffs[i];
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    kx ^= (uint64_t)__shfl_xor((unsigned long long)kx, d, 64);
+    vs += (uint64_t)__shfl_xor((unsigned long long)vs, d, 64);
+  }
+  if (lane_id() == 0) {
+    atomicXor(&out[0], (unsigned long long)kx);
+    atomicAdd(&out[1], (unsigned long long)vs);
   }
 }
 
@@ -2807,20 +2754,18 @@ hipError_t scan_u32_to_u64(void* tmp, size_t* tmp_bytes, const uint32_t* in, uin
   return hipcub::DeviceScan::ExclusiveSum(tmp, *tmp_bytes, in, out, (int)n, s);
 }
 
-uint64_t* g_huff_prof = nullptr;
-uint64_t* g_lz_prof = nullptr;  // HBAM_HUFF_PROF: phase-B per-block cycle profile (8 u64 per block)  // HBAM_HUFF_PROF: per-block cycle profile (hbam_pipeline.cpp)
-
-// max_stage = largest staged span of the chunk's blocks (huff_stage_bytes)
 hipError_t launch_huff_tables(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
                               uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s) {
   if (nb == 0) return hipSuccess;
   hipLaunchKernelGGL(k_huff_tables, dim3(nb), dim3(64), 0, s, file, blocks, b0, tables, tinfo);
   return hipGetLastError();
 }
-// phase A proper; the chunk's tables must be built (launch_huff_tables)
-static hipError_t launch_huff_only(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                                   uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
-                                   const uint8_t* tables, const HuffTableInfo* tinfo, hipStream_t s) {
+// phase A proper; the chunk's tables must be built (launch_huff_tables).
+// max_stage = largest staged span of the chunk's blocks (huff_stage_bytes)
+hipError_t launch_inflate_huff_prebuilt(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
+                                        uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
+                                        const uint8_t* tables, const HuffTableInfo* tinfo, hipStream_t s) {
+  if (nb == 0) return hipSuccess;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_inflate_huff<true>),
@@ -2829,49 +2774,18 @@ static hipError_t launch_huff_only(const uint8_t* file, const BlockInfo* blocks,
     attr_set = true;
   }
   const uint32_t staged_lds = kHuffStaticBytes + ((max_stage + 15) & ~15u);
-  const bool stage = kHuffStageMode == 2 || (kHuffStageMode == 1 && staged_lds <= kHuffStageMaxLds);
-  if (stage)
+  if (staged_lds <= kHuffStageMaxLds)
     hipLaunchKernelGGL(k_inflate_huff<true>, dim3(nb), dim3(kHuffThreads), staged_lds, s, file, blocks, b0,
-                       chunk_ustart, tokens, hout, tables, tinfo, g_huff_prof);
+                       chunk_ustart, tokens, hout, tables, tinfo);
   else
     hipLaunchKernelGGL(k_inflate_huff<false>, dim3(nb), dim3(kHuffThreads), kHuffStaticBytes, s, file, blocks, b0,
-                       chunk_ustart, tokens, hout, tables, tinfo, g_huff_prof);
+                       chunk_ustart, tokens, hout, tables, tinfo);
   return hipGetLastError();
-}
-static hipError_t launch_huff(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                              uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
-                              uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s) {
-  hipError_t e = launch_huff_tables(file, blocks, b0, nb, tables, tinfo, s);
-  if (e != hipSuccess) return e;
-  return launch_huff_only(file, blocks, b0, nb, chunk_ustart, tokens, hout, max_stage, tables, tinfo, s);
-}
-hipError_t launch_inflate_huff_prebuilt(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                                        uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
-                                        const uint8_t* tables, const HuffTableInfo* tinfo, hipStream_t s) {
-  if (nb == 0) return hipSuccess;
-  return launch_huff_only(file, blocks, b0, nb, chunk_ustart, tokens, hout, max_stage, tables, tinfo, s);
-}
-hipError_t launch_inflate(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                          uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint8_t* u, uint32_t max_stage,
-                          uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s) {
-  if (nb == 0) return hipSuccess;
-  hipError_t e = launch_huff(file, blocks, b0, nb, chunk_ustart, tokens, hout, max_stage, tables, tinfo, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_inflate_lz77, dim3(nb), dim3(kLzThreads), 0, s, blocks, b0, chunk_ustart, tokens, hout, u,
-                     g_lz_prof);
-  return hipGetLastError();
-}
-hipError_t launch_inflate_huff(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                               uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
-                               uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s) {
-  if (nb == 0) return hipSuccess;
-  return launch_huff(file, blocks, b0, nb, chunk_ustart, tokens, hout, max_stage, tables, tinfo, s);
 }
 hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb, uint64_t chunk_ustart,
                                const uint32_t* tokens, const HuffOut* hout, uint8_t* u, hipStream_t s) {
   if (nb == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_inflate_lz77, dim3(nb), dim3(kLzThreads), 0, s, blocks, b0, chunk_ustart, tokens, hout, u,
-                     g_lz_prof);
+  hipLaunchKernelGGL(k_inflate_lz77, dim3(nb), dim3(kLzThreads), 0, s, blocks, b0, chunk_ustart, tokens, hout, u);
   return hipGetLastError();
 }
 
@@ -2888,27 +2802,25 @@ hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s) 
   E.n_ref = a.n_ref;
   E.k0 = a.k0;
   E.k1 = a.k1;
+  E.validate = a.validate;
+  E.ref_len = a.ref_len;
   const uint32_t nb = a.k1 - a.k0;
   if (nb == 0) return hipSuccess;
   const unsigned tb = 64, gb = (nb + tb - 1) / tb;
   switch (stage) {
-    case 0:
-      if (mode == kReader) hipLaunchKernelGGL(k_rec_guess<kReader>, dim3(nb), dim3(64), 0, s, E, a.g, a.x);
-      else hipLaunchKernelGGL(k_rec_guess<kIndexer>, dim3(nb), dim3(64), 0, s, E, a.g, a.x);
-      break;
-    case 1:
+    case kStageSerialLink:
       if (mode == kReader) hipLaunchKernelGGL(k_rec_link<kReader>, dim3(1), dim3(256), 0, s, E, a.g, a.x, a.entry, a.summary);
       else hipLaunchKernelGGL(k_rec_link<kIndexer>, dim3(1), dim3(256), 0, s, E, a.g, a.x, a.entry, a.summary);
       break;
-    case 2:
+    case kStageCount:
       if (mode == kReader) hipLaunchKernelGGL(k_rec_count<kReader>, dim3(gb), dim3(tb), 0, s, E, a.entry, a.cnt, a.err, a.need);
       else hipLaunchKernelGGL(k_rec_count<kIndexer>, dim3(gb), dim3(tb), 0, s, E, a.entry, a.cnt, a.err, a.need);
       break;
-    case 3:
+    case kStageEmit:
       if (mode == kReader) hipLaunchKernelGGL(k_rec_emit<kReader>, dim3(gb), dim3(tb), 0, s, E, a.entry, a.cnt, a.base, a.rec_pos, a.rec_voff);
       else hipLaunchKernelGGL(k_rec_emit<kIndexer>, dim3(gb), dim3(tb), 0, s, E, a.entry, a.cnt, a.base, a.rec_pos, a.rec_voff);
       break;
-    case 5: {  // v2: candidates + walks
+    case kStageWalk: {  // candidates + walks
       if (mode == kReader) {
         hipLaunchKernelGGL(k_rec_cand<kReader>, dim3(nb), dim3(64), 0, s, E, a.cand);
         hipLaunchKernelGGL(k_rec_walk<kReader>, dim3((nb + 255) / 256), dim3(256), 0, s, E, a.cand, nullptr, a.g,
@@ -2924,7 +2836,7 @@ hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s) 
       }
       break;
     }
-    case 6: {  // v2: y, exclusive max-scan, check with re-walk requests
+    case kStageLinkCheck: {  // y, exclusive max-scan, check with re-walk requests
       hipError_t e = hipMemsetAsync(a.force, 0xff, (size_t)nb * 8, s);
       if (e != hipSuccess) return e;
       hipLaunchKernelGGL(k_rec_link_y, dim3(gb), dim3(tb), 0, s, a.g, a.x, nb, a.x2);
@@ -2934,10 +2846,10 @@ hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s) 
       hipLaunchKernelGGL(k_rec_linkfix, dim3(gb), dim3(tb), 0, s, E, a.g, a.x, a.base, a.entry, a.force, a.counters);
       break;
     }
-    case 7:    // v2: re-walk the requested blocks (entries validated)
-    case 8: {  // v2: force off the serial link's (exact) entry[], then re-walk
-      const bool validate = stage == 7;
-      if (stage == 8) hipLaunchKernelGGL(k_force_from_entry, dim3(gb), dim3(tb), 0, s, a.g, a.entry, nb, a.force);
+    case kStageRewalk:       // re-walk the requested blocks (entries validated)
+    case kStageRewalkAll: {  // force off the serial link's (exact) entry[], then re-walk
+      const bool validate = stage == kStageRewalk;
+      if (stage == kStageRewalkAll) hipLaunchKernelGGL(k_force_from_entry, dim3(gb), dim3(tb), 0, s, a.g, a.entry, nb, a.force);
       if (mode == kReader)
         hipLaunchKernelGGL(k_rec_walk<kReader>, dim3((nb + 255) / 256), dim3(256), 0, s, E, a.cand, a.force, a.g,
                            a.x, a.wcnt, a.list, a.counters + 2, validate);
@@ -2946,7 +2858,7 @@ hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s) 
                            a.x, a.wcnt, a.list, a.counters + 2, validate);
       break;
     }
-    case 9:  // v2: per-record check
+    case kStageCheck:  // per-record check
       if (mode == kReader)
         hipLaunchKernelGGL(k_rec_check<kReader>, dim3(nb), dim3(64), 0, s, E, a.entry, a.wcnt, a.list, a.cnt, a.err,
                            a.need);
@@ -2954,15 +2866,6 @@ hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s) 
         hipLaunchKernelGGL(k_rec_check<kIndexer>, dim3(nb), dim3(64), 0, s, E, a.entry, a.wcnt, a.list, a.cnt,
                            a.err, a.need);
       break;
-    case 4: {  // parallel link: y, exclusive max-scan, check
-      hipLaunchKernelGGL(k_rec_link_y, dim3(gb), dim3(tb), 0, s, a.g, a.x, nb, a.x2);
-      size_t sb = a.scan_bytes;
-      hipError_t e = hipcub::DeviceScan::ExclusiveScan(a.scan_tmp, sb, a.x2, a.base, hipcub::Max(),
-                                                       (uint64_t)0, (int)nb, s);
-      if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(k_rec_link_check, dim3(gb), dim3(tb), 0, s, E, a.g, a.x, a.base, a.entry, a.changed);
-      break;
-    }
     default:
       return hipErrorInvalidValue;
   }
@@ -2982,6 +2885,8 @@ hipError_t launch_rec_out(const ChainArgs& a, int mode, bool decode, const Colum
   E.n_ref = a.n_ref;
   E.k0 = a.k0;
   E.k1 = a.k1;
+  E.validate = a.validate;
+  E.ref_len = a.ref_len;
   const uint32_t nb = a.k1 - a.k0;
   if (nb == 0) return hipSuccess;
   if (mode == kReader && decode)
@@ -3022,9 +2927,20 @@ hipError_t launch_truncate_counts(uint32_t* cnt, uint32_t nb, const uint32_t* cu
   hipLaunchKernelGGL(k_truncate_counts, dim3((nb + 255) / 256), dim3(256), 0, s, cnt, nb, cut);
   return hipGetLastError();
 }
-hipError_t launch_sbi_emit(const uint64_t* voff, uint64_t n, uint32_t g, uint64_t* ent, hipStream_t s) {
+hipError_t launch_sbi_emit(const uint64_t* voff, uint64_t n, uint32_t g, uint64_t o0, uint64_t* ent, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_sbi_emit, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, voff, n, g, ent);
+  hipLaunchKernelGGL(k_sbi_emit, dim3(grid_for(n, 256, 16384)), dim3(256), 0, s, voff, n, g, o0, ent);
+  return hipGetLastError();
+}
+hipError_t launch_next_pos(const uint8_t* u, const uint64_t* rec_pos, uint64_t n, uint64_t p0, int mode,
+                           uint64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_next_pos, dim3(1), dim3(64), 0, s, u, rec_pos, n, p0, mode, out);
+  return hipGetLastError();
+}
+hipError_t launch_digest(const int64_t* keys, const uint64_t* voffs, uint64_t n, uint64_t* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_digest, dim3(grid_for(n, 256, 2048)), dim3(256), 0, s, keys, voffs, n,
+                     reinterpret_cast<unsigned long long*>(out));
   return hipGetLastError();
 }
 hipError_t launch_wr_encode(const uint8_t* u, uint64_t p0, uint64_t nbytes, const uint64_t* rec_pos,
@@ -3057,16 +2973,3 @@ hipError_t launch_wr_decode(const uint8_t* buf, uint64_t len, const uint64_t* of
 }
 
 }  // namespace hbam
-#ifdef HBAM_PROBE
-namespace hbam {
-__global__ void k_probe_spec(const uint32_t* W, uint32_t a, uint32_t stop, uint32_t E, uint32_t* out) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  HuffLds& L = *reinterpret_cast<HuffLds*>(smem);
-  W = reinterpret_cast<const uint32_t*>(smem + sizeof(HuffLds));
-  MergePts mp;
-  uint32_t mj = 0, x, nt, nb;
-  uint32_t ev = lane_decode<LD_SPEC>(L, W, a + threadIdx.x, stop, E, x, nt, nb, mp, mj, nullptr, 0, 0);
-  out[threadIdx.x] = ev + x + nt + nb + mp.p0 + mp.p3;
-}
-}
-#endif

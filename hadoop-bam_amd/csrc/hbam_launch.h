@@ -15,10 +15,11 @@ struct ChainArgs {
   uint32_t ndead;
   int32_t n_ref;
   uint32_t k0, k1;
+  int validate;            // reader mode: 0 SILENT, 1 LENIENT (decode structure only), 2 STRICT (SAMRecord.isValid)
+  const int32_t* ref_len;  // n_ref reference lengths (nullptr: alignment-start bound not checked)
   // per-block scratch (indexed by k - k0)
   uint64_t *g, *x, *entry, *summary, *base;
-  uint64_t* x2;        // parallel link: y (guess exits)
-  uint32_t* changed;   // parallel link: violation count
+  uint64_t* x2;        // parallel link: y (walk exits)
   void* scan_tmp;      // parallel link: hipcub temp storage
   size_t scan_bytes;
   uint32_t* cnt;
@@ -26,7 +27,7 @@ struct ChainArgs {
   unsigned long long* need;
   // outputs
   uint64_t *rec_pos, *rec_voff;
-  // chain v2 (lane-per-block walks + per-block record lists)
+  // lane-per-block walks + per-block record lists
   uint64_t* cand;       // first plausible record start per block
   uint64_t* force;      // re-walk requests (kNone = keep)
   uint32_t* wcnt;       // records listed per block
@@ -36,11 +37,23 @@ struct ChainArgs {
 constexpr uint32_t kListCap = 2048;              // >= 65536 / 36 + 2: every reader-mode record start
 constexpr uint64_t kForceEmpty = ~0ull - 1;      // force[]: the block holds no record start
 
+// launch_chain stages
+enum ChainStage : int {
+  kStageSerialLink = 1,  // exact serial link over the walk exits (entry[] + summary)
+  kStageCount = 2,       // per-block count + validation by walking (list overflow path)
+  kStageEmit = 3,        // per-block positions + voffs by walking (list overflow path)
+  kStageWalk = 5,        // candidates + lane-per-block walks
+  kStageLinkCheck = 6,   // max-scan link check with re-walk requests
+  kStageRewalk = 7,      // re-walk the requested blocks (entries validated)
+  kStageRewalkAll = 8,   // re-walk every block off the serial link's entry[]
+  kStageCheck = 9,       // per-record check of the lists -> cnt / err / need
+};
+
 // candidates in [lo, hi); file + buf_base is the (aligned) device buffer start
 hipError_t launch_bgzf_scan(const uint8_t* file, uint64_t buf_base, uint64_t lo, uint64_t hi, uint64_t* cand,
                             uint32_t cap, uint32_t* count, hipStream_t s);
-// partial != 0: bytes past hi are not uploaded yet; a block cut by hi ends
-// the range (verify: flags[2] = 1; walk: out[2..3] = its start, status OK)
+// partial != 0: bytes past hi are not part of the window; a block cut by hi
+// ends the range (verify: flags[2] = 1; walk: out[2..3] = its start, status OK)
 hipError_t launch_bgzf_verify(const uint8_t* file, uint64_t lo, uint64_t hi, const uint64_t* cand, uint32_t n,
                               BlockInfo* blocks, uint32_t* flags, uint32_t partial, hipStream_t s);
 hipError_t launch_bgzf_walk(const uint8_t* file, uint64_t lo, uint64_t hi, BlockInfo* blocks, uint32_t cap,
@@ -52,22 +65,13 @@ hipError_t sort_u64(void* tmp, size_t* tmp_bytes, uint64_t* keys_in, uint64_t* k
                     hipStream_t s);
 hipError_t scan_u32_to_u64(void* tmp, size_t* tmp_bytes, const uint32_t* in, uint64_t* out, uint32_t n,
                            hipStream_t s);
-hipError_t launch_inflate(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                          uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint8_t* u, uint32_t max_stage,
-                          uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s);
-hipError_t launch_inflate_huff(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                               uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
-                               uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s);
-// phase A split in two: the first DEFLATE block's header + tables of every
-// block of a chunk (k_huff_tables), then the decode reading them
+// inflate phase A in two launches: the first DEFLATE block's header + tables
+// of every block of a chunk (k_huff_tables), then the decode reading them
 hipError_t launch_huff_tables(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
                               uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s);
 hipError_t launch_inflate_huff_prebuilt(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
                                         uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
                                         const uint8_t* tables, const HuffTableInfo* tinfo, hipStream_t s);
-// HBAM_HUFF_PROF profile buffer (16 u64 per block) or nullptr
-extern uint64_t* g_huff_prof;
-extern uint64_t* g_lz_prof;
 // LDS bytes phase A stages for a block: its cdata from the 16 B-aligned start,
 // footer included, plus one 16 B pad (must match k_inflate_huff).
 inline uint32_t huff_stage_bytes(const BlockInfo& b) {
@@ -76,12 +80,8 @@ inline uint32_t huff_stage_bytes(const BlockInfo& b) {
 }
 hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb, uint64_t chunk_ustart,
                                const uint32_t* tokens, const HuffOut* hout, uint8_t* u, hipStream_t s);
-// stage: 0 guess, 1 serial link, 2 count, 3 emit, 4 parallel link (base = in[] scratch),
-//        5 candidates + walks (v2), 6 link check with re-walk requests (v2),
-//        7 re-walk requested blocks (v2), 8 re-walk every block off entry[] (v2),
-//        9 per-record check -> cnt/err/need (v2)
 hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s);
-// chain v2 output: positions, voffs and (decode) the SoA columns, one wave per block
+// positions, voffs and (decode) the SoA columns off the per-block lists, one wave per block
 hipError_t launch_rec_out(const ChainArgs& a, int mode, bool decode, const Columns& col, hipStream_t s);
 hipError_t link_scan_bytes(uint32_t nb, size_t* bytes);
 hipError_t launch_rec_decode(const uint8_t* u, const uint64_t* rec_pos, uint64_t n, const Columns& col,
@@ -89,7 +89,14 @@ hipError_t launch_rec_decode(const uint8_t* u, const uint64_t* rec_pos, uint64_t
 hipError_t launch_first_error_hout(const HuffOut* hout, uint32_t b0, uint32_t nb, uint32_t* first, hipStream_t s);
 hipError_t launch_first_error_i32(const int32_t* err, uint32_t nb, uint32_t* first, hipStream_t s);
 hipError_t launch_truncate_counts(uint32_t* cnt, uint32_t nb, const uint32_t* cut, hipStream_t s);
-hipError_t launch_sbi_emit(const uint64_t* voff, uint64_t n, uint32_t g, uint64_t* ent, hipStream_t s);
+// .splitting-bai entries of records with global ordinals o0 .. o0+n-1
+// (ordinals k*g - 1): ent[j] for the j-th such ordinal of the span
+hipError_t launch_sbi_emit(const uint64_t* voff, uint64_t n, uint32_t g, uint64_t o0, uint64_t* ent, hipStream_t s);
+// *out = the chain successor of the last of n records (p0 when n == 0)
+hipError_t launch_next_pos(const uint8_t* u, const uint64_t* rec_pos, uint64_t n, uint64_t p0, int mode,
+                           uint64_t* out, hipStream_t s);
+// out[0] ^= xor of keys (if keys), out[1] += sum of voffs
+hipError_t launch_digest(const int64_t* keys, const uint64_t* voffs, uint64_t n, uint64_t* out, hipStream_t s);
 // keys deferred by decode_record (rest > kLongHash bytes): one wave per record
 hipError_t launch_long_hash(const uint8_t* u, const uint64_t* rec_pos, const Columns& col, hipStream_t s);
 // SAMRecordWritable.write of a span's records: u[p0, p0+nbytes) -> dst

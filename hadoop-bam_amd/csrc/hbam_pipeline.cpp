@@ -1,4 +1,5 @@
-// hbam_pipeline.cpp -- host orchestration of the gfx950 BAM read pipeline.
+// hbam_pipeline.cpp -- host orchestration of one HBM window of the gfx950 BAM
+// read pipeline (see hbam_pipeline.h).
 #include "hbam_pipeline.h"
 
 #include <algorithm>
@@ -11,12 +12,12 @@
 namespace hbam {
 
 namespace {
-#ifndef HBAM_INFLATE_CHUNK
-#define HBAM_INFLATE_CHUNK 16384
-#endif
-constexpr uint32_t kInflateChunkBlocks = HBAM_INFLATE_CHUNK;  // blocks per phase-A/B launch pair
+constexpr uint32_t kInflateChunkBlocks = 16384;  // blocks per phase-A/B launch pair
 constexpr int kMaxChainIters = 64;
-constexpr int kMaxLinkFix = 4;  // re-walk rounds before the serial link
+constexpr int kMaxLinkFix = 4;        // re-walk rounds before the serial link
+constexpr int kMaxFreeStarts = 64;    // header candidates tried by a free-start locate
+// e_true of an open window: records may run past its last block
+constexpr uint64_t kOpenEnd = 1ull << 62;
 }  // namespace
 
 Pipeline::Pipeline(int device) : device_(device) {
@@ -38,18 +39,15 @@ Pipeline::Pipeline(int device) : device_(device) {
 
 Pipeline::~Pipeline() {
   (void)hipSetDevice(device_);
-  if (own_file_ && dfile_) (void)hipFree(dfile_);
+  (void)hipDeviceSynchronize();
   for (auto& e : ev_) (void)hipEventDestroy(e);
   for (auto& e : sync_ev_) (void)hipEventDestroy(e);
   for (auto& e : tev_) (void)hipEventDestroy(e);
   for (auto& e : copy_ev_) (void)hipEventDestroy(e);
-  if (stream_b_) (void)hipStreamDestroy(stream_b_);
-  if (stream_copy_) (void)hipStreamDestroy(stream_copy_);
-  if (stream_loc_) (void)hipStreamDestroy(stream_loc_);
-  if (stream_t_) (void)hipStreamDestroy(stream_t_);
   for (auto& e : tab_ev_) (void)hipEventDestroy(e);
   for (auto& e : hdone_ev_) (void)hipEventDestroy(e);
-  if (stream_) (void)hipStreamDestroy(stream_);
+  for (hipStream_t s : {stream_b_, stream_copy_, stream_loc_, stream_t_, stream_})
+    if (s) (void)hipStreamDestroy(s);
 }
 
 int Pipeline::fail(int code, const std::string& msg) {
@@ -69,31 +67,44 @@ int Pipeline::hip_check(hipError_t e, const char* what) {
     if (_rc != kOk) return _rc;                        \
   } while (0)
 
-int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base_offset) {
+int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof) {
   HIPCHK(hipSetDevice(device_));
-  if (own_file_ && dfile_) (void)hipFree(dfile_);
-  dfile_ = nullptr;
-  HIPCHK(hipMalloc(reinterpret_cast<void**>(&dfile_), len + kFilePad));
-  own_file_ = true;
+  HIPCHK(own_file_.reserve(len + kFilePad));
+  dfile_ = own_file_.p;
   if (len) HIPCHK(hipMemcpyAsync(dfile_, data, len, hipMemcpyHostToDevice, stream_));
   HIPCHK(hipMemsetAsync(dfile_ + len, 0, kFilePad, stream_));
   HIPCHK(hipStreamSynchronize(stream_));
   flen_ = len;
-  base_ = base_offset;
+  base_ = base;
+  at_eof_ = at_eof;
+  window_end_ = base + len;
   hblocks_.clear();
+  inflated_.clear();
+  total_u_ = 0;
+  return kOk;
+}
+
+int Pipeline::attach_device(const uint8_t* dptr, uint64_t len, uint64_t base, bool at_eof) {
+  dfile_ = const_cast<uint8_t*>(dptr);
+  flen_ = len;
+  base_ = base;
+  at_eof_ = at_eof;
+  window_end_ = base + len;
+  hblocks_.clear();
+  inflated_.clear();
   total_u_ = 0;
   return kOk;
 }
 
 int Pipeline::reload(const uint8_t* data, uint64_t len, bool pinned, float* ms) {
-  if (!dfile_ || !own_file_ || len != flen_) return fail(kErrState, "reload needs a loaded file of the same size");
+  if (!dfile_ || dfile_ != own_file_.p || len != flen_)
+    return fail(kErrState, "reload needs a loaded window of the same size");
   HIPCHK(hipSetDevice(device_));
   uint8_t* staging = nullptr;
   if (pinned && len) {  // page-locked copy of the bytes (untimed), as a JNI direct buffer would be
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&staging), len, hipHostMallocDefault));
     memcpy(staging, data, len);
   }
-  int rc = kOk;
   auto body = [&]() -> int {
     HIPCHK(hipEventRecord(ev_[6], stream_));
     if (len) HIPCHK(hipMemcpyAsync(dfile_, staging ? staging : data, len, hipMemcpyHostToDevice, stream_));
@@ -102,7 +113,7 @@ int Pipeline::reload(const uint8_t* data, uint64_t len, bool pinned, float* ms) 
     HIPCHK(hipEventElapsedTime(ms, ev_[6], ev_[7]));
     return kOk;
   };
-  rc = body();
+  const int rc = body();
   if (staging) (void)hipHostFree(staging);
   return rc;
 }
@@ -124,19 +135,17 @@ int Pipeline::d2d_bandwidth(uint64_t bytes, int iters, float* gbps) {
   return kOk;
 }
 
-int Pipeline::attach_device(const uint8_t* dptr, uint64_t len, uint64_t base_offset) {
-  if (own_file_ && dfile_) (void)hipFree(dfile_);
-  dfile_ = const_cast<uint8_t*>(dptr);
-  own_file_ = false;
-  flen_ = len;
-  base_ = base_offset;
-  hblocks_.clear();
-  total_u_ = 0;
+int Pipeline::set_ref_lengths(const std::vector<int32_t>& lens) {
+  HIPCHK(ref_len_.reserve(lens.size() + 1));
+  if (!lens.empty())
+    HIPCHK(hipMemcpyAsync(ref_len_.p, lens.data(), lens.size() * 4, hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  n_ref_len_ = (uint32_t)lens.size();
   return kOk;
 }
 
-int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, uint32_t nprev, uint64_t ubase, hipStream_t s,
-                           uint32_t* nnew, uint64_t* tail) {
+int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_start, uint32_t nprev, uint64_t ubase,
+                           hipStream_t s, uint32_t* nnew, uint64_t* tail) {
   *nnew = 0;
   *tail = hi;
   const uint8_t* fbase = dfile_ - base_;  // absolute file coordinates
@@ -145,31 +154,37 @@ int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, uint32_t npre
   // (or any chain break) take the serial walk, whose table bound is len/26.
   const uint32_t cap = (uint32_t)std::min<uint64_t>(len / 1024 + 4096, 0x7fffffffu);
   const uint32_t walk_cap = (uint32_t)std::min<uint64_t>(len / 26 + 16, 0x7fffffffu);
-  DevBuf<uint64_t>& cand = cand_;
-  DevBuf<uint64_t>& sorted = sorted_;
-  HIPCHK(cand.reserve(cap));
+  HIPCHK(cand_.reserve(cap));
   HIPCHK(flags_.reserve(4));
   uint32_t init[4] = {0, 0, 0xffffffffu, 0};
   HIPCHK(hipMemcpyAsync(flags_.p, init, sizeof init, hipMemcpyHostToDevice, s));
   // flags_[0] = candidate count, [1] = chain break, [2] = first big ISIZE, [3] = cut tail
-  HIPCHK(launch_bgzf_scan(fbase, base_, lo, hi, cand.p, cap, flags_.p, s));
+  HIPCHK(launch_bgzf_scan(fbase, base_, lo, hi, cand_.p, cap, flags_.p, s));
   uint32_t count = 0;
   HIPCHK(hipMemcpyAsync(&count, flags_.p, 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   bool serial = count > cap || (count == 0 && len > 0);
+  if (free_start && count == 0) return kOk;  // no header in the window: no blocks
   uint32_t n = serial ? 0 : count;
+  std::vector<uint64_t> starts;  // free start: candidates to try, in order
   if (!serial && n > 0) {
     HIPCHK(dblocks_.grow(nprev + n + 1));
-    HIPCHK(sorted.reserve(n));
+    HIPCHK(sorted_.reserve(n));
     size_t tmp_bytes = 0;
-    HIPCHK(sort_u64(nullptr, &tmp_bytes, cand.p, sorted.p, n, s));
+    HIPCHK(sort_u64(nullptr, &tmp_bytes, cand_.p, sorted_.p, n, s));
     HIPCHK(scan_tmp_.reserve(tmp_bytes + 16));
-    HIPCHK(sort_u64(scan_tmp_.p, &tmp_bytes, cand.p, sorted.p, n, s));
-    HIPCHK(launch_bgzf_verify(fbase, lo, hi, sorted.p, n, dblocks_.p + nprev, flags_.p + 1, partial ? 1u : 0u, s));
+    HIPCHK(sort_u64(scan_tmp_.p, &tmp_bytes, cand_.p, sorted_.p, n, s));
+    if (free_start) {
+      starts.resize(std::min<uint32_t>(n, kMaxFreeStarts));
+      HIPCHK(hipMemcpyAsync(starts.data(), sorted_.p, starts.size() * 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      lo = starts[0];
+    }
+    HIPCHK(launch_bgzf_verify(fbase, lo, hi, sorted_.p, n, dblocks_.p + nprev, flags_.p + 1, partial ? 1u : 0u, s));
     uint32_t fl[3];
     uint64_t last = 0;
     HIPCHK(hipMemcpyAsync(fl, flags_.p + 1, 12, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&last, sorted.p + n - 1, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&last, sorted_.p + n - 1, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     if (fl[0]) serial = true;
     else if (fl[1] != 0xffffffffu) return fail(kErrFormat, "BGZF block with ISIZE > 65536 (unsupported on device)");
@@ -181,24 +196,35 @@ int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, uint32_t npre
   if (serial) {
     uint32_t out[4];
     HIPCHK(dblocks_.grow(nprev + walk_cap + 1));
-    HIPCHK(hipMemsetAsync(flags_.p, 0, 16, s));
-    HIPCHK(launch_bgzf_walk(fbase, lo, hi, dblocks_.p + nprev, walk_cap, flags_.p, partial ? 1u : 0u, s));
-    HIPCHK(hipMemcpyAsync(out, flags_.p, 16, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    n = out[0];
-    const uint64_t at = (uint64_t)out[2] | ((uint64_t)out[3] << 32);
-    if (out[1] != kOk) return fail((int)out[1], "malformed BGZF block at offset " + std::to_string(at));
-    if (partial) *tail = at;
+    if (starts.empty()) starts.push_back(lo);
+    bool found = false;
+    for (size_t j = 0; j < starts.size() && !found; ++j) {
+      HIPCHK(hipMemsetAsync(flags_.p, 0, 16, s));
+      HIPCHK(launch_bgzf_walk(fbase, starts[j], hi, dblocks_.p + nprev, walk_cap, flags_.p, partial ? 1u : 0u, s));
+      HIPCHK(hipMemcpyAsync(out, flags_.p, 16, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      n = out[0];
+      const uint64_t at = (uint64_t)out[2] | ((uint64_t)out[3] << 32);
+      if (out[1] != kOk) {
+        if (free_start) continue;  // a false header candidate: try the next one
+        return fail((int)out[1], "malformed BGZF block at offset " + std::to_string(at));
+      }
+      if (free_start && n == 0) continue;
+      if (partial) *tail = at;
+      found = true;
+    }
+    if (!found) {
+      if (free_start) return kOk;  // no block chain in the window
+      return fail(kErrFormat, "malformed BGZF block");
+    }
   }
   HIPCHK(dblocks_.grow(nprev + n + 1));
-  DevBuf<uint64_t>& isz = isz_;
-  DevBuf<uint64_t>& ust = ust_;
-  HIPCHK(isz.reserve(n + 1));
-  HIPCHK(ust.reserve(n + 1));
+  HIPCHK(isz_.reserve(n + 1));
+  HIPCHK(ust_.reserve(n + 1));
   size_t sb = 0;
-  HIPCHK(launch_block_ustart(dblocks_.p + nprev, n, isz.p, ust.p, nullptr, &sb, ubase, s));
+  HIPCHK(launch_block_ustart(dblocks_.p + nprev, n, isz_.p, ust_.p, nullptr, &sb, ubase, s));
   HIPCHK(scan_tmp_.reserve(sb + 16));
-  HIPCHK(launch_block_ustart(dblocks_.p + nprev, n, isz.p, ust.p, scan_tmp_.p, &sb, ubase, s));
+  HIPCHK(launch_block_ustart(dblocks_.p + nprev, n, isz_.p, ust_.p, scan_tmp_.p, &sb, ubase, s));
   hblocks_.resize(nprev + n);
   if (n)
     HIPCHK(hipMemcpyAsync(hblocks_.data() + nprev, dblocks_.p + nprev, n * sizeof(BlockInfo), hipMemcpyDeviceToHost,
@@ -227,15 +253,17 @@ int Pipeline::finish_blocks() {
   return kOk;
 }
 
-int Pipeline::locate() {
+int Pipeline::locate(bool free_start) {
   HIPCHK(hipSetDevice(device_));
   if (timing) HIPCHK(hipEventRecord(ev_[0], stream_));
   hblocks_.clear();
   inflated_.clear();
   uint32_t n = 0;
   uint64_t tail = 0;
-  int rc = locate_range(base_, base_ + flen_, false, 0, 0, stream_, &n, &tail);
+  int rc = locate_range(base_, base_ + flen_, !at_eof_, free_start, 0, 0, stream_, &n, &tail);
   if (rc != kOk) return rc;
+  window_end_ = at_eof_ ? base_ + flen_ : tail;
+  if (n && at_eof_ && free_start) window_end_ = hblocks_[n - 1].coff + hblocks_[n - 1].csize;
   if (timing) {
     HIPCHK(hipEventRecord(ev_[1], stream_));
     HIPCHK(hipEventSynchronize(ev_[1]));
@@ -248,7 +276,8 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
                            float* ms) {
   *ms = 0;
   *out = SpanDev();
-  if (!dfile_ || !own_file_ || len != flen_) return fail(kErrState, "run_streamed needs a loaded file of the same size");
+  if (!dfile_ || dfile_ != own_file_.p || len != flen_ || base_ != 0 || !at_eof_)
+    return fail(kErrState, "run_streamed needs the whole file loaded in one window");
   HIPCHK(hipSetDevice(device_));
   piece = std::max<uint64_t>(piece, 1ull << 20);
   const uint64_t np = std::max<uint64_t>(1, (len + piece - 1) / piece);
@@ -287,7 +316,7 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
     const uint64_t hi = base_ + (last ? len : (k + 1) * piece);
     uint32_t nnew = 0;
     uint64_t tail = hi;
-    int rc = locate_range(lo, hi, !last, nb, total_u_, stream_loc_, &nnew, &tail);
+    int rc = locate_range(lo, hi, !last, false, nb, total_u_, stream_loc_, &nnew, &tail);
     if (rc != kOk) return rc;
     if (nnew) {
       const BlockInfo& e = hblocks_[nb + nnew - 1];
@@ -301,6 +330,7 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
     }
     lo = tail;
   }
+  window_end_ = base_ + len;
   int rc = finish_blocks();  // waits for the queued inflates (stream_)
   if (rc != kOk) return rc;
   HIPCHK(flags_.reserve(4));
@@ -333,25 +363,10 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
   const uint8_t* fbase = dfile_ - base_;
   if (timing) HIPCHK(hipEventRecord(ev_[2], stream_));
   float huff_ms = 0, lz_ms = 0;
-  // HBAM_HUFF_PROF=1: phase-A per-block cycle profile of large inflates (stderr)
-  static const bool prof_on = getenv("HBAM_HUFF_PROF") != nullptr;
-  DevBuf<uint64_t> prof;
-  const bool prof_this = prof_on && b1 - b0 >= 1024;
-  DevBuf<uint64_t> lzprof;
-  if (prof_this) {
-    HIPCHK(prof.reserve(16ull * nblk));
-    HIPCHK(hipMemsetAsync(prof.p, 0, 16ull * nblk * 8, stream_));
-    g_huff_prof = prof.p;
-    HIPCHK(lzprof.reserve(8ull * nblk));
-    HIPCHK(hipMemsetAsync(lzprof.p, 0, 8ull * nblk * 8, stream_));
-    g_lz_prof = lzprof.p;
-  }
   // Chunks of up to kInflateChunkBlocks blocks.  Phase A of chunk j runs on
   // stream_, phase B on stream_b_ after it; token buffers alternate by chunk
   // parity, so phase A of chunk j+1 overlaps phase B of chunk j (phase A needs
   // ~12 KiB of LDS per workgroup and fits beside a phase-B workgroup on a CU).
-  // HBAM_INFLATE_SERIAL=1 keeps both phases on stream_ (comparison runs).
-  static const bool serial = getenv("HBAM_INFLATE_SERIAL") != nullptr;
   struct Chunk { uint32_t b, e; };
   std::vector<Chunk> chunks;
   uint32_t b = b0;
@@ -386,11 +401,9 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
       HIPCHK(tables_[i].reserve(max_nb * kHuffTableImage));
       HIPCHK(tinfo_[i].reserve(max_nb));
     }
-  }
-  hipStream_t sb = serial ? stream_ : stream_b_;
-  if (!serial && any) {  // phase B and the table builds see everything queued on stream_ before this call
+    // phase B and the table builds see everything queued on stream_ before this call
     HIPCHK(hipEventRecord(sync_ev_[0], stream_));
-    HIPCHK(hipStreamWaitEvent(sb, sync_ev_[0], 0));
+    HIPCHK(hipStreamWaitEvent(stream_b_, sync_ev_[0], 0));
     HIPCHK(hipStreamWaitEvent(stream_t_, sync_ev_[0], 0));
   }
   for (size_t j = 0; j < nc; ++j) {
@@ -399,32 +412,27 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
     const uint64_t cu = hblocks_[cb].ustart;
     uint32_t max_stage = 0;
     for (uint32_t k = cb; k < ce; ++k) max_stage = std::max(max_stage, huff_stage_bytes(hblocks_[k]));
-    if (!serial && j >= 2) HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + par], 0));  // B(j-2) released the buffer
+    if (j >= 2) HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + par], 0));  // B(j-2) released the buffer
     if (timing) HIPCHK(hipEventRecord(tev_[3 * j], stream_));
     // tables of chunk j on stream_t_ (they overlap phase A of chunk j-1; the
     // parity buffer is free once phase A of chunk j-2 is done)
-    hipStream_t st = serial ? stream_ : stream_t_;
-    if (!serial && j >= 2) HIPCHK(hipStreamWaitEvent(st, hdone_ev_[par], 0));
-    HIPCHK(launch_huff_tables(fbase, dblocks_.p, cb, ce - cb, tables_[par].p, tinfo_[par].p, st));
-    if (!serial) {
-      HIPCHK(hipEventRecord(tab_ev_[par], st));
-      HIPCHK(hipStreamWaitEvent(stream_, tab_ev_[par], 0));
-    }
+    if (j >= 2) HIPCHK(hipStreamWaitEvent(stream_t_, hdone_ev_[par], 0));
+    HIPCHK(launch_huff_tables(fbase, dblocks_.p, cb, ce - cb, tables_[par].p, tinfo_[par].p, stream_t_));
+    HIPCHK(hipEventRecord(tab_ev_[par], stream_t_));
+    HIPCHK(hipStreamWaitEvent(stream_, tab_ev_[par], 0));
     HIPCHK(launch_inflate_huff_prebuilt(fbase, dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, max_stage,
                                         tables_[par].p, tinfo_[par].p, stream_));
-    if (!serial) HIPCHK(hipEventRecord(hdone_ev_[par], stream_));
+    HIPCHK(hipEventRecord(hdone_ev_[par], stream_));
     if (timing) HIPCHK(hipEventRecord(tev_[3 * j + 1], stream_));
-    if (!serial) {
-      HIPCHK(hipEventRecord(sync_ev_[par], stream_));
-      HIPCHK(hipStreamWaitEvent(sb, sync_ev_[par], 0));
-    }
-    HIPCHK(launch_inflate_lz77(dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, du_.p, sb));
-    if (timing) HIPCHK(hipEventRecord(tev_[3 * j + 2], sb));
-    if (!serial) HIPCHK(hipEventRecord(sync_ev_[2 + par], sb));
+    HIPCHK(hipEventRecord(sync_ev_[par], stream_));
+    HIPCHK(hipStreamWaitEvent(stream_b_, sync_ev_[par], 0));
+    HIPCHK(launch_inflate_lz77(dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, du_.p, stream_b_));
+    if (timing) HIPCHK(hipEventRecord(tev_[3 * j + 2], stream_b_));
+    HIPCHK(hipEventRecord(sync_ev_[2 + par], stream_b_));
     for (uint32_t k = cb; k < ce; ++k) inflated_[k] = 1;
     ++inflate_launches_;
   }
-  if (!serial && any) {  // everything after this call on stream_ sees phase B done
+  if (any) {  // everything after this call on stream_ sees phase B done
     HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + ((nc - 1) & 1)], 0));
     if (nc >= 2) HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + ((nc - 2) & 1)], 0));
   }
@@ -444,39 +452,6 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
       huff_ms += a;
       lz_ms += c;
     }
-  }
-  g_huff_prof = nullptr;
-  g_lz_prof = nullptr;
-  if (prof_this && any) {
-    HIPCHK(hipStreamSynchronize(stream_));
-    std::vector<uint64_t> hl(8ull * nblk);
-    HIPCHK(hipMemcpy(hl.data(), lzprof.p, hl.size() * 8, hipMemcpyDeviceToHost));
-    double la[8] = {0};
-    uint64_t ln = 0;
-    for (uint32_t k = b0; k < b1; ++k) {
-      if (hl[8ull * k + 5] == 0) continue;
-      ++ln;
-      for (int i = 0; i < 8; ++i) la[i] += (double)hl[8ull * k + i];
-    }
-    static const char* lnames[8] = {"scan", "fill_own", "fill_wait", "resolve", "store", "total", "loads", "-"};
-    fprintf(stderr, "[lz77 prof] %llu blocks, mean cycles per block:", (unsigned long long)ln);
-    for (int i = 0; i < 7; ++i) fprintf(stderr, " %s=%.0f", lnames[i], ln ? la[i] / ln : 0.0);
-    fprintf(stderr, "\n");
-    std::vector<uint64_t> h(16ull * nblk);
-    HIPCHK(hipMemcpy(h.data(), prof.p, h.size() * 8, hipMemcpyDeviceToHost));
-    double acc[11] = {0};
-    uint64_t n = 0;
-    for (uint32_t k = b0; k < b1; ++k) {
-      if (h[16ull * k + 10] == 0) continue;
-      ++n;
-      for (int i = 0; i < 11; ++i) acc[i] += (double)h[16ull * k + i];
-    }
-    static const char* names[11] = {"stage", "wave0_hdr", "spec", "sync", "scan", "emit", "handback", "tables",
-                                     "passes", "sync_iters", "total"};
-    fprintf(stderr, "[huff prof] %llu blocks, mean cycles per block:", (unsigned long long)n);
-    for (int i = 0; i < 11; ++i)
-      fprintf(stderr, " %s=%.0f", names[i], n ? acc[i] / n : 0.0);
-    fprintf(stderr, "\n");
   }
   if (!any) {
     times.inflate = times.huff = times.lz77 = 0;
@@ -540,7 +515,7 @@ int64_t Pipeline::pos_of_voff(uint64_t voff) const {
     uint32_t mid = (lo + hi) / 2;
     if (hblocks_[mid].coff >= coff) hi = mid; else lo = mid + 1;
   }
-  if (lo >= n) return (coff == base_ + flen_ && uoff == 0) ? (int64_t)total_u_ : -1;
+  if (lo >= n) return (coff == window_end_ && uoff == 0) ? (int64_t)total_u_ : -1;
   if (hblocks_[lo].coff != coff || uoff > hblocks_[lo].isize) return -1;
   return (int64_t)(hblocks_[lo].ustart + uoff);
 }
@@ -554,7 +529,7 @@ uint64_t Pipeline::q_end_of(uint64_t vend) const {
     uint32_t mid = (lo + hi) / 2;
     if (hblocks_[mid].coff >= c) hi = mid; else lo = mid + 1;
   }
-  if (lo >= n) return total_u_ + 1;  // every position qualifies
+  if (lo >= n) return total_u_ + 1;  // every position of the window qualifies
   const BlockInfo& b = hblocks_[lo];
   if (b.coff == c) return b.ustart + std::min<uint64_t>(u, b.isize);
   return b.ustart;
@@ -574,14 +549,19 @@ int Pipeline::read_stream(uint64_t pos, uint64_t len, std::vector<uint8_t>* out)
 }
 
 int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool decode, SpanDev* out) {
-  HIPCHK(hipSetDevice(device_));
   *out = SpanDev();
   const int64_t sp = pos_of_voff(vstart);
   if (sp < 0) return fail(kErrIO, "Invalid file pointer: " + std::to_string(vstart));
-  const uint64_t p0 = (uint64_t)sp;
+  return decode_span_pos((uint64_t)sp, vend, mode, decode, out);
+}
+
+int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool decode, SpanDev* out) {
+  HIPCHK(hipSetDevice(device_));
+  *out = SpanDev();
   const uint64_t q_end = q_end_of(vend);
   out->p0 = p0;
   out->q_end = q_end;
+  out->next_pos = p0;
   const uint32_t nblk = (uint32_t)hblocks_.size();
   if (p0 >= q_end || p0 >= total_u_) return kOk;
   const uint32_t k0 = block_containing(p0);
@@ -589,20 +569,26 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
   uint32_t inf_end = std::min(nblk, k1 + 2);
   ChainArgs a{};
   a.blocks = dblocks_.p;
-  a.e_true = total_u_;
+  a.e_true = at_eof_ ? total_u_ : kOpenEnd;
   a.p0 = p0;
   a.q_end = q_end;
   a.dead = dead_.p;
   a.ndead = ndead_;
   a.n_ref = n_ref_;
   a.k0 = k0;
+  a.validate = mode != kReader ? 0 : stringency_ == kStrict ? 2 : stringency_ == kLenient ? 1 : 0;
+  a.ref_len = n_ref_len_ == (uint32_t)std::max(n_ref_, 0) && n_ref_len_ ? ref_len_.p : nullptr;
   if (timing) HIPCHK(hipEventRecord(ev_[0], stream_));
-  float infl_ms = 0;
+  float infl_ms = 0, huff_ms = 0, lz_ms = 0;
   bool lists = true;  // chain v2 lists hold every record start (no overflow)
   for (int it = 0;; ++it) {
     if (it >= kMaxChainIters) return fail(kErrState, "record chain did not converge");
     int rc = inflate(k0, inf_end);
-    if (timing) infl_ms += times.inflate;
+    if (timing) {
+      infl_ms += times.inflate;
+      huff_ms += times.huff;
+      lz_ms += times.lz77;
+    }
     if (rc != kOk) return rc;
     a.u = du_.p;
     a.e_inf = inf_end < nblk ? hblocks_[inf_end].ustart : total_u_;
@@ -643,47 +629,27 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
     a.scan_bytes = lsb;
     HIPCHK(hipMemsetAsync(need_.p, 0, 8, stream_));
     HIPCHK(hipMemsetAsync(counters_.p, 0, 16, stream_));
-    HIPCHK(launch_chain(a, mode, 5, stream_));  // candidates + lane-per-block walks
+    HIPCHK(launch_chain(a, mode, kStageWalk, stream_));  // candidates + lane-per-block walks
     // link: max-scan of the walk exits; re-walk blocks that are off the chain
     bool serial = false;
     for (int fix = 0;; ++fix) {
       HIPCHK(hipMemsetAsync(counters_.p, 0, 8, stream_));
-      HIPCHK(launch_chain(a, mode, 6, stream_));
+      HIPCHK(launch_chain(a, mode, kStageLinkCheck, stream_));
       uint32_t ctr[2] = {0, 0};
       HIPCHK(hipMemcpyAsync(ctr, counters_.p, 8, hipMemcpyDeviceToHost, stream_));
       HIPCHK(hipStreamSynchronize(stream_));
-      static const bool dbg = getenv("HBAM_DEBUG_LINK") != nullptr;
-      if (dbg && (ctr[0] || ctr[1])) {  // print the first flagged blocks of this round
-        std::vector<uint64_t> hg(nb), hx(nb), hin(nb), hf(nb);
-        HIPCHK(hipMemcpy(hg.data(), g_.p, nb * 8, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(hx.data(), x_.p, nb * 8, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(hin.data(), base_arr_.p, nb * 8, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(hf.data(), force_.p, nb * 8, hipMemcpyDeviceToHost));
-        int shown = 0;
-        fprintf(stderr, "[link] round %d hard=%u fix=%u nb=%u\n", fix, ctr[0], ctr[1], nb);
-        for (uint32_t i = 0; i < nb && shown < 6; ++i) {
-          const BlockInfo& b = hblocks_[k0 + i];
-          const bool flagged = hf[i] != kNone || (i > 0 && hin[i] < b.ustart && hin[i] < q_end);
-          if (!flagged) continue;
-          ++shown;
-          fprintf(stderr, "  blk %u ustart=%llu bend=%llu in=%lld g=%lld x=%lld force=%lld prev_g=%lld prev_x=%lld\n", i,
-                  (unsigned long long)b.ustart, (unsigned long long)(b.ustart + b.isize), (long long)hin[i],
-                  (long long)hg[i], (long long)hx[i], (long long)hf[i], i ? (long long)hg[i - 1] : -1,
-                  i ? (long long)hx[i - 1] : -1);
-        }
-      }
       if (ctr[0]) { serial = true; break; }
       if (ctr[1] == 0) break;
       if (fix == kMaxLinkFix) { serial = true; break; }
       ++link_rewalks_;
-      HIPCHK(launch_chain(a, mode, 7, stream_));
+      HIPCHK(launch_chain(a, mode, kStageRewalk, stream_));
     }
     uint64_t sm[2] = {0, 0};
     unsigned long long need = 0;
     if (serial) {  // exact serial link (writes entry[] + summary), then lists off entry[]
       ++link_fallbacks_;
-      HIPCHK(launch_chain(a, mode, 1, stream_));
-      HIPCHK(launch_chain(a, mode, 8, stream_));
+      HIPCHK(launch_chain(a, mode, kStageSerialLink, stream_));
+      HIPCHK(launch_chain(a, mode, kStageRewalkAll, stream_));
       HIPCHK(hipMemcpyAsync(sm, summary_.p, 16, hipMemcpyDeviceToHost, stream_));
     } else {  // final chain position = max of every walk exit; no stop
       uint64_t t[2] = {0, 0};
@@ -697,7 +663,7 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
     HIPCHK(hipMemcpyAsync(&ovf, counters_.p + 2, 4, hipMemcpyDeviceToHost, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
     lists = ovf == 0;
-    HIPCHK(launch_chain(a, mode, lists ? 9 : 2, stream_));  // count + validate
+    HIPCHK(launch_chain(a, mode, lists ? kStageCheck : kStageCount, stream_));  // count + validate
     HIPCHK(hipMemcpyAsync(&need, need_.p, 8, hipMemcpyDeviceToHost, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
     const uint64_t final_pos = sm[0];
@@ -731,7 +697,7 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
     HIPCHK(launch_truncate_counts(cnt_.p, nb, flags_.p + 3, stream_));
     out->status = code;
     const BlockInfo& b = hblocks_[k0 + first];
-    const char* what = code == kErrFormat ? "Invalid record length"
+    const char* what = code == kErrFormat ? "Invalid record (SAMFormatException)"
                        : code == kErrTrunc ? "Premature EOF in BAM record"
                        : code == kErrArg   ? "Reference index not found in sequence dictionary"
                                            : "Invalid alignment";
@@ -767,11 +733,15 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
     if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
     HIPCHK(launch_rec_out(a, mode, dec, c, stream_));
   } else {      // a block listed more starts than kListCap: per-block walks
-    HIPCHK(launch_chain(a, mode, 3, stream_));
+    HIPCHK(launch_chain(a, mode, kStageEmit, stream_));
     if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
     if (dec) HIPCHK(launch_rec_decode(du_.p, rec_pos_.p, total, c, stream_));
   }
   if (dec) HIPCHK(launch_long_hash(du_.p, rec_pos_.p, c, stream_));
+  // the next record's start: the chain successor of the last record
+  HIPCHK(scalars_.reserve(4));
+  HIPCHK(launch_next_pos(du_.p, rec_pos_.p, total, p0, mode, scalars_.p, stream_));
+  HIPCHK(hipMemcpyAsync(&out->next_pos, scalars_.p, 8, hipMemcpyDeviceToHost, stream_));
   if (timing) HIPCHK(hipEventRecord(ev_[2], stream_));
   HIPCHK(hipStreamSynchronize(stream_));
   if (timing) {
@@ -781,6 +751,8 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
     times.chain = all - infl_ms;
     times.decode = dcd;
     times.inflate = infl_ms;
+    times.huff = huff_ms;
+    times.lz77 = lz_ms;
   }
   return kOk;
 }
@@ -889,16 +861,31 @@ int Pipeline::decode_writables(const uint8_t* buf, uint64_t len, const uint64_t*
   return kOk;
 }
 
-int Pipeline::splitting_entries(const SpanDev& span, uint32_t g, std::vector<uint64_t>* out) {
+int Pipeline::splitting_entries(const SpanDev& span, uint32_t g, uint64_t o0, std::vector<uint64_t>* out) {
   out->clear();
-  const uint64_t m = span.n / g;
+  // global ordinals o0 .. o0+n-1; entries at ordinals k*g - 1
+  const uint64_t m = (o0 + span.n) / g - o0 / g;
   if (m == 0) return kOk;
   DevBuf<uint64_t> ent;
-  HIPCHK(ent.reserve(m + 1));
-  HIPCHK(launch_sbi_emit(span.rec_voff, span.n, g, ent.p, stream_));
+  HIPCHK(ent.reserve(m));
+  HIPCHK(launch_sbi_emit(span.rec_voff, span.n, g, o0, ent.p, stream_));
   out->resize(m);
-  HIPCHK(hipMemcpyAsync(out->data(), ent.p + 1, m * 8, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipMemcpyAsync(out->data(), ent.p, m * 8, hipMemcpyDeviceToHost, stream_));
   HIPCHK(hipStreamSynchronize(stream_));
+  return kOk;
+}
+
+int Pipeline::span_digest(const SpanDev& span, uint64_t* key_xor, uint64_t* voff_sum) {
+  *key_xor = *voff_sum = 0;
+  if (span.n == 0) return kOk;
+  HIPCHK(scalars_.reserve(4));
+  HIPCHK(hipMemsetAsync(scalars_.p, 0, 32, stream_));
+  HIPCHK(launch_digest(span.col.key, span.rec_voff, span.n, scalars_.p + 1, stream_));
+  uint64_t d[2];
+  HIPCHK(hipMemcpyAsync(d, scalars_.p + 1, 16, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  *key_xor = d[0];
+  *voff_sum = d[1];
   return kOk;
 }
 

@@ -1,10 +1,15 @@
-// hbam_pipeline.h -- one-GPU device pipeline for the BAM read hot path.
+// hbam_pipeline.h -- one HBM window of the BAM read hot path on one GPU.
 //
-// Owns the device-resident compressed file, its BGZF block table, the
-// inflated stream and the per-span record arrays.  All compute runs in the
-// gfx950 kernels of hbam_kernels.hip; the host only sizes buffers, launches,
-// and reads back counters.  There is no CPU fallback: any HIP failure is an
-// error returned to the caller.
+// A Pipeline holds one window of a BGZF file: the compressed bytes [lo, hi)
+// (copied from host memory or attached from a device-resident copy), its BGZF
+// block table, the inflated stream of those blocks and the per-span record
+// arrays.  A window that stops short of the end of the file is "open": a
+// record that runs past its last block is not truncated, it is left for the
+// next window (BamFile in hbam_host.h moves windows along a span and carries
+// the next record's position across).  All compute runs in the gfx950
+// kernels of hbam_kernels.hip; the host sizes buffers, launches and reads
+// back counters.  There is no CPU fallback: any HIP failure is an error
+// returned to the caller.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -58,7 +63,8 @@ struct DevBuf {
 // Result of one span decode, resident on the device.
 struct SpanDev {
   uint64_t n = 0;                 // records
-  uint64_t p0 = 0, q_end = 0;     // logical positions
+  uint64_t p0 = 0, q_end = 0;     // window positions: span start, first position past the span
+  uint64_t next_pos = 0;          // chain position after the last record (the next record's start)
   int status = kOk;               // status of the first failing record (records before it are valid)
   std::string error;
   uint64_t* rec_pos = nullptr;    // device
@@ -71,6 +77,10 @@ struct StageTimes {  // milliseconds of the last decode (HIP events)
   float locate = 0, inflate = 0, huff = 0, lz77 = 0, chain = 0, decode = 0;
 };
 
+// Record-level validation ([htsjdk] ValidationStringency, the
+// hadoopbam.samheaderreader.validation-stringency property).
+enum Stringency : int { kStrict = 0, kLenient = 1, kSilent = 2 };
+
 class Pipeline {
  public:
   explicit Pipeline(int device);
@@ -82,24 +92,32 @@ class Pipeline {
   hipStream_t stream() const { return stream_; }
   const std::string& error() const { return err_; }
 
-  // Copy a BGZF file (or a BGZF-aligned shard) into HBM.  base_offset is the
-  // file offset of data[0] (shards); voffs are reported in file coordinates.
-  int load(const uint8_t* data, uint64_t len, uint64_t base_offset = 0);
-  // Copy the same-size file bytes into the resident buffer again, timed with
+  // Copy file bytes [base, base + len) into the window buffer.  at_eof: the
+  // range ends at the end of the file (else the window is open).
+  int load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof);
+  // Use device-resident file bytes [base, base + len) (readable for kFilePad
+  // bytes past len).
+  int attach_device(const uint8_t* dptr, uint64_t len, uint64_t base, bool at_eof);
+  // Copy the same-size window bytes into the resident buffer again, timed with
   // HIP events (PCIe-inclusive measurements); pinned: from a page-locked copy.
   int reload(const uint8_t* data, uint64_t len, bool pinned, float* ms);
   // hipMemcpy device-to-device bandwidth (read + write bytes per second / 1e9)
   int d2d_bandwidth(uint64_t bytes, int iters, float* gbps);
-  // Use an already device-resident buffer (must be padded by kFilePad bytes).
-  int attach_device(const uint8_t* dptr, uint64_t len, uint64_t base_offset = 0);
   uint64_t file_len() const { return flen_; }
+  uint64_t base() const { return base_; }
+  bool at_eof() const { return at_eof_; }
   const uint8_t* d_file() const { return dfile_; }
 
-  // BGZF block discovery over the whole loaded range.
-  int locate();
+  // BGZF block discovery over the window.  An open window keeps only the
+  // blocks that end inside it.  free_start: the window may begin inside a
+  // block (split-guess windows); the block chain starts at the first header
+  // candidate whose BSIZE chain runs to the window end.
+  int locate(bool free_start = false);
   const std::vector<BlockInfo>& blocks() const { return hblocks_; }
   uint64_t total_u() const { return total_u_; }
   const BlockInfo* d_blocks() const { return dblocks_.p; }
+  // file offset just past the last located block (where the next window starts)
+  uint64_t window_end() const { return window_end_; }
 
   // Inflate blocks [b0, b1) into the contiguous inflated stream.  check =
   // false leaves the work queued (no DEFLATE error check, no host wait).
@@ -116,8 +134,13 @@ class Pipeline {
   const uint8_t* d_u() const { return du_.p; }
 
   // Record chain over the span [vstart, vend) under reader or indexer rules;
-  // decode=true also fills the SoA columns + keys (reader mode only).
+  // decode=true also fills the SoA columns + keys (reader mode only).  In an
+  // open window the span also ends at the first record that does not end
+  // inside the window (out->next_pos = its start).
   int decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool decode, SpanDev* out);
+  // Same, from a window position (index mode: a carried position may lie
+  // past the first block).
+  int decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool decode, SpanDev* out);
 
   // Header bytes: inflate the first blocks until `need` stream bytes exist.
   int read_stream(uint64_t pos, uint64_t len, std::vector<uint8_t>* out);
@@ -133,8 +156,11 @@ class Pipeline {
   // last ends at len): SoA columns + keys; out->n stops at the first bad value.
   int decode_writables(const uint8_t* buf, uint64_t len, const uint64_t* offs, uint64_t n, SpanDev* out);
 
-  // .splitting-bai entries (without the leading header voff / trailing size)
-  int splitting_entries(const SpanDev& span, uint32_t granularity, std::vector<uint64_t>* out);
+  // .splitting-bai entries of a span whose first record has global ordinal
+  // `ordinal0` (SplittingBAMIndexer.java:273-277: ordinals k*g - 1)
+  int splitting_entries(const SpanDev& span, uint32_t granularity, uint64_t ordinal0, std::vector<uint64_t>* out);
+  // order-independent digests of a decoded span's keys / voffs (bench checks)
+  int span_digest(const SpanDev& span, uint64_t* key_xor, uint64_t* voff_sum);
 
   // host helpers on the block table
   int64_t pos_of_voff(uint64_t voff) const;
@@ -144,6 +170,9 @@ class Pipeline {
 
   void set_n_ref(int32_t n) { n_ref_ = n; }
   int32_t n_ref() const { return n_ref_; }
+  void set_stringency(int s) { stringency_ = s; }
+  // reference lengths for the STRICT alignment-start checks (empty = none)
+  int set_ref_lengths(const std::vector<int32_t>& lens);
 
   uint64_t link_fallbacks() const { return link_fallbacks_; }
   uint64_t link_rewalks() const { return link_rewalks_; }
@@ -156,8 +185,8 @@ class Pipeline {
   // BGZF blocks of [lo, hi) appended at index nprev with ustart from ubase,
   // on stream s (synchronized).  partial: a block cut by hi is left out and
   // *tail = its start (hi when none).
-  int locate_range(uint64_t lo, uint64_t hi, bool partial, uint32_t nprev, uint64_t ubase, hipStream_t s,
-                   uint32_t* nnew, uint64_t* tail);
+  int locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_start, uint32_t nprev, uint64_t ubase,
+                   hipStream_t s, uint32_t* nnew, uint64_t* tail);
   int finish_blocks();  // total_u_, dead positions, pads, per-block state after locate
   // SoA store for n records (voff = rec_voff_) + the deferred long-key list
   int alloc_columns(uint64_t n, uint64_t stream_bytes, Columns* c);
@@ -172,14 +201,19 @@ class Pipeline {
   std::string err_;
 
   uint8_t* dfile_ = nullptr;
-  bool own_file_ = false;
+  DevBuf<uint8_t> own_file_;  // window bytes copied from the host (+ kFilePad zeros)
   uint64_t flen_ = 0, base_ = 0;
+  bool at_eof_ = true;
+  uint64_t window_end_ = 0;
 
   DevBuf<BlockInfo> dblocks_;
   std::vector<BlockInfo> hblocks_;
   uint64_t total_u_ = 0;
   uint32_t ndead_ = 0;
   int32_t n_ref_ = 0;
+  int stringency_ = kStrict;
+  DevBuf<int32_t> ref_len_;
+  uint32_t n_ref_len_ = 0;
   uint64_t link_fallbacks_ = 0;
   uint64_t link_rewalks_ = 0;      // re-walk rounds of the parallel link
   uint64_t inflate_launches_ = 0;  // phase A/B launch pairs so far
@@ -212,6 +246,7 @@ class Pipeline {
   DevBuf<uint8_t> wbuf_;                 // readFields: serialized values
   DevBuf<uint64_t> woffs_;               // readFields: value framing
   DevBuf<unsigned long long> wbad_;      // readFields: first bad value
+  DevBuf<uint64_t> scalars_;             // next_pos / digests read back by the host
 
   hipEvent_t ev_[8];
   hipEvent_t sync_ev_[4];           // [0,1] phase A done, [2,3] phase B done, per token buffer

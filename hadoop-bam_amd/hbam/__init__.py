@@ -27,13 +27,21 @@ ERROR_NAMES = {1: "SAMFormatException", 2: "FileTruncatedException", 3: "Illegal
 u64, i64, i32, u32, P = C.c_uint64, C.c_int64, C.c_int32, C.c_uint32, C.c_void_p
 
 
+STRICT, LENIENT, SILENT = 0, 1, 2  # hadoopbam.samheaderreader.validation-stringency
+
+
 class Opts(C.Structure):
-    _fields_ = [("device", i32), ("check_crc", i32), ("reserved0", i32), ("reserved1", i32)]
+    _fields_ = [("device", i32), ("check_crc", i32), ("stringency", i32), ("reserved", i32),
+                ("window_bytes", u64)]
+
+
+def _opts(device=0, check_crc=False, stringency=STRICT, window_bytes=0):
+    return Opts(device, int(check_crc), stringency, 0, window_bytes)
 
 
 class HeaderInfo(C.Structure):
     _fields_ = [("n_ref", i32), ("l_text", i32), ("first_record_voff", u64), ("file_size", u64),
-                ("n_blocks", u64), ("uncompressed_size", u64), ("text", C.c_char_p)]
+                ("text", C.c_char_p)]
 
 
 _COLS = [("ref_id", np.int32), ("pos", np.int32), ("l_seq", np.int32), ("next_ref_id", np.int32),
@@ -44,7 +52,8 @@ _COLS = [("ref_id", np.int32), ("pos", np.int32), ("l_seq", np.int32), ("next_re
 
 class Batch(C.Structure):
     _fields_ = [("n", u64)] + [(n, P) for n, _ in _COLS] + [("data", P), ("data_len", u64),
-                                                            ("status", i32), ("reserved", i32)]
+                                                            ("status", i32), ("reserved", i32),
+                                                            ("next_voff", u64)]
 
 
 class GpuStats(C.Structure):
@@ -53,7 +62,7 @@ class GpuStats(C.Structure):
                 ("ms_locate", C.c_float), ("ms_inflate", C.c_float), ("ms_huff", C.c_float),
                 ("ms_lz77", C.c_float), ("ms_chain", C.c_float), ("ms_decode", C.c_float),
                 ("ms_total", C.c_float), ("status", i32), ("link_fallbacks", i32),
-                ("inflate_launches", i32), ("link_rewalks", i32)]
+                ("inflate_launches", i32), ("link_rewalks", i32), ("windows", i32), ("reserved", i32)]
 
 
 def _sig(name, res, args):
@@ -72,7 +81,13 @@ _sig("hbam_last_error", C.c_char_p, [P])
 _sig("hbam_free", None, [P])
 _sig("hbam_header", C.c_int, [P, C.POINTER(HeaderInfo)])
 _sig("hbam_ref", C.c_int, [P, i32, C.POINTER(C.c_char_p), C.POINTER(i32)])
-_sig("hbam_decode_span", C.c_int, [P, u64, u64, C.POINTER(Batch)])
+_sig("hbam_decode_span", C.c_int, [P, u64, u64, u64, C.POINTER(Batch)])
+_sig("hbam_decode_span_device", C.c_int, [P, u64, u64, i32, C.POINTER(GpuStats)])
+_sig("hbam_reader_position", C.c_int, [P, u64, C.POINTER(u64)])
+_sig("hbam_file_stats", C.c_int, [P, C.POINTER(u64), C.POINTER(u64)])
+_sig("hbam_bytes_read", C.c_int, [P, C.POINTER(u64)])
+_sig("hbam_prefetch", C.c_int, [P, u64, u64])
+_sig("hbam_splitting_index_for_records", C.c_int, [C.POINTER(Opts), P, u64, i32, u64, C.POINTER(P), C.POINTER(u64)])
 _sig("hbam_build_splitting_index", C.c_int, [P, i32, C.POINTER(P), C.POINTER(u64)])
 _sig("hbam_guess_record_starts", C.c_int, [P, P, P, u64, P])
 _sig("hbam_guess_bgzf_block_starts", C.c_int, [P, P, P, u64, P])
@@ -86,7 +101,9 @@ _sig("hbam_device_count", i32, [])
 _sig("hbam_gpu_create", C.c_int, [i32, C.POINTER(P)])
 _sig("hbam_gpu_destroy", None, [P])
 _sig("hbam_gpu_error", C.c_char_p, [P])
-_sig("hbam_gpu_load", C.c_int, [P, P, u64, u64, i32, u64])
+_sig("hbam_gpu_load", C.c_int, [P, P, u64])
+_sig("hbam_gpu_set_window", C.c_int, [P, u64])
+_sig("hbam_gpu_index", C.c_int, [P, i32, C.POINTER(P), C.POINTER(u64), C.POINTER(C.c_float)])
 _sig("hbam_gpu_run", C.c_int, [P, i32, C.POINTER(GpuStats)])
 _sig("hbam_gpu_fetch", C.c_int, [P, P, P, u64])
 _sig("hbam_encode_writables", C.c_int, [P, P, u64, P, C.POINTER(u64)])
@@ -137,20 +154,23 @@ def bgzf_compress(data, block_lens=None, block_size=HTSJDK_BLOCK_SIZE, level=5, 
     (hbam_bgzf_compress): the BGZF file bytes.  block_lens (optional) cuts
     the payload as the writer's flushes did; else every block_size bytes."""
     if isinstance(data, np.ndarray):
-        buf, n = data, data.nbytes
-        ptr = data.ctypes.data if n else None
+        buf = np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+        n = buf.nbytes
+        ptr = buf.ctypes.data if n else None
     else:
         buf = C.create_string_buffer(bytes(data), max(len(data), 1))
         ptr, n = buf, len(data)
-    lens = None
-    nl = 0
+    lens_ptr, nl = None, 0
     if block_lens is not None:
+        # an explicit list (even an empty one) is passed as a non-NULL pointer,
+        # so the C side checks that it covers the payload
         lens = np.ascontiguousarray(np.asarray(block_lens, dtype=np.uint32))
-        nl = len(lens)
-    o = Opts(device, 0, 0, 0)
+        keep = lens if len(lens) else np.zeros(1, np.uint32)
+        lens_ptr, nl = keep.ctypes.data, len(lens)
+    o = _opts(device)
     out = P()
     olen = u64()
-    rc = _L.hbam_bgzf_compress(C.byref(o), ptr, n, lens.ctypes.data if nl else None, nl, block_size, level,
+    rc = _L.hbam_bgzf_compress(C.byref(o), ptr, n, lens_ptr, nl, block_size, level,
                                BGZF_EOF if eof else 0, C.byref(out), C.byref(olen))
     if rc != OK:
         raise HbamError(rc, _L.hbam_gpu_error(None).decode())
@@ -168,8 +188,29 @@ def get_key(ref_idx, alignment_start):
     return _L.hbam_get_key(ref_idx, alignment_start)
 
 
+def splitting_index_for_records(voffs, granularity, file_size, device=0) -> bytes:
+    """Write-time .splitting-bai (SplittingBAMIndexer.processAlignment over
+    records with these voffs, then finish(file_size)), entries on the GPU."""
+    v = np.ascontiguousarray(voffs, np.uint64)
+    keep = v if len(v) else np.zeros(1, np.uint64)
+    out = P()
+    n = u64()
+    rc = _L.hbam_splitting_index_for_records(C.byref(_opts(device)), keep.ctypes.data, len(v), granularity,
+                                             file_size, C.byref(out), C.byref(n))
+    if rc != OK:
+        raise HbamError(rc, _L.hbam_last_error(None).decode())
+    try:
+        return C.string_at(out, n.value)
+    finally:
+        _L.hbam_free(out)
+
+
+def _stats_dict(st):
+    return {f: getattr(st, f) for f, _ in GpuStats._fields_}
+
+
 def _batch_dict(b, rc):
-    out = {"status": rc}
+    out = {"status": rc, "next_voff": b.next_voff}
     for name, dt in _COLS:
         p = getattr(b, name)
         nb = b.n * np.dtype(dt).itemsize
@@ -217,7 +258,7 @@ class Codec:
 
     def __init__(self, device=0):
         self._h = P()
-        rc = _L.hbam_open_codec(C.byref(Opts(device, 0, 0, 0)), C.byref(self._h))
+        rc = _L.hbam_open_codec(C.byref(_opts(device)), C.byref(self._h))
         if rc != OK:
             msg = _L.hbam_last_error(self._h).decode(errors="replace")
             _L.hbam_close(self._h)
@@ -240,11 +281,14 @@ class Codec:
 
 
 class BamFile:
-    """An opened BAM (or plain BGZF with bam=False) on one GPU."""
+    """An opened BAM (or plain BGZF with bam=False) on one GPU.  path= opens
+    a file split-locally (only the windows a decode needs are read);
+    window_bytes = compressed bytes per HBM window (0: 4 GiB)."""
 
-    def __init__(self, data: bytes = None, path: str = None, device=0, bam=True, check_crc=False):
+    def __init__(self, data: bytes = None, path: str = None, device=0, bam=True, check_crc=False,
+                 stringency=STRICT, window_bytes=0):
         self._h = P()
-        o = Opts(device, int(check_crc), 0, 0)
+        o = _opts(device, check_crc, stringency, window_bytes)
         if path is not None:
             rc = _L.hbam_open(path.encode(), C.byref(o), C.byref(self._h))
             self.size = os.path.getsize(path)
@@ -288,8 +332,45 @@ class BamFile:
             raise self._err(rc)
         text = C.string_at(h.text, h.l_text).decode(errors="replace") if h.l_text else ""
         return {"n_ref": h.n_ref, "l_text": h.l_text, "first_record_voff": h.first_record_voff,
-                "file_size": h.file_size, "n_blocks": h.n_blocks,
-                "uncompressed_size": h.uncompressed_size, "text": text}
+                "file_size": h.file_size, "text": text}
+
+    def file_stats(self):
+        """(BGZF blocks, inflated bytes) of the whole file."""
+        nb, us = u64(), u64()
+        rc = _L.hbam_file_stats(self._h, C.byref(nb), C.byref(us))
+        if rc != OK:
+            raise self._err(rc)
+        return nb.value, us.value
+
+    def bytes_read(self):
+        """Host -> HBM bytes this file has copied so far."""
+        n = u64()
+        rc = _L.hbam_bytes_read(self._h, C.byref(n))
+        if rc != OK:
+            raise self._err(rc)
+        return n.value
+
+    def prefetch(self, lo, hi):
+        rc = _L.hbam_prefetch(self._h, lo, hi)
+        if rc != OK:
+            raise self._err(rc)
+
+    def reader_position(self, i):
+        """BAMRecordReader.getProgress's in.position() after record i of the last batch."""
+        v = u64()
+        rc = _L.hbam_reader_position(self._h, i, C.byref(v))
+        if rc != OK:
+            raise self._err(rc)
+        return v.value
+
+    def decode_span_device(self, vstart, vend, timing=False, decode=True, digest=True):
+        """The span decoded with the records left in HBM: stats dict."""
+        st = GpuStats()
+        flags = (1 if timing else 0) | (0 if decode else 2) | (4 if digest else 0)
+        rc = _L.hbam_decode_span_device(self._h, vstart, vend, flags, C.byref(st))
+        if rc != OK:
+            raise self._err(rc)
+        return _stats_dict(st)
 
     def ref(self, i):
         name = C.c_char_p()
@@ -299,15 +380,29 @@ class BamFile:
             raise self._err(rc)
         return name.value.decode(), ln.value
 
-    def decode_span(self, vstart, vend, raise_on_error=True):
-        """SoA dict for FileVirtualSplit [vstart, vend); 'status' holds the
-        status of a record that ended the span early."""
+    def decode_span(self, vstart, vend, raise_on_error=True, max_records=0):
+        """SoA dict for FileVirtualSplit [vstart, vend) (at most max_records
+        records; 0 = all); 'status' holds the status of a record that ended
+        the span early, 'next_voff' where the next batch continues."""
         b = Batch()
-        rc = _L.hbam_decode_span(self._h, vstart, vend, C.byref(b))
+        rc = _L.hbam_decode_span(self._h, vstart, vend, max_records, C.byref(b))
         if rc != OK and (raise_on_error or b.n == 0 and rc not in (E_FORMAT, E_TRUNC, E_ARG, E_IO)):
             raise self._err(rc)
         self._last_n = b.n
         return _batch_dict(b, rc)
+
+    def iter_batches(self, vstart, vend, max_records, raise_on_error=True):
+        """The split in bounded batches (BAMRecordReader's iteration)."""
+        v = vstart
+        while v < vend:
+            r = self.decode_span(v, vend, raise_on_error=raise_on_error, max_records=max_records)
+            if len(r["key"]):
+                yield r
+            if r["status"] != OK or not len(r["key"]):
+                if r["status"] != OK:
+                    yield r
+                return
+            v = r["next_voff"]
 
     def encode_writables(self):
         """SAMRecordWritable.write of every record of the last decode_span
@@ -418,25 +513,41 @@ class Gpu:
         except Exception:
             pass
 
-    def load(self, data, base_offset=0, n_ref=0, first_pos=None):
+    def load(self, data):
+        """Make a whole BAM resident in HBM (header parsed)."""
         if isinstance(data, np.ndarray):
             ptr, n = data.ctypes.data, data.nbytes
             self._keep = data
         else:
             self._keep = C.create_string_buffer(bytes(data), len(data))
             ptr, n = self._keep, len(data)
-        fp = (1 << 64) - 1 if first_pos is None else first_pos
-        rc = _L.hbam_gpu_load(self._h, ptr, n, base_offset, n_ref, fp)
+        rc = _L.hbam_gpu_load(self._h, ptr, n)
         if rc != OK:
             raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
         self._keep = None
 
-    def run(self, timing=False, decode=True):
+    def set_window(self, window_bytes):
+        _L.hbam_gpu_set_window(self._h, window_bytes)
+
+    def run(self, timing=False, decode=True, digest=False):
         st = GpuStats()
-        rc = _L.hbam_gpu_run(self._h, (1 if timing else 0) | (0 if decode else 2), C.byref(st))
+        flags = (1 if timing else 0) | (0 if decode else 2) | (4 if digest else 0)
+        rc = _L.hbam_gpu_run(self._h, flags, C.byref(st))
         if rc != OK:
             raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
-        return {f: getattr(st, f) for f, _ in GpuStats._fields_}
+        return _stats_dict(st)
+
+    def index(self, granularity=4096):
+        """.splitting-bai of the resident file: (bytes, ms)."""
+        p = P()
+        n = u64()
+        ms = C.c_float()
+        rc = _L.hbam_gpu_index(self._h, granularity, C.byref(p), C.byref(n), C.byref(ms))
+        if rc != OK:
+            raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
+        b = C.string_at(p, n.value)
+        _L.hbam_free(p)
+        return b, ms.value
 
     def run_streamed(self, ptr, nbytes, piece_bytes=64 << 20):
         """hbam_gpu_run_streamed: copy the file from host memory at `ptr` in
@@ -445,7 +556,7 @@ class Gpu:
         rc = _L.hbam_gpu_run_streamed(self._h, ptr, nbytes, piece_bytes, C.byref(st))
         if rc != OK:
             raise HbamError(rc, _L.hbam_gpu_error(self._h).decode())
-        return {f: getattr(st, f) for f, _ in GpuStats._fields_}
+        return _stats_dict(st)
 
     def reload(self, ptr, nbytes, pinned=True):
         """Host->HBM copy of the loaded file's bytes from `ptr` (through a

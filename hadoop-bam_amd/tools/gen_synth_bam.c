@@ -6,7 +6,7 @@
  *   mode 0  "C2": paired-end 150 bp, coordinate-sorted over 25 hg19-like
  *           contigs at ~30x local coverage; 98 % mapped (1-3 CIGAR ops),
  *           1.5 % unmapped-placed (mate's refID/pos), 0.5 % unplaced at the end;
- *           read names SYN:1:<tile>:<x>:<y>; Illumina-like per-cycle qualities;
+ *           read names SYN-HS2000:<lane>:FC706VJ:<swath>:<tile>:<x>:<y>; Illumina-like per-cycle qualities;
  *           aux NM:i MD:Z AS:i XS:i RG:Z.
  *   mode 1  "C4": ONT-like long reads, 10-50 kb (log-normal, median 20 kb),
  *           Q 5-30, CIGARs of 100s-1000s of ops, MM:Z + ML:B:C, 10 % unmapped.
@@ -78,12 +78,17 @@ static int reg2bin(int beg, int end) {
   return 0;
 }
 
-/* position of mapped record i: genome walk at 30x local coverage */
+/* position of mapped record i: genome walk at 30x local coverage; a read
+ * (<= 50 kb of reference for long reads) never runs off its contig */
 static void locus(const model *m, uint64_t i, int *ref, int32_t *pos) {
-  uint64_t g = (i * m->span) / (m->n_mapped ? m->n_mapped : 1);
+  /* start of read i: an even walk plus jitter below one step, so starts
+   * stay sorted but their spacing (and the seq nibble phase) varies */
+  const uint64_t step = m->span / (m->n_mapped ? m->n_mapped : 1);
+  uint64_t g = (i * m->span) / (m->n_mapped ? m->n_mapped : 1) + (step > 1 ? hash2(0x10c05ULL, i) % step : 0);
   int c = 0;
   while (c < 24 && g >= (uint64_t)kContigLen[c]) { g -= (uint64_t)kContigLen[c]; ++c; }
-  if (g + 200 > (uint64_t)kContigLen[c]) g = (uint64_t)kContigLen[c] - 200;
+  const uint64_t room = m->p->mode == 1 ? 60000 : 200;
+  if (g + room > (uint64_t)kContigLen[c]) g = kContigLen[c] > (int32_t)room ? (uint64_t)kContigLen[c] - room : 0;
   *ref = c;
   *pos = (int32_t)g;
 }
@@ -172,8 +177,9 @@ static uint32_t make_record(const model *m, uint64_t i, uint8_t *o) {
   /* read name */
   char name[64];
   uint64_t ns = hash2(p->seed ^ 0xabcdefULL, pair);
-  int nl = snprintf(name, sizeof name, "SYN:1:%u:%u:%u", (unsigned)(1101 + ns % 20), (unsigned)((ns >> 8) % 30000),
-                    (unsigned)((ns >> 24) % 40000));
+  int nl = snprintf(name, sizeof name, "SYN-HS2000:%u:FC706VJ:%u:%u:%u:%u", (unsigned)(1 + ns % 8),
+                    (unsigned)(1 + (ns >> 3) % 8), (unsigned)(1101 + (ns >> 6) % 68), (unsigned)((ns >> 16) % 21000),
+                    (unsigned)((ns >> 32) % 200000));
   const int l_read_name = nl + 1;
   /* aux */
   char md[64];
@@ -196,7 +202,9 @@ static uint32_t make_record(const model *m, uint64_t i, uint8_t *o) {
   /* ---- write ---- */
   int end = pos;
   for (uint32_t k = 0; k < ncig; ++k) { int op = cig[k] & 0xf; if (op == 0 || op == 2) end += (int)(cig[k] >> 4); }
-  int bin = unplaced ? 4680 : reg2bin(pos < 0 ? 0 : pos, end > pos ? end : pos + 1);
+  /* htsjdk computeIndexingBin: reg2bin(alignmentStart-1, alignmentEnd), a
+   * one-base span when the read is unmapped (unplaced: reg2bin(-1, 0) = 4680) */
+  int bin = pos < 0 ? 4680 : reg2bin(pos, (!unmapped && end > pos) ? end : pos + 1);
   put32(o, (uint32_t)bs);
   put32(o + 4, (uint32_t)ref);
   put32(o + 8, (uint32_t)pos);
@@ -221,27 +229,44 @@ static uint32_t make_record(const model *m, uint64_t i, uint8_t *o) {
     uint8_t hi, lo;
     int c0 = ref < 0 ? (int)(splitmix(&ms) & 3) : ref_base(ref, (uint64_t)(pos + k));
     int c1 = ref < 0 ? (int)(splitmix(&ms) & 3) : ref_base(ref, (uint64_t)(pos + k + 1));
-    if ((splitmix(&ms) & 127) == 0) c0 = (c0 + 1) & 3;
+    {  /* ~1.5 % substitutions on either base of the pair (errors + SNVs) */
+      const uint64_t e = splitmix(&ms);
+      if ((e & 63) == 0) c0 = (c0 + 1 + (int)((e >> 8) % 3)) & 3;
+      if (((e >> 16) & 63) == 0) c1 = (c1 + 1 + (int)((e >> 24) % 3)) & 3;
+    }
     hi = code[c0];
     lo = (k + 1 < l_seq) ? code[c1] : 0;
     *w++ = (uint8_t)(hi << 4 | lo);
   }
-  /* qual: per-cycle Illumina-like random walk (Q2..Q41) / ONT Q5..30 */
-  int q = p->mode == 0 ? 36 : 18;
-  for (int k = 0; k < l_seq; ++k) {
-    uint64_t r = splitmix(&ms);
-    int d = (int)(r % 7) - 3;
-    q += d / 2;
-    if (p->mode == 0) {
-      int cap = k < 100 ? 41 : 41 - (k - 100) / 4;
-      if (q > cap) q = cap;
-      if ((r >> 20) % 50 == 0) q = 2 + (int)((r >> 30) % 10);
+  /* qual: Illumina-like per-cycle model for short reads -- mean 37 falling
+   * to ~30 over the read, per-base noise ~N(0, 4.3) (Q2..Q41), 2 % isolated
+   * low-quality calls and, in 8 % of reads, a Q2 tail (the Illumina read
+   * segment indicator) -- about 3.9 bits per quality after DEFLATE, which puts
+   * C2 at ~1.5 GB compressed as SURVEY 8d asks; ONT-like random walk Q5..30
+   * for long reads */
+  if (p->mode == 0) {
+    uint64_t tr = splitmix(&ms);
+    const int tail = (tr % 100) < 8 ? l_seq - 5 - (int)((tr >> 8) % 40) : l_seq;
+    for (int k = 0; k < l_seq; ++k) {
+      uint64_t r = splitmix(&ms);
+      const int sum = (int)(r & 255) + (int)((r >> 8) & 255) + (int)((r >> 16) & 255) + (int)((r >> 24) & 255);
+      int q = 36 - k / 20 + (sum - 510) / 30;
+      if (((r >> 32) & 63) == 0) q = 2 + (int)((r >> 40) % 12);
+      if (k >= tail) q = 2;
+      if (q > 41) q = 41;
       if (q < 2) q = 2;
-    } else {
+      *w++ = (uint8_t)q;
+    }
+  } else {
+    int q = 18;
+    for (int k = 0; k < l_seq; ++k) {
+      uint64_t r = splitmix(&ms);
+      int d = (int)(r % 7) - 3;
+      q += d / 2;
       if (q > 30) q = 30;
       if (q < 5) q = 5;
+      *w++ = (uint8_t)q;
     }
-    *w++ = (uint8_t)q;
   }
   if (p->mode == 0) {
     memcpy(w, "NMC", 3); w[3] = (uint8_t)nm; w += 4;

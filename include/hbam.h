@@ -2,9 +2,9 @@
  * hbam.h -- C ABI of the MI355X-native Hadoop-BAM read path (libhbam.so).
  *
  * This is the boundary a JNI shim behind org.seqdoop.hadoop_bam binds (see
- * INTEGRATION.md).  Plain C: pointers, sizes and status codes only.  Every
- * entry point names the reference interface it replaces (paths relative to
- * /root/reference/src/main/java/org/seqdoop/hadoop_bam/).
+ * INTEGRATION.md and java/).  Plain C: pointers, sizes and status codes only.
+ * Every entry point names the reference interface it replaces (paths relative
+ * to /root/reference/src/main/java/org/seqdoop/hadoop_bam/).
  *
  * Status codes map 1:1 onto the Java exception a caller must raise:
  *   HBAM_E_FORMAT -> htsjdk.samtools.SAMFormatException
@@ -13,6 +13,13 @@
  *   HBAM_E_IO     -> java.io.IOException (RuntimeIOException for bad DEFLATE data)
  *   HBAM_E_DEVICE -> java.io.IOException (HIP runtime failure; never a silent CPU path)
  * The message is available from hbam_last_error(ctx).
+ *
+ * I/O: a ctx reads the file the way BAMRecordReader reads its split through
+ * WrapSeekable (WrapSeekable.java:42-87): opening parses the header only, and
+ * a decode copies into HBM just the window of compressed bytes it works on
+ * (opts.window_bytes at a time, the next record's position carried from one
+ * window to the next).  Device memory is bounded by the window, whatever the
+ * file size.
  *
  * Threading: a ctx is single-threaded (RecordReader contract); the library is
  * re-entrant across ctxs.  Each ctx owns one HIP stream on its device.
@@ -38,16 +45,22 @@ extern "C" {
 #define HBAM_E_STATE 6
 #define HBAM_E_NOMEM 7
 
-#define HBAM_ABI_VERSION 1
+#define HBAM_ABI_VERSION 2
+
+/* htsjdk ValidationStringency, as util/SAMHeaderReader.java:45-46 reads it */
+#define HBAM_STRICT 0  /* htsjdk's default: SAMRecord.isValid errors -> SAMFormatException */
+#define HBAM_LENIENT 1 /* errors are logged; records still decoded for the check */
+#define HBAM_SILENT 2  /* no validation */
 
 typedef struct hbam_ctx hbam_ctx;
 
 /* Reader options: the hadoopbam.* Configuration properties a JNI shim reads. */
 typedef struct hbam_opts {
-  int32_t device;     /* hadoopbam.gpu.device: HIP device ordinal (default 0) */
-  int32_t check_crc;  /* BlockCompressedInputStream.setCheckCrcs (default 0) */
-  int32_t reserved0;
-  int32_t reserved1;
+  int32_t device;        /* hadoopbam.gpu.device: HIP device ordinal (default 0) */
+  int32_t check_crc;     /* BlockCompressedInputStream.setCheckCrcs (default 0) */
+  int32_t stringency;    /* hadoopbam.samheaderreader.validation-stringency (HBAM_STRICT when unset) */
+  int32_t reserved;
+  uint64_t window_bytes; /* hadoopbam.gpu.window-bytes: compressed bytes per HBM window (0 = 4 GiB) */
 } hbam_opts;
 
 /* BAM header summary ([htsjdk] BAMFileReader.readHeader). */
@@ -56,12 +69,10 @@ typedef struct hbam_header_info {
   int32_t l_text;               /* SAM header text length */
   uint64_t first_record_voff;   /* getFilePointerSpanningReads().getFirstOffset() */
   uint64_t file_size;           /* compressed bytes */
-  uint64_t n_blocks;            /* BGZF blocks */
-  uint64_t uncompressed_size;   /* inflated bytes of all blocks */
   const char *text;             /* l_text bytes, owned by ctx */
 } hbam_header_info;
 
-/* One decoded span in SoA form: exactly the argument list of
+/* A batch of decoded records in SoA form: exactly the argument list of
  * LazyBAMRecordFactory.createBAMRecord (LazyBAMRecordFactory.java:37-50)
  * plus the BAMRecordReader key (BAMRecordReader.java:81-121) and the BGZF
  * virtual offset of each record.  pos / next_pos are the 0-based BAM fields
@@ -80,16 +91,16 @@ typedef struct hbam_batch {
   uint64_t data_len;
   int32_t status;      /* status of the record that ended the span early (0 = clean end) */
   int32_t reserved;
+  uint64_t next_voff;  /* where the split continues: pass it as vstart of the next call; >= vend when done */
 } hbam_batch;
 
-/* Open a BAM file / in-memory BAM: loads the compressed bytes into HBM,
- * discovers every BGZF block on the GPU, inflates and parses the header.
+/* Open a BAM file (read-only map; nothing but the header is read) / an
+ * in-memory BAM / a plain BGZF file (VCF/BCF payloads: no BAM header).
  * Replaces BAMRecordReader.initialize's SamReader construction
  * (BAMRecordReader.java:142-149,186-200) and SAMHeaderReader.readSAMHeaderFrom
  * (util/SAMHeaderReader.java:57-75). */
 int hbam_open(const char *path, const hbam_opts *opts, hbam_ctx **out);
 int hbam_open_mem(const void *data, uint64_t len, const hbam_opts *opts, hbam_ctx **out);
-/* Same, for a plain BGZF file (VCF/BCF payloads): no BAM header parse. */
 int hbam_open_bgzf(const void *data, uint64_t len, const hbam_opts *opts, hbam_ctx **out);
 void hbam_close(hbam_ctx *ctx);
 const char *hbam_last_error(hbam_ctx *ctx);
@@ -99,22 +110,45 @@ int32_t hbam_abi_version(void);
 int hbam_header(hbam_ctx *ctx, hbam_header_info *out);
 /* reference i of the binary dictionary: name (NUL-terminated, ctx-owned) and length */
 int hbam_ref(hbam_ctx *ctx, int32_t i, const char **name, int32_t *length);
+/* BGZF block count and inflated size of the whole file (reads every block header) */
+int hbam_file_stats(hbam_ctx *ctx, uint64_t *n_blocks, uint64_t *uncompressed_size);
+/* host -> HBM bytes this ctx has copied so far (its window loads + prefetch) */
+int hbam_bytes_read(hbam_ctx *ctx, uint64_t *bytes);
+/* Copy file bytes [lo, hi) into HBM now; later windows inside the range decode
+ * from HBM without host reads. */
+int hbam_prefetch(hbam_ctx *ctx, uint64_t lo, uint64_t hi);
 
-/* Decode every record of FileVirtualSplit [vstart, vend) (vStart inclusive,
- * vEnd exclusive: FileVirtualSplit.java:82-86) exactly as
- * BAMRecordReader.initialize + nextKeyValue loop would
- * (BAMRecordReader.java:151-154,181-182,223-232).  Records before a failing
- * record are returned with out->status set and the call returns that status. */
-int hbam_decode_span(hbam_ctx *ctx, uint64_t vstart, uint64_t vend, hbam_batch *out);
+/* Decode records of FileVirtualSplit [vstart, vend) (vStart inclusive, vEnd
+ * exclusive: FileVirtualSplit.java:82-86) exactly as BAMRecordReader.initialize
+ * + the nextKeyValue loop would (BAMRecordReader.java:151-154,181-182,223-232),
+ * with the ctx's validation stringency.  At most max_records records are
+ * returned (0 = every record of the split); out->next_voff is where the next
+ * call continues, so a split streams in bounded batches:
+ *   for (v = vStart; hbam_decode_span(ctx, v, vEnd, max, &b) == HBAM_OK && b.n; v = b.next_voff) ...
+ * A call whose vstart is the previous batch's next_voff continues without
+ * re-decoding.  Records before a failing record are returned with out->status
+ * set and the call returns that status. */
+int hbam_decode_span(hbam_ctx *ctx, uint64_t vstart, uint64_t vend, uint64_t max_records, hbam_batch *out);
+/* BAMRecordReader.getProgress's in.position() (BAMRecordReader.java:209-219):
+ * the compressed stream position after nextKeyValue returned record i of the
+ * last batch (htsjdk's iterator has read one record ahead). */
+int hbam_reader_position(hbam_ctx *ctx, uint64_t i, uint64_t *pos);
 
 /* SplittingBAMIndexer.index(in, out, inputSize, granularity)
  * (SplittingBAMIndexer.java:248-290): the .splitting-bai bytes, big-endian u64
- * entries, byte-identical to the reference.  *buf released with hbam_free. */
+ * entries, byte-identical to the reference; the file is streamed through HBM
+ * window by window.  *buf released with hbam_free. */
 int hbam_build_splitting_index(hbam_ctx *ctx, int32_t granularity, uint8_t **buf, uint64_t *len);
+/* Write-time index: new SplittingBAMIndexer(out, granularity), processAlignment
+ * for records with virtual offsets voffs[0..n) in file order, then
+ * finish(file_size) (SplittingBAMIndexer.java:175-243, driven by
+ * BAMRecordWriter.java:145-149).  Entries selected on the GPU. */
+int hbam_splitting_index_for_records(const hbam_opts *opts, const uint64_t *voffs, uint64_t n, int32_t granularity,
+                                     uint64_t file_size, uint8_t **buf, uint64_t *len);
 
 /* BAMSplitGuesser.guessNextBAMRecordStart(beg, end) (BAMSplitGuesser.java:108-235)
- * for n split points at once (one GPU launch); out[i] == ends[i] when no
- * record start is found, as in the reference. */
+ * for n split points at once (one GPU launch per window of nearby points);
+ * out[i] == ends[i] when no record start is found, as in the reference. */
 int hbam_guess_record_starts(hbam_ctx *ctx, const uint64_t *begs, const uint64_t *ends, uint64_t n,
                              uint64_t *out);
 
@@ -136,12 +170,13 @@ int hbam_get_splits(hbam_ctx *ctx, const uint64_t *starts, const uint64_t *lengt
 
 /* ---- SAMRecordWritable codec (map-output serialization for the shuffle) ---- */
 /* SAMRecordWritable.write (SAMRecordWritable.java:55-64) of every record of
- * the last hbam_decode_span on ctx, computed on the GPU: [htsjdk]
+ * the last hbam_decode_span batch on ctx, computed on the GPU: [htsjdk]
  * BAMRecordCodec.encode of each BAMRecord, back to back (block_size, the fixed
  * fields, the undecoded rest; indexBin written as 0 when refID < 0).  *len
  * receives the total size; out == NULL only sizes.  offs (NULL or n+1
  * entries) receives each record's start, offs[n] = *len.  cap < *len ->
- * HBAM_E_ARG. */
+ * HBAM_E_ARG.  A batch from several windows (max_records = 0 over a split
+ * longer than a window) -> HBAM_E_STATE: encode bounded batches. */
 int hbam_encode_writables(hbam_ctx *ctx, uint8_t *out, uint64_t cap, uint64_t *offs, uint64_t *len);
 /* SAMRecordWritable.readFields (SAMRecordWritable.java:65-68) for n serialized
  * values at once: value i = buf[offs[i], offs[i+1]) (the last ends at len), as
@@ -165,15 +200,15 @@ int hbam_open_codec(const hbam_opts *opts, hbam_ctx **out);
  * byte-identical to zlib 1.2.11 (levels 0..9; htsjdk's default is 5); a block
  * that does not fit the 65518-byte compressed buffer is written by the
  * NO_COMPRESSION fallback (one stored block).  Blocks: block_lens[0..n_blocks)
- * (each <= 65536, as BlockCompressedOutputStream.flush cuts them), or when
- * block_lens is NULL, len cut every block_size bytes.  *out (BGZF file bytes)
- * is released with hbam_free. */
+ * (each <= 65536, as BlockCompressedOutputStream.flush cuts them; their sum
+ * must be len), or when block_lens is NULL, len cut every block_size bytes.
+ * *out (BGZF file bytes) is released with hbam_free. */
 int hbam_bgzf_compress(const hbam_opts *opts, const void *data, uint64_t len, const uint32_t *block_lens,
                        uint64_t n_blocks, int32_t block_size, int32_t level, int32_t flags, uint8_t **out,
                        uint64_t *out_len);
 
-/* BGZF block table (coff, csize, isize, ustart) and inflated bytes: used by
- * tests and by the BGZF text formats. */
+/* BGZF block table (coff, csize, isize, ustart) and inflated bytes of the
+ * whole file: used by tests and by the BGZF text formats. */
 int hbam_blocks(hbam_ctx *ctx, uint64_t *coff, uint32_t *csize, uint32_t *isize, uint64_t *ustart,
                 uint64_t cap, uint64_t *n);
 int hbam_read_inflated(hbam_ctx *ctx, uint64_t pos, uint64_t len, uint8_t *dst);
@@ -186,13 +221,11 @@ int64_t hbam_get_key0(int32_t ref_idx, int32_t alignment_start0);
 int64_t hbam_get_key(int32_t ref_idx, int32_t alignment_start);
 int64_t hbam_murmurhash3(const void *key, uint64_t len, int32_t seed);
 
-/* ---- device-resident pipeline (benchmark / multi-GPU shard driver) ---- */
-typedef struct hbam_gpu hbam_gpu;
-
+/* ---- device-resident decode (benchmark / multi-GPU shard driver) ---- */
 typedef struct hbam_gpu_stats {
-  uint64_t n_blocks;          /* BGZF blocks discovered */
-  uint64_t compressed_bytes;  /* C */
-  uint64_t inflated_bytes;    /* U */
+  uint64_t n_blocks;          /* BGZF blocks decoded (summed over windows) */
+  uint64_t compressed_bytes;  /* C of the decoded windows */
+  uint64_t inflated_bytes;    /* U of the decoded windows */
   uint64_t records;           /* N */
   uint64_t first_voff, last_voff;
   uint64_t key_xor, voff_sum; /* order-independent digests of the keys / voffs */
@@ -201,24 +234,37 @@ typedef struct hbam_gpu_stats {
   int32_t link_fallbacks;     /* record-chain spans that took the exact serial link */
   int32_t inflate_launches;   /* phase A + B launch pairs of this run */
   int32_t link_rewalks;       /* parallel-link re-walk rounds of this run */
+  int32_t windows;            /* HBM windows the span was decoded in */
+  int32_t reserved;
 } hbam_gpu_stats;
+
+/* hbam_decode_span with the records left in HBM (no host copies): counts,
+ * digests (flags bit2) and per-stage timings (flags bit0) only; flags bit1
+ * skips the field decode (chain + voffs only). */
+int hbam_decode_span_device(hbam_ctx *ctx, uint64_t vstart, uint64_t vend, int32_t flags, hbam_gpu_stats *st);
+
+typedef struct hbam_gpu hbam_gpu;
 
 int hbam_gpu_create(int32_t device, hbam_gpu **out);
 void hbam_gpu_destroy(hbam_gpu *g);
 const char *hbam_gpu_error(hbam_gpu *g);
-/* Load a whole BAM (base_offset = 0) or a BGZF-aligned shard of one. For a
- * shard, first_pos is the inflated-stream offset (within the shard) of its
- * first record start; for a whole file pass UINT64_MAX (use the header). */
-int hbam_gpu_load(hbam_gpu *g, const void *data, uint64_t len, uint64_t base_offset, int32_t n_ref,
-                  uint64_t first_pos);
-/* One pass of the hot path over the resident bytes: BGZF discovery, inflate,
- * record scan, field decode + keys + voffs (flags bit0: also timing per stage,
- * bit1: skip decode). */
+/* Make a whole BAM file resident in HBM (copied from host memory) and parse
+ * its header. */
+int hbam_gpu_load(hbam_gpu *g, const void *data, uint64_t len);
+/* HBM window of the decode (default 4 GiB of compressed bytes): a file larger
+ * than the window is decoded window by window. */
+int hbam_gpu_set_window(hbam_gpu *g, uint64_t window_bytes);
+/* One pass of the hot path over the resident file, first record to EOF:
+ * BGZF discovery, inflate, record scan, field decode + keys + voffs, window by
+ * window (flags as hbam_decode_span_device). */
 int hbam_gpu_run(hbam_gpu *g, int32_t flags, hbam_gpu_stats *stats);
-/* End-to-end pass from host memory: the file (same bytes/length as the
- * loaded one) is copied host->HBM in pieces of piece_bytes on a copy stream
- * while the BGZF blocks of every landed piece are located and inflated on
- * the compute streams; then the record chain + decode (as hbam_gpu_run).
+/* .splitting-bai of the resident file (SplittingBAMIndexer.index), *ms = HIP-event
+ * time of the whole call. */
+int hbam_gpu_index(hbam_gpu *g, int32_t granularity, uint8_t **buf, uint64_t *len, float *ms);
+/* End-to-end pass from host memory: the file (same bytes/length as the loaded
+ * one, one window) is copied host->HBM in pieces of piece_bytes on a copy
+ * stream while the BGZF blocks of every landed piece are located and inflated
+ * on the compute streams; then the record chain + decode (as hbam_gpu_run).
  * st->ms_total = first copy to last decode.  data should come from
  * hbam_host_alloc (page-locked) for the copies to overlap the kernels. */
 int hbam_gpu_run_streamed(hbam_gpu *g, const void *data, uint64_t len, uint64_t piece_bytes, hbam_gpu_stats *st);
@@ -232,20 +278,21 @@ void hbam_host_free(void *p);
 int hbam_gpu_reload(hbam_gpu *g, const void *data, uint64_t len, int32_t pinned, float *ms);
 /* Measured hipMemcpy device-to-device bandwidth, (read + write) GB/s. */
 int hbam_gpu_d2d_bandwidth(hbam_gpu *g, uint64_t bytes, int32_t iters, float *gbps);
-/* SAMRecordWritable.write of every record of the last run into a device
- * buffer owned by g, iters timed times (HIP events on the pipeline stream);
- * hbam_gpu_fetch_encoded copies [pos, pos+len) of the result to the host. */
+/* SAMRecordWritable.write of every record of the last run's last window into
+ * a device buffer owned by g, iters timed times (HIP events on the pipeline
+ * stream); hbam_gpu_fetch_encoded copies [pos, pos+len) of it to the host. */
 int hbam_gpu_encode_writables(hbam_gpu *g, int32_t iters, float *ms_per_iter, uint64_t *bytes);
 int hbam_gpu_fetch_encoded(hbam_gpu *g, uint64_t pos, uint64_t len, uint8_t *dst);
-/* BGZF-compress the inflated stream of the last run on the GPU with the
- * loaded file's block boundaries (hbam_bgzf_compress semantics; iters timed
- * repetitions, HIP events); the result stays in HBM, hbam_gpu_fetch_compressed
- * copies [pos, pos+len) of it to the host.  Recompressing a file written by
- * zlib at the same level reproduces it byte for byte. */
+/* BGZF-compress the inflated stream of the last run (one window) on the GPU
+ * with the loaded file's block boundaries (hbam_bgzf_compress semantics;
+ * iters timed repetitions, HIP events); the result stays in HBM,
+ * hbam_gpu_fetch_compressed copies [pos, pos+len) of it to the host.
+ * Recompressing a file written by zlib at the same level reproduces it byte
+ * for byte. */
 int hbam_gpu_bgzf_compress(hbam_gpu *g, int32_t level, int32_t flags, int32_t iters, float *ms_per_iter,
                            uint64_t *out_len);
 int hbam_gpu_fetch_compressed(hbam_gpu *g, uint64_t pos, uint64_t len, uint8_t *dst);
-/* Copy results of the last run to the host (any pointer may be NULL). */
+/* Copy keys / voffs of the last run's last window to the host (either may be NULL). */
 int hbam_gpu_fetch(hbam_gpu *g, int64_t *keys, uint64_t *voffs, uint64_t cap);
 int32_t hbam_device_count(void);
 

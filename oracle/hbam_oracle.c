@@ -27,6 +27,8 @@ struct orc_stream {
   int32_t l_text;
   uint64_t header_end; /* inflated-stream position after the binary refs */
   int has_header;
+  int32_t *ref_len;    /* binary dictionary lengths (STRICT alignment-start checks) */
+  int stringency;      /* ORC_STRICT (htsjdk default) / ORC_LENIENT / ORC_SILENT */
   char err[256];
 };
 
@@ -251,12 +253,17 @@ static int parse_header(orc_stream *s) {
   if (end - p < 4) return set_err(s, ORC_E_TRUNC, "no reference sequence count");
   int32_t n_ref = rdi32(d + p);
   p += 4;
+  free(s->ref_len);
+  s->ref_len = (int32_t *)calloc(n_ref > 0 ? (size_t)n_ref : 1, sizeof(int32_t));
+  if (!s->ref_len) return set_err(s, ORC_E_NOMEM, "oom");
   for (int32_t i = 0; i < n_ref; i++) {
     if (end - p < 4) return set_err(s, ORC_E_TRUNC, "EOF before reference %d", i + 1);
     int32_t l_name = rdi32(d + p);
     p += 4;
     if (l_name < 0 || end - p < (uint64_t)l_name + 4) return set_err(s, ORC_E_TRUNC, "reference %d truncated", i + 1);
-    p += (uint64_t)l_name + 4;
+    p += (uint64_t)l_name;
+    s->ref_len[i] = rdi32(d + p);
+    p += 4;
   }
   s->l_text = l_text;
   s->n_ref = n_ref < 0 ? 0 : n_ref;
@@ -297,6 +304,7 @@ int orc_open(const uint8_t *f, uint64_t n, int check_crc, int want_header, orc_s
 
 void orc_close(orc_stream *s) {
   if (!s) return;
+  free(s->ref_len);
   free(s->blk);
   free(s->data);
   free(s);
@@ -403,6 +411,172 @@ static int rec_grow(rec_buf *b) {
   return ORC_OK;
 }
 
+/* ------------------------------------------------------------------------ */
+/* [htsjdk] SAMRecord.isValid(firstOnly) as BAMFileReader's iterator runs it */
+/* on every record unless the stringency is SILENT; STRICT throws the first   */
+/* error as a SAMFormatException, LENIENT only logs (but the lazy fields are  */
+/* still decoded for the check, so a record whose read name / cigar / seq /   */
+/* qual do not fit, or a cigar op code > 8, still fails).  Stringency comes   */
+/* from hadoopbam.samheaderreader.validation-stringency                       */
+/* (util/SAMHeaderReader.java:45-46, BAMRecordReader.java:142,192-194).       */
+/* Restated rule list, parity unpinned by the reference:      */
+/* no test of it asserts a validation error; test.bam (read under STRICT by   */
+/* TestSplittingBAMIndexer) passes every rule.                                */
+/* rec = the record's block_size field; returns 1 if invalid.                 */
+/* ------------------------------------------------------------------------ */
+static int32_t region_to_bin(int32_t beg, int32_t end) { /* GenomicIndexUtil.regionToBin */
+  --end;
+  if (beg >> 14 == end >> 14) return ((1 << 15) - 1) / 7 + (beg >> 14);
+  if (beg >> 17 == end >> 17) return ((1 << 12) - 1) / 7 + (beg >> 17);
+  if (beg >> 20 == end >> 20) return ((1 << 9) - 1) / 7 + (beg >> 20);
+  if (beg >> 23 == end >> 23) return ((1 << 6) - 1) / 7 + (beg >> 23);
+  if (beg >> 26 == end >> 26) return ((1 << 3) - 1) / 7 + (beg >> 26);
+  return 0;
+}
+
+/* aux lookup of a two-letter tag in t[0, len); *zlen = Z/H string length */
+static int aux_has(const uint8_t *t, int64_t len, const char *tag, int64_t *zlen) {
+  int64_t i = 0;
+  while (i + 3 <= len) {
+    const int hit = t[i] == (uint8_t)tag[0] && t[i + 1] == (uint8_t)tag[1];
+    const uint8_t ty = t[i + 2];
+    i += 3;
+    int64_t sz;
+    if (ty == 'A' || ty == 'c' || ty == 'C') sz = 1;
+    else if (ty == 's' || ty == 'S') sz = 2;
+    else if (ty == 'i' || ty == 'I' || ty == 'f') sz = 4;
+    else if (ty == 'Z' || ty == 'H') {
+      int64_t j = i;
+      while (j < len && t[j]) j++;
+      if (hit) *zlen = j - i;
+      sz = j - i + 1;
+    } else if (ty == 'B') {
+      if (i + 5 > len) return 0;
+      const uint8_t sub = t[i];
+      const int64_t cnt = rdi32(t + i + 1);
+      const int64_t es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
+      if (cnt < 0) return 0;
+      sz = 5 + cnt * es;
+    } else {
+      return 0;
+    }
+    if (hit) return 1;
+    if (sz > len - i) return 0; /* a malformed aux block ends the lookup */
+    i += sz;
+  }
+  return 0;
+}
+
+enum { OP_M = 0, OP_I = 1, OP_D = 2, OP_N = 3, OP_S = 4, OP_H = 5, OP_P = 6, OP_EQ = 7, OP_X = 8 };
+static int op_real(uint32_t op) { return op == OP_M || op == OP_I || op == OP_D || op == OP_N || op == OP_EQ || op == OP_X; }
+
+int orc_record_invalid(const uint8_t *rec, int32_t bs, int32_t n_ref, const int32_t *ref_len, int strict) {
+  const int32_t ref = rdi32(rec + 4), pos = rdi32(rec + 8);
+  const uint32_t lrn = rec[12], mapq = rec[13], bin = rd16(rec + 14), ncig = rd16(rec + 16), flag = rd16(rec + 18);
+  const int32_t lseq = rdi32(rec + 20), nref = rdi32(rec + 24), npos = rdi32(rec + 28);
+  /* the lazily decoded fields must lie inside the record (BAMRecord offsets) */
+  if (lrn < 1 || lseq < 0) return 1;
+  if (32 + (int64_t)lrn + 4 * (int64_t)ncig + ((int64_t)lseq + 1) / 2 + (int64_t)lseq > (int64_t)bs) return 1;
+  const uint8_t *cig = rec + 36 + lrn;
+  for (uint32_t k = 0; k < ncig; k++)
+    if ((rd32(cig + 4 * k) & 0xf) > 8) return 1; /* CigarOperator.binaryToEnum */
+  if (!strict) return 0;
+  const int paired = (flag & 0x1) != 0, unmapped = (flag & 0x4) != 0;
+  if (!paired) { /* INVALID_FLAG_* of an unpaired read, INVALID_MATE_REF_INDEX */
+    if (flag & 0x2 || flag & 0x8 || flag & 0x20 || flag & 0x40 || flag & 0x80) return 1;
+    if (nref != -1) return 1;
+  } else {
+    /* isValidReferenceIndexAndPosition(mate): "*" <=> mate start 0 */
+    if (nref == -1 && npos + 1 != 0) return 1;
+    if (nref != -1 && npos + 1 == 0) return 1;
+    if (nref != -1 && ref_len && (int64_t)npos + 1 > ref_len[nref]) return 1;
+    if (nref == -1 && !(flag & 0x8)) return 1;       /* mapped mate needs a mate reference */
+    if (!(flag & 0x40) && !(flag & 0x80)) return 1;  /* PAIRED_READ_NOT_MARKED_AS_FIRST_OR_SECOND */
+  }
+  if (unmapped) {
+    if (flag & 0x100) return 1; /* INVALID_FLAG_NOT_PRIM_ALIGNMENT */
+    if (flag & 0x800) return 1; /* INVALID_FLAG_SUPPLEMENTARY_ALIGNMENT */
+    if (mapq != 0) return 1;    /* INVALID_MAPPING_QUALITY */
+    /* htsjdk no longer rejects a cigar on an unmapped read ("now allowed,
+       because there are current tools that do this"): test.bam has them */
+  } else {
+    if (ncig == 0) return 1;    /* INVALID_CIGAR: mapped read without cigar */
+    if (n_ref == 0) return 1;   /* MISSING_SEQUENCE_DICTIONARY */
+  }
+  /* isValidReferenceIndexAndPosition(read) */
+  if (ref == -1 && pos + 1 != 0) return 1;
+  if (ref != -1 && pos + 1 == 0) return 1;
+  if (ref != -1 && ref_len && (int64_t)pos + 1 > ref_len[ref]) return 1;
+  /* Cigar.isValid + SAMUtils.validateCigar (mapped reads) */
+  int64_t qlen = 0, rlen = 0;
+  for (uint32_t k = 0; k < ncig; k++) {
+    const uint32_t c = rd32(cig + 4 * k), op = c & 0xf, len = c >> 4;
+    if (op == OP_M || op == OP_I || op == OP_S || op == OP_EQ || op == OP_X) qlen += len;
+    if (op == OP_M || op == OP_D || op == OP_N || op == OP_EQ || op == OP_X) rlen += len;
+  }
+  if (!unmapped) {
+    int seen_real = 0;
+    int64_t ref_at = (int64_t)pos + 1;
+    for (uint32_t k = 0; k < ncig; k++) {
+      const uint32_t c = rd32(cig + 4 * k), op = c & 0xf, len = c >> 4;
+      if (len == 0) return 1; /* zero-length element */
+      if (op == OP_H) {
+        if (k != 0 && k != ncig - 1) return 1;
+      } else if (op == OP_S) {
+        if (k == 0 || k == ncig - 1) {
+          /* soft clip at either end */
+        } else if (k == 1) {
+          const int three_with_h = ncig == 3 && (rd32(cig + 8) & 0xf) == OP_H;
+          if (!three_with_h && (rd32(cig) & 0xf) != OP_H) return 1;
+        } else if (k == ncig - 2) {
+          if ((rd32(cig + 4 * (ncig - 1)) & 0xf) != OP_H) return 1;
+        } else {
+          return 1;
+        }
+      } else if (op == OP_P) {
+        if (k != 0) {
+          if (k == ncig - 1) return 1;
+          if (!op_real(rd32(cig + 4 * (k - 1)) & 0xf) || !op_real(rd32(cig + 4 * (k + 1)) & 0xf)) return 1;
+        }
+      } else { /* real operator */
+        seen_real = 1;
+        if (op == OP_I || op == OP_D) { /* an M/N/=/X or P must separate two I or two D */
+          for (uint32_t j = k + 1; j < ncig; j++) {
+            const uint32_t nx = rd32(cig + 4 * j) & 0xf;
+            if ((op_real(nx) && nx != OP_I && nx != OP_D) || nx == OP_P) break;
+            if (nx == op) return 1;
+          }
+        }
+      }
+      if (op == OP_M || op == OP_EQ || op == OP_X) { /* alignment block inside the reference */
+        if (ref >= 0 && ref_len && ref_at + len - 1 > ref_len[ref]) return 1;
+      }
+      if (op == OP_M || op == OP_D || op == OP_N || op == OP_EQ || op == OP_X) ref_at += len;
+    }
+    if (!seen_real) return 1;
+  }
+  { /* INVALID_INDEXING_BIN: computeIndexingBin() */
+    const int32_t start0 = pos;
+    int32_t end = unmapped ? 0 : (int32_t)((int64_t)pos + 1 + rlen - 1);
+    if (end <= 0) end = start0 + 1;
+    if ((uint32_t)region_to_bin(start0, end) != bin) return 1;
+  }
+  if (lseq != 0 && ncig != 0 && qlen != lseq) return 1; /* MISMATCH_CIGAR_SEQ_LENGTH */
+  if (lseq == 0 && !(flag & 0x100)) { /* EMPTY_READ unless FZ, or non-empty CQ and CS */
+    const uint8_t *aux = cig + 4 * ncig;
+    const int64_t alen = (int64_t)bs - 32 - lrn - 4 * (int64_t)ncig;
+    int64_t z = -1;
+    if (!aux_has(aux, alen, "FZ", &z)) {
+      int64_t cq = -1, cs = -1;
+      const int hq = aux_has(aux, alen, "CQ", &cq), hs = aux_has(aux, alen, "CS", &cs);
+      if (!hq || !hs || cq <= 0 || cs <= 0) return 1;
+    }
+  }
+  return 0;
+}
+
+void orc_set_stringency(orc_stream *s, int stringency) { s->stringency = stringency; }
+
 int orc_decode_span(orc_stream *s, uint64_t vstart, uint64_t vend, orc_records *out) {
   memset(out, 0, sizeof *out);
   rec_buf b;
@@ -428,6 +602,11 @@ int orc_decode_span(orc_stream *s, uint64_t vstart, uint64_t vend, orc_records *
     int32_t ref_id = rdi32(r + 4), next_ref = rdi32(r + 24);
     if (ref_id < -1 || ref_id >= s->n_ref) { rc = set_err(s, ORC_E_ARG, "Reference index %d not found in sequence dictionary.", ref_id); break; }
     if (next_ref < -1 || next_ref >= s->n_ref) { rc = set_err(s, ORC_E_ARG, "Reference index %d not found in sequence dictionary.", next_ref); break; }
+    if (s->stringency != ORC_SILENT &&
+        orc_record_invalid(r, bs, s->n_ref, s->ref_len, s->stringency == ORC_STRICT)) {
+      rc = set_err(s, ORC_E_FORMAT, "SAMRecord.isValid failed at %llu", (unsigned long long)v);
+      break;
+    }
     if (b.r.n == b.cap && (rc = rec_grow(&b)) != ORC_OK) break;
     uint64_t i = b.r.n++;
     b.r.ref_id[i] = ref_id;

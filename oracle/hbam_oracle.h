@@ -35,6 +35,11 @@ extern "C" {
 #define ORC_E_IO 4     /* IOException / RuntimeIOException */
 #define ORC_E_NOMEM 7
 
+/* [htsjdk] ValidationStringency (hadoopbam.samheaderreader.validation-stringency) */
+#define ORC_STRICT 0
+#define ORC_LENIENT 1
+#define ORC_SILENT 2
+
 typedef struct {
   uint64_t coff;   /* compressed offset of the block in the file */
   uint32_t csize;  /* BSIZE + 1 */
@@ -79,6 +84,12 @@ typedef struct {
 /* BAMRecordReader.initialize/nextKeyValue over FileVirtualSplit [vstart,vend)
  * (BAMRecordReader.java:123-232 + [htsjdk] BAMFileReader span iterator). */
 int orc_decode_span(orc_stream *s, uint64_t vstart, uint64_t vend, orc_records *out);
+/* validation stringency of orc_decode_span (default ORC_STRICT, htsjdk's) */
+void orc_set_stringency(orc_stream *s, int stringency);
+/* [htsjdk] SAMRecord.isValid restated (strict) or the lazy-decode structure
+ * checks only (!strict) for the record whose block_size field is at rec;
+ * 1 = invalid.  ref_len may be NULL. */
+int orc_record_invalid(const uint8_t *rec, int32_t bs, int32_t n_ref, const int32_t *ref_len, int strict);
 void orc_records_free(orc_records *r);
 
 /* SAMRecordWritable.write (SAMRecordWritable.java:55-64) of every record in r

@@ -58,6 +58,9 @@ def lib():
         L.orc_writable_encode.argtypes = [P, P, P, P]
         L.orc_writable_encode.restype = u64
         L.orc_writable_decode.argtypes = [P, u64, P, u64, P]
+        L.orc_set_stringency.argtypes = [P, C.c_int]
+        L.orc_record_invalid.argtypes = [P, i32, i32, P, C.c_int]
+        L.orc_record_invalid.restype = C.c_int
         _LIB = L
     return _LIB
 
@@ -83,10 +86,14 @@ class OracleError(RuntimeError):
         self.code = code
 
 
-class Stream:
-    """A whole BGZF file inflated by zlib + BAM header parse (the oracle)."""
+STRICT, LENIENT, SILENT = 0, 1, 2  # [htsjdk] ValidationStringency
 
-    def __init__(self, data: bytes, check_crc=False, parse_header=True):
+
+class Stream:
+    """A whole BGZF file inflated by zlib + BAM header parse (the oracle).
+    stringency: validation of decode_span (htsjdk's default STRICT)."""
+
+    def __init__(self, data: bytes, check_crc=False, parse_header=True, stringency=STRICT):
         L = lib()
         self._buf = C.create_string_buffer(bytes(data), len(data))
         self.file = bytes(data)
@@ -97,6 +104,10 @@ class Stream:
             L.orc_close(self._h)
             self._h = None
             raise OracleError(rc, msg)
+        L.orc_set_stringency(self._h, stringency)
+
+    def set_stringency(self, stringency):
+        lib().orc_set_stringency(self._h, stringency)
 
     def close(self):
         if self._h:
@@ -259,3 +270,16 @@ def bgzf_compress(data: bytes, block_lens, level=5, eof=True) -> bytes:
     if n == (1 << 64) - 1:
         raise OracleError(4, "zlib deflate failed")
     return out[:n].tobytes()
+
+
+def record_invalid(rec: bytes, n_ref, ref_len=None, strict=True):
+    """[htsjdk] SAMRecord.isValid restated (orc_record_invalid); rec starts at
+    block_size."""
+    import struct
+    bs = struct.unpack_from("<i", rec, 0)[0]
+    buf = C.create_string_buffer(bytes(rec), max(len(rec), 1))
+    rl = None
+    if ref_len is not None:
+        arr = np.ascontiguousarray(ref_len, np.int32)
+        rl = arr.ctypes.data
+    return bool(lib().orc_record_invalid(buf, bs, n_ref, rl, 1 if strict else 0))

@@ -202,3 +202,125 @@ def writable_encode(data: bytes) -> bytes:
         out.append(rest)
         p += 4 + bs
     return b"".join(out)
+
+
+# ---------------------------------------------------------------------------
+# [htsjdk] SAMRecord.isValid under ValidationStringency.STRICT, restated a
+# second time (independently of orc_record_invalid) over a decoded record:
+# the two restatements are cross-checked by tests/test_strict.py.  Rule list:
+# DESIGN.md 2.1.  rec = bytes starting at block_size.
+# ---------------------------------------------------------------------------
+def _reg2bin(beg, end):
+    end -= 1
+    for shift, off in ((14, 4681), (17, 585), (20, 73), (23, 9), (26, 1)):
+        if beg >> shift == end >> shift:
+            return off + (beg >> shift)
+    return 0
+
+
+def _aux_tags(aux: bytes):
+    """{tag: Z-string length or None}; None if the aux block does not parse."""
+    tags, i = {}, 0
+    sizes = {"A": 1, "c": 1, "C": 1, "s": 2, "S": 2, "i": 4, "I": 4, "f": 4}
+    while i + 3 <= len(aux):
+        tag, ty = aux[i:i + 2].decode("latin-1"), chr(aux[i + 2])
+        i += 3
+        if ty in sizes:
+            n, zl = sizes[ty], None
+        elif ty in "ZH":
+            j = aux.find(b"\0", i)
+            j = len(aux) if j < 0 else j
+            zl, n = j - i, j - i + 1
+        elif ty == "B":
+            if i + 5 > len(aux):
+                return tags
+            sub, cnt = chr(aux[i]), struct.unpack_from("<i", aux, i + 1)[0]
+            if cnt < 0:
+                return tags
+            n, zl = 5 + cnt * (1 if sub in "cC" else 2 if sub in "sS" else 4), None
+        else:
+            return tags
+        tags.setdefault(tag, zl)
+        if n > len(aux) - i:
+            return tags
+        i += n
+    return tags
+
+
+def record_invalid(rec: bytes, n_ref: int, ref_len=None, strict=True) -> bool:
+    (bs, ref, pos, lrn, mapq, bin_, ncig, flag, lseq, nref, npos, tlen) = struct.unpack_from("<iiiBBHHHiiii", rec, 0)
+    if lrn < 1 or lseq < 0 or 32 + lrn + 4 * ncig + (lseq + 1) // 2 + lseq > bs:
+        return True
+    cig = [struct.unpack_from("<I", rec, 36 + lrn + 4 * k)[0] for k in range(ncig)]
+    ops = [(c & 15, c >> 4) for c in cig]
+    if any(op > 8 for op, _ in ops):
+        return True
+    if not strict:
+        return False
+    M, I, D, N, S, H, P, EQ, X = range(9)
+    paired, unmapped = bool(flag & 1), bool(flag & 4)
+    if not paired:
+        if flag & (2 | 8 | 0x20 | 0x40 | 0x80) or nref != -1:
+            return True
+    else:
+        if (nref == -1) != (npos == -1):
+            return True
+        if nref != -1 and ref_len is not None and npos + 1 > ref_len[nref]:
+            return True
+        if nref == -1 and not flag & 8:
+            return True
+        if not flag & 0xC0:
+            return True
+    if unmapped:
+        if flag & 0x900 or mapq:
+            return True
+    elif not ncig or n_ref == 0:
+        return True
+    if (ref == -1) != (pos == -1):
+        return True
+    if ref != -1 and ref_len is not None and pos + 1 > ref_len[ref]:
+        return True
+    real = {M, I, D, N, EQ, X}
+    if not unmapped:
+        if any(ln == 0 for _, ln in ops) or not any(op in real for op, _ in ops):
+            return True
+        last = len(ops) - 1
+        for k, (op, _) in enumerate(ops):
+            if op == H and 0 < k < last:
+                return True
+            if op == S and 0 < k < last:
+                ok = (k == 1 and (ops[0][0] == H or (len(ops) == 3 and ops[2][0] == H))) or \
+                     (k == last - 1 and ops[last][0] == H)
+                if not ok:
+                    return True
+            if op == P and k > 0 and (k == last or ops[k - 1][0] not in real or ops[k + 1][0] not in real):
+                return True
+        # two I (or two D) with no M/N/=/X or P between them
+        seg = []
+        for op, _ in ops + [(M, 1)]:
+            if op in (M, N, EQ, X, P):
+                if seg.count(I) > 1 or seg.count(D) > 1:
+                    return True
+                seg = []
+            elif op in (I, D):
+                seg.append(op)
+        at = pos + 1
+        for op, ln in ops:
+            if op in (M, EQ, X) and ref >= 0 and ref_len is not None and at + ln - 1 > ref_len[ref]:
+                return True
+            if op in (M, D, N, EQ, X):
+                at += ln
+    rlen = sum(ln for op, ln in ops if op in (M, D, N, EQ, X))
+    qlen = sum(ln for op, ln in ops if op in (M, I, S, EQ, X))
+    end = 0 if unmapped else pos + rlen
+    if end <= 0:
+        end = pos + 1
+    if _reg2bin(pos, end) != bin_:
+        return True
+    if lseq and ncig and qlen != lseq:
+        return True
+    if lseq == 0 and not flag & 0x100:
+        tags = _aux_tags(rec[36 + lrn + 4 * ncig:4 + bs])
+        if "FZ" not in tags and not (tags.get("CQ") and tags.get("CS")):
+            return True
+    return False

@@ -20,7 +20,44 @@ def test_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert hbam.lib().hbam_abi_version() == 1
+    assert hbam.lib().hbam_abi_version() == 2
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirrors have the layout a C compiler gives include/hbam.h."""
+    import os
+    import subprocess
+    src = tmp_path / "layout.c"
+    src.write_text("""#include <stdio.h>
+#include <stddef.h>
+#include "hbam.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(hbam_opts), offsetof(hbam_opts, window_bytes),
+         sizeof(hbam_batch), offsetof(hbam_batch, next_voff), offsetof(hbam_batch, status),
+         sizeof(hbam_gpu_stats), sizeof(hbam_header_info));
+  return 0;
+}
+""")
+    exe = tmp_path / "layout"
+    inc = os.path.join(os.path.dirname(hbam.HEADER_PATH))
+    subprocess.check_call(["gcc", "-I", inc, "-o", str(exe), str(src)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    assert got == [C.sizeof(hbam.Opts), hbam.Opts.window_bytes.offset, C.sizeof(hbam.Batch),
+                   hbam.Batch.next_voff.offset, hbam.Batch.status.offset, C.sizeof(hbam.GpuStats),
+                   C.sizeof(hbam.HeaderInfo)]
+
+
+def test_unknown_stringency_is_an_argument_error(test_bam):
+    # hadoopbam.samheaderreader.validation-stringency takes STRICT / LENIENT / SILENT only
+    with pytest.raises(hbam.HbamError) as e:
+        hbam.BamFile(test_bam, stringency=7)
+    assert e.value.code == hbam.E_ARG
+
+
+def test_write_time_index_granularity_checked_first():
+    with pytest.raises(hbam.HbamError) as e:
+        hbam.splitting_index_for_records([1, 2, 3], 0, 100)
+    assert e.value.code == hbam.E_ARG
 
 
 def test_static_keys_match_reference_semantics():
@@ -61,4 +98,8 @@ def test_bgzf_compress_argument_errors():
     assert e.value.code == hbam.E_ARG
     with pytest.raises(hbam.HbamError) as e:
         hbam.bgzf_compress(b"ACGT" * 10, block_size=65537)
+    assert e.value.code == hbam.E_ARG
+    # an explicit empty block list does not cover a non-empty payload
+    with pytest.raises(hbam.HbamError) as e:
+        hbam.bgzf_compress(b"ACGT" * 10, block_lens=[])
     assert e.value.code == hbam.E_ARG
