@@ -142,6 +142,20 @@ int orc_get_splits(orc_stream *s, const uint8_t *file, uint64_t flen,
 uint64_t orc_bgzf_compress(const uint8_t *data, uint64_t len, const uint32_t *block_lens,
                            uint64_t nblk, int level, int eof, uint8_t *out);
 
+/* The restated reader / indexer over a whole file on `threads` host threads
+ * (orc_scan.c): mode 0 = BAMRecordReader over [first record, EOF) with the
+ * given stringency (record count, xor of keys, sum of voffs); mode 1 =
+ * SplittingBAMIndexer.index at granularity g into *sbi (orc_free).
+ * max_blocks > 0 reads only the first max_blocks BGZF blocks (a sample).
+ * Same results as orc_decode_span / orc_splitting_index, streamed block by
+ * block: memory is independent of the file size. */
+typedef struct {
+  uint64_t records, key_xor, voff_sum, blocks, u_bytes;
+  int32_t status, rewalks;
+} orc_scan_result;
+int orc_scan(const uint8_t *file, uint64_t len, int threads, int mode, int stringency, int32_t g,
+             uint64_t max_blocks, uint8_t **sbi, uint64_t *sbi_len, orc_scan_result *res);
+
 /* zlib crc32, for tests */
 uint32_t orc_crc32(const uint8_t *p, uint64_t n);
 

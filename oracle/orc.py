@@ -59,6 +59,7 @@ def lib():
         L.orc_writable_encode.restype = u64
         L.orc_writable_decode.argtypes = [P, u64, P, u64, P]
         L.orc_set_stringency.argtypes = [P, C.c_int]
+        L.orc_scan.argtypes = [P, u64, C.c_int, C.c_int, C.c_int, i32, u64, C.POINTER(P), C.POINTER(u64), P]
         L.orc_record_invalid.argtypes = [P, i32, i32, P, C.c_int]
         L.orc_record_invalid.restype = C.c_int
         _LIB = L
@@ -283,3 +284,33 @@ def record_invalid(rec: bytes, n_ref, ref_len=None, strict=True):
         arr = np.ascontiguousarray(ref_len, np.int32)
         rl = arr.ctypes.data
     return bool(lib().orc_record_invalid(buf, bs, n_ref, rl, 1 if strict else 0))
+
+
+class _ScanResult(C.Structure):
+    _fields_ = [("records", C.c_uint64), ("key_xor", C.c_uint64), ("voff_sum", C.c_uint64),
+                ("blocks", C.c_uint64), ("u_bytes", C.c_uint64), ("status", C.c_int32), ("rewalks", C.c_int32)]
+
+
+def scan(data, threads=1, mode="decode", stringency=STRICT, granularity=4096, max_blocks=0):
+    """orc_scan: the restated reader (mode 'decode') or indexer (mode 'index')
+    over a whole file on `threads` host threads; data = bytes or a uint8
+    ndarray.  Returns (result dict, .splitting-bai bytes or None)."""
+    L = lib()
+    if isinstance(data, np.ndarray):
+        ptr, n = data.ctypes.data, data.nbytes
+    else:
+        keep = C.create_string_buffer(bytes(data), max(len(data), 1))
+        ptr, n = C.addressof(keep), len(data)
+    r = _ScanResult()
+    out = C.c_void_p()
+    olen = C.c_uint64()
+    m = 0 if mode == "decode" else 1
+    rc = L.orc_scan(ptr, n, threads, m, stringency, granularity, max_blocks,
+                    C.byref(out) if m else None, C.byref(olen) if m else None, C.byref(r))
+    sbi = None
+    if m and out.value:
+        sbi = C.string_at(out, olen.value)
+        L.orc_free(out)
+    d = {f: getattr(r, f) for f, _ in _ScanResult._fields_}
+    d["rc"] = rc
+    return d, sbi
