@@ -165,9 +165,12 @@ int BamFile::prefetch(uint64_t lo, uint64_t hi) {
     err_ = "prefetch needs a host copy of the file";
     return kErrState;
   }
-  if (hipSetDevice(pipe_->device()) != hipSuccess || src_.dev.reserve(hi - lo + hbam::kFilePad) != hipSuccess ||
-      hipMemcpy(src_.dev.p, src_.host + lo, hi - lo, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(src_.dev.p + (hi - lo), 0, hbam::kFilePad) != hipSuccess) {
+  // byte lo lands at dev.p + lo % 16: file offsets keep their 16 B alignment
+  // on the device, which the kernels' aligned loads assume
+  uint8_t* at;
+  if (hipSetDevice(pipe_->device()) != hipSuccess || src_.dev.reserve(hi - lo + 16 + hbam::kFilePad) != hipSuccess ||
+      hipMemcpy(at = src_.dev.p + (lo & 15), src_.host + lo, hi - lo, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(at + (hi - lo), 0, hbam::kFilePad) != hipSuccess) {
     err_ = "prefetch: HIP copy failed";
     return kErrDevice;
   }
@@ -187,14 +190,15 @@ int BamFile::load_window(uint64_t lo, uint64_t hi, bool free_start, bool host_on
   win_lo_ = ~0ull;
   int rc;
   if (dev) {
-    rc = pipe_->attach_device(src_.dev.p + (lo - src_.dev_lo), hi - lo, lo, hi == src_.size);
+    rc = pipe_->attach_device(src_.dev.p + (src_.dev_lo & 15) + (lo - src_.dev_lo), hi - lo, lo, hi == src_.size);
   } else {
     if (!src_.host) {
       err_ = "file bytes [" + std::to_string(lo) + ", " + std::to_string(hi) + ") are not resident in HBM";
       return kErrState;
     }
-    rc = pipe_->load(src_.host + lo, hi - lo, lo, hi == src_.size);
-    src_.bytes_read += hi - lo;
+    uint64_t copied = 0;
+    rc = pipe_->load(src_.host + lo, hi - lo, lo, hi == src_.size, &copied);
+    src_.bytes_read += copied;
   }
   if (rc == kOk) rc = pipe_->locate(free_start);
   if (rc != kOk) {
@@ -345,17 +349,21 @@ int BamFile::parse_header() {
   }
 }
 
-int BamFile::decode_step(const Carry& from, uint64_t vend, hbam::ChainMode mode, bool decode, bool continuation,
+int BamFile::decode_step(Carry from, uint64_t vend, hbam::ChainMode mode, bool decode, bool continuation,
                          Step* out) {
   *out = Step();
   Carry c = from;
   uint64_t span_w = window_bytes_;
-  bool host_only = false;
+  bool host_only = false, clamp = vend != ~0ull;
   for (int guard = 0; guard < 96; ++guard) {
     out->next = c;
     if (c.upos <= 0xffff && c.voff() >= vend) return kOk;  // the split ends here
     if (c.coff >= src_.size) return kOk;                    // past the last block: end of stream
-    int rc = load_window(c.coff, c.coff + span_w, false, host_only);
+    // a split ending at vend needs its last record's bytes, rarely more than
+    // a block past vend: no need to copy a whole window beyond it
+    uint64_t hi = c.coff + span_w;
+    if (clamp) hi = std::min(hi, std::max((vend >> 16) + 0x20000, c.coff + 0x20000));
+    int rc = load_window(c.coff, hi, false, host_only);
     if (rc != kOk) return rc;
     hbam::Pipeline& p = *pipe_;
     const auto& B = p.blocks();
@@ -390,8 +398,8 @@ int BamFile::decode_step(const Carry& from, uint64_t vend, hbam::ChainMode mode,
     }
     if (s.status == kOk && s.n == 0 && s.next_pos == p0 && p0 < s.q_end && !p.at_eof()) {
       // the first record does not end inside this window: a bigger one
-      if (win_hi_ < std::min(src_.size, c.coff + span_w)) host_only = true;  // clipped by the HBM-resident range
-      else span_w *= 2;
+      if (win_hi_ < std::min(src_.size, hi) && !host_only) host_only = true;  // clipped by the HBM-resident range
+      else span_w = 2 * std::max(span_w, win_hi_ - c.coff), clamp = false;      // a record longer than the window
       continue;
     }
     out->span = s;
@@ -404,7 +412,9 @@ int BamFile::decode_step(const Carry& from, uint64_t vend, hbam::ChainMode mode,
     } else {
       out->next = Carry{p.window_end(), np - p.total_u()};
     }
-    bool ended = s.status != kOk || np >= s.q_end || (p.at_eof() && np >= p.total_u());
+    // q_end > total_u: vend lies past this window (an indexer record that
+    // straddles the window end puts np there too, and the walk goes on)
+    bool ended = s.status != kOk || (s.q_end <= p.total_u() && np >= s.q_end) || (p.at_eof() && np >= p.total_u());
     if (!ended) {  // stopped at a dead position: an empty block k >= 1 starts there (finish_blocks)
       auto it = std::lower_bound(B.begin(), B.end(), np, [](const BlockInfo& b, uint64_t x) { return b.ustart < x; });
       for (; it != B.end() && it->ustart == np && !ended; ++it)

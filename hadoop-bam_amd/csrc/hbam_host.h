@@ -45,7 +45,7 @@ class PinnedVec {
   PinnedVec(const PinnedVec&) = delete;
   PinnedVec& operator=(const PinnedVec&) = delete;
   ~PinnedVec() { release(); }
-  bool resize(size_t n);  // contents not kept on growth
+  bool resize(size_t n);  // keeps the first min(n, size()) elements
   size_t size() const { return n_; }
   T* data() { return p_; }
   const T* data() const { return p_; }
@@ -134,7 +134,7 @@ class BamFile {
   // Decode the part of FileVirtualSplit [.., vend) that starts at `from`
   // and lies in one window.  continuation: `from` is the carry of the
   // previous step (not a reader seek).
-  int decode_step(const Carry& from, uint64_t vend, hbam::ChainMode mode, bool decode, bool continuation,
+  int decode_step(Carry from, uint64_t vend, hbam::ChainMode mode, bool decode, bool continuation,
                   Step* out);
 
   // Every BGZF block of the file (window by window; cached).  ustart is the

@@ -2712,10 +2712,11 @@ static inline unsigned grid_for(uint64_t n, unsigned bs, unsigned cap = 65535u *
 
 hipError_t launch_bgzf_scan(const uint8_t* file, uint64_t buf_base, uint64_t lo, uint64_t hi, uint64_t* cand,
                             uint32_t cap, uint32_t* count, hipStream_t s) {
-  // scan from the position at or below lo that is 16 B aligned in the device
-  // buffer (file + buf_base = the buffer start, hipMalloc-aligned);
-  // candidates below lo are dropped
-  const uint64_t a = buf_base + ((lo - buf_base) & ~15ull);
+  // scan from the 16 B aligned file offset at or below lo (windows are placed
+  // so that file offsets keep their alignment; the bytes below buf_base are
+  // allocated); candidates below lo are dropped
+  (void)buf_base;
+  const uint64_t a = lo & ~15ull;
   const uint64_t nc = (hi - a + 15) / 16;
   hipLaunchKernelGGL(k_bgzf_scan, dim3(grid_for(nc, 256, 8192)), dim3(256), 0, s, file + a, hi - a, a, lo, cand,
                      cap, count);

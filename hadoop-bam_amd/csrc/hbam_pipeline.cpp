@@ -67,11 +67,21 @@ int Pipeline::hip_check(hipError_t e, const char* what) {
     if (_rc != kOk) return _rc;                        \
   } while (0)
 
-int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof) {
+int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof, uint64_t* host_bytes) {
   HIPCHK(hipSetDevice(device_));
-  HIPCHK(own_file_.reserve(len + kFilePad));
-  dfile_ = own_file_.p;
-  if (len) HIPCHK(hipMemcpyAsync(dfile_, data, len, hipMemcpyHostToDevice, stream_));
+  // the prefix of [base, base + len) that the window in place already holds
+  uint64_t keep = 0;
+  if (dfile_ && own_file_.p && dfile_ == own_file_.p + (base_ & 15) && base >= base_ && base < base_ + flen_)
+    keep = std::min(base_ + flen_, base + len) - base;
+  const uint8_t* old = keep ? dfile_ + (base - base_) : nullptr;
+  if (keep) own_file_.swap(own_spare_);
+  // byte `base` lands at a buffer offset of base % 16: the kernels address the
+  // window in file coordinates (dfile_ - base_) with 16 B aligned loads
+  HIPCHK(own_file_.reserve(len + 16 + kFilePad));
+  dfile_ = own_file_.p + (base & 15);
+  if (keep) HIPCHK(hipMemcpyAsync(dfile_, old, keep, hipMemcpyDeviceToDevice, stream_));
+  if (len > keep) HIPCHK(hipMemcpyAsync(dfile_ + keep, data + keep, len - keep, hipMemcpyHostToDevice, stream_));
+  if (host_bytes) *host_bytes = len - keep;
   HIPCHK(hipMemsetAsync(dfile_ + len, 0, kFilePad, stream_));
   HIPCHK(hipStreamSynchronize(stream_));
   flen_ = len;
@@ -85,6 +95,8 @@ int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof
 }
 
 int Pipeline::attach_device(const uint8_t* dptr, uint64_t len, uint64_t base, bool at_eof) {
+  if ((reinterpret_cast<uintptr_t>(dptr) - base) & 15)
+    return fail(kErrArg, "attach_device: file offset and device address differ in 16 B alignment");
   dfile_ = const_cast<uint8_t*>(dptr);
   flen_ = len;
   base_ = base;
@@ -97,7 +109,7 @@ int Pipeline::attach_device(const uint8_t* dptr, uint64_t len, uint64_t base, bo
 }
 
 int Pipeline::reload(const uint8_t* data, uint64_t len, bool pinned, float* ms) {
-  if (!dfile_ || dfile_ != own_file_.p || len != flen_)
+  if (!dfile_ || dfile_ != own_file_.p + (base_ & 15) || len != flen_)
     return fail(kErrState, "reload needs a loaded window of the same size");
   HIPCHK(hipSetDevice(device_));
   uint8_t* staging = nullptr;

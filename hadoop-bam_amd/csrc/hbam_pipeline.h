@@ -25,7 +25,14 @@ template <typename T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;  // elements
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
+  void swap(DevBuf& o) {
+    std::swap(p, o.p);
+    std::swap(n, o.n);
+  }
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;
@@ -94,7 +101,10 @@ class Pipeline {
 
   // Copy file bytes [base, base + len) into the window buffer.  at_eof: the
   // range ends at the end of the file (else the window is open).
-  int load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof);
+  // When the window in place was loaded from the host too and holds a prefix
+  // of the new range, that prefix moves device to device and only the rest
+  // crosses PCIe; *host_bytes (optional) = the bytes copied from `data`.
+  int load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof, uint64_t* host_bytes = nullptr);
   // Use device-resident file bytes [base, base + len) (readable for kFilePad
   // bytes past len).
   int attach_device(const uint8_t* dptr, uint64_t len, uint64_t base, bool at_eof);
@@ -202,6 +212,7 @@ class Pipeline {
 
   uint8_t* dfile_ = nullptr;
   DevBuf<uint8_t> own_file_;  // window bytes copied from the host (+ kFilePad zeros)
+  DevBuf<uint8_t> own_spare_;  // the other buffer of the pair (a window's kept prefix moves across)
   uint64_t flen_ = 0, base_ = 0;
   bool at_eof_ = true;
   uint64_t window_end_ = 0;

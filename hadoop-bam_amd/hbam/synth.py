@@ -27,6 +27,8 @@ def _lib():
         _G.gen_bam.argtypes = [C.POINTER(_Params), C.POINTER(C.c_void_p), C.POINTER(C.c_uint64),
                                C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         _G.gen_free.argtypes = [C.c_void_p]
+        _G.gen_bam_segment.argtypes = [C.POINTER(_Params), C.c_uint64, C.c_uint64, C.c_int, C.POINTER(C.c_void_p),
+                                       C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     return _G
 
 
@@ -51,3 +53,27 @@ def make_bam(n_records, mode="short", level=5, strategy="default", block_payload
         data = C.string_at(out, n.value)
     _lib().gen_free(out)
     return data, {"n_records": n_records, "compressed": n.value, "blocks": nb.value, "uncompressed": u.value}
+
+
+def make_bam_segment(n_records, lo, hi, with_header, eof_block, mode="short", level=5, block_payload=65280,
+                     threads=None, seed=0x48424D00, all_unmapped=False):
+    """Records [lo, hi) of the n_records model as BGZF blocks ending at a
+    record boundary (header first if with_header, EOF block if eof_block):
+    the segments of consecutive record ranges concatenate into one BAM, so N
+    processes can each write their part of one file.  Returns (uint8 ndarray,
+    info)."""
+    import numpy as np
+    p = _Params(n_records, 1 if mode == "long" else 0, level, 0, block_payload,
+                threads or min(16, os.cpu_count() or 8), int(eof_block), int(all_unmapped), seed)
+    out = C.c_void_p()
+    n = C.c_uint64()
+    nb = C.c_uint64()
+    u = C.c_uint64()
+    rc = _lib().gen_bam_segment(C.byref(p), lo, hi, int(with_header), C.byref(out), C.byref(n), C.byref(nb),
+                                C.byref(u))
+    if rc != 0:
+        raise RuntimeError(f"gen_bam_segment failed ({rc})")
+    arr = np.empty(n.value, np.uint8)
+    C.memmove(arr.ctypes.data, out, n.value)
+    _lib().gen_free(out)
+    return arr, {"records": hi - lo, "compressed": n.value, "blocks": nb.value, "uncompressed": u.value}

@@ -305,6 +305,7 @@ static size_t make_header(uint8_t *o) {
 typedef struct {
   const model *m;
   uint64_t lo, hi;          /* record range */
+  uint64_t base;            /* first record of the segment: sizes / offs index i - base */
   uint32_t *sizes;
   uint64_t *offs;
   uint8_t *u;
@@ -322,9 +323,9 @@ static void *worker(void *arg) {
   job *j = (job *)arg;
   const gen_params *p = j->m->p;
   if (j->phase == 0) {
-    for (uint64_t i = j->lo; i < j->hi; ++i) j->sizes[i] = make_record(j->m, i, NULL);
+    for (uint64_t i = j->lo; i < j->hi; ++i) j->sizes[i - j->base] = make_record(j->m, i, NULL);
   } else if (j->phase == 1) {
-    for (uint64_t i = j->lo; i < j->hi; ++i) make_record(j->m, i, j->u + j->offs[i]);
+    for (uint64_t i = j->lo; i < j->hi; ++i) make_record(j->m, i, j->u + j->offs[i - j->base]);
   } else {
     z_stream z;
     for (uint64_t b = j->blk_lo; b < j->blk_hi; ++b) {
@@ -362,35 +363,44 @@ static void run_jobs(job *jobs, int nt) {
   for (int t = 0; t < nt; ++t) pthread_join(th[t], NULL);
 }
 
-/* Generate a BAM into a malloc'd buffer.  Returns 0 on success. */
-int gen_bam(const gen_params *p, uint8_t **out, uint64_t *out_len, uint64_t *n_blocks, uint64_t *u_len) {
+/* Records [lo, hi) of the n_records-record model as a run of BGZF blocks:
+ * the BAM header first when with_header, the payload cut every block_payload
+ * bytes with a short last block (the run ends at a record boundary, so the
+ * runs of consecutive record ranges concatenate into one BAM), the EOF
+ * block when p->eof_block.  Returns 0 on success. */
+int gen_bam_segment(const gen_params *p, uint64_t lo, uint64_t hi, int with_header, uint8_t **out, uint64_t *out_len,
+                    uint64_t *n_blocks, uint64_t *u_len) {
   model m;
   m.p = p;
   const uint64_t N = p->n_records;
+  if (hi > N) hi = N;
+  if (lo > hi) lo = hi;
   m.n_unplaced_start = p->mode == 0 ? N - N / 200 : N;
   m.n_mapped = m.n_unplaced_start;
   /* 30x local coverage of 150 bp reads: 5 bp per read */
   m.span = p->mode == 0 ? m.n_mapped * 5 : m.n_mapped * 1500;
   int nt = p->threads > 0 ? (p->threads > 256 ? 256 : p->threads) : 8;
-  uint32_t *sizes = (uint32_t *)malloc((N + 1) * sizeof *sizes);
-  uint64_t *offs = (uint64_t *)malloc((N + 1) * sizeof *offs);
+  const uint64_t R = hi - lo;
+  uint32_t *sizes = (uint32_t *)malloc((R + 1) * sizeof *sizes);
+  uint64_t *offs = (uint64_t *)malloc((R + 1) * sizeof *offs);
   job jobs[256];
   for (int t = 0; t < nt; ++t) {
     memset(&jobs[t], 0, sizeof jobs[t]);
     jobs[t].m = &m;
-    jobs[t].lo = N * (uint64_t)t / (uint64_t)nt;
-    jobs[t].hi = N * (uint64_t)(t + 1) / (uint64_t)nt;
+    jobs[t].lo = lo + R * (uint64_t)t / (uint64_t)nt;
+    jobs[t].hi = lo + R * (uint64_t)(t + 1) / (uint64_t)nt;
+    jobs[t].base = lo;
     jobs[t].sizes = sizes;
     jobs[t].offs = offs;
     jobs[t].phase = 0;
   }
   run_jobs(jobs, nt);
-  const size_t hl = make_header(NULL);
+  const size_t hl = with_header ? make_header(NULL) : 0;
   uint64_t u = hl;
-  for (uint64_t i = 0; i < N; ++i) { offs[i] = u; u += sizes[i]; }
+  for (uint64_t i = 0; i < R; ++i) { offs[i] = u; u += sizes[i]; }
   uint8_t *ub = (uint8_t *)malloc(u + 16);
   if (!ub) return 1;
-  make_header(ub);
+  if (with_header) make_header(ub);
   for (int t = 0; t < nt; ++t) { jobs[t].u = ub; jobs[t].phase = 1; }
   run_jobs(jobs, nt);
   const uint64_t nb = (u + (uint64_t)p->block_payload - 1) / (uint64_t)p->block_payload;
@@ -428,6 +438,11 @@ int gen_bam(const gen_params *p, uint8_t **out, uint64_t *out_len, uint64_t *n_b
   if (n_blocks) *n_blocks = nb + (p->eof_block ? 1 : 0);
   if (u_len) *u_len = u;
   return 0;
+}
+
+/* Generate a whole BAM into a malloc'd buffer.  Returns 0 on success. */
+int gen_bam(const gen_params *p, uint8_t **out, uint64_t *out_len, uint64_t *n_blocks, uint64_t *u_len) {
+  return gen_bam_segment(p, 0, p->n_records, 1, out, out_len, n_blocks, u_len);
 }
 
 void gen_free(void *p) { free(p); }

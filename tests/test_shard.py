@@ -18,17 +18,35 @@ import orc
 from hbam import shard, synth
 
 
+GUESS_BYTES = 3 * 0xFFFF + 0xFFFE  # BAMSplitGuesser MAX_BYTES_READ (BAMSplitGuesser.java:66-73)
+
+
 class OracleDecoder:
+    """The oracle as a rank's decoder, with the byte accounting of a split
+    reader: BAMSplitGuesser reads at most GUESS_BYTES from the split start,
+    and BAMRecordReader reads from its first block to the end of the block
+    holding its last record's last byte (WrapSeekable seeks, no more)."""
+
     def __init__(self, data):
         self.s = orc.Stream(data)
+        self.read = 0
 
     def guess_record_starts(self, begs, ends):
+        self.read += sum(min(e - b, GUESS_BYTES) for b, e in zip(begs, ends))
         return [self.s.guess_record_start(b, e) for b, e in zip(begs, ends)]
 
     def decode_span(self, vs, ve):
         rc, r = self.s.decode_span(vs, ve)
         assert rc == 0
+        if len(r["voff"]):
+            last = int(r["offset"][-1]) + 36 + int(r["rest_len"][-1]) - 1
+            bl = self.s.blocks
+            k = int(np.searchsorted(bl["ustart"] + bl["isize"], last, side="right"))
+            self.read += int(bl["coff"][k]) + int(bl["csize"][k]) - (vs >> 16)
         return r
+
+    def bytes_read(self):
+        return self.read
 
 
 def _free_port():
@@ -37,17 +55,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
+WINDOW = 256 * 1024  # GPU decoder: compressed bytes per HBM window
+
+
 def _worker(rank, world, port, path, outdir, granularity, use_gpu):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    data = open(path, "rb").read()
     if use_gpu:
-        import hbam
-        dec = hbam.BamFile(data, device=0)
+        import hbam  # split-local: the rank maps the file and copies only the windows it decodes
+        dec = hbam.BamFile(path=path, device=0, window_bytes=WINDOW)
         first = dec.header()["first_record_voff"]
     else:
-        dec = OracleDecoder(data)
+        dec = OracleDecoder(open(path, "rb").read())
         first = dec.s.first_record_voff
 
     def all_gather(obj):
@@ -55,12 +75,13 @@ def _worker(rank, world, port, path, outdir, granularity, use_gpu):
         dist.all_gather_object(out, obj)
         return out
 
-    rd = shard.ShardedBamReader(dec, len(data), first, rank, world, all_gather)
+    rd = shard.ShardedBamReader(dec, os.path.getsize(path), first, rank, world, all_gather)
     recs, base, total, sbi = rd.run(granularity)
     keys = recs["key"] if recs is not None else np.zeros(0, np.int64)
     voffs = recs["voff"] if recs is not None else np.zeros(0, np.uint64)
     np.savez(os.path.join(outdir, f"r{rank}.npz"), key=keys, voff=voffs, base=base, total=total,
-             sbi=np.frombuffer(sbi, np.uint8) if sbi is not None else np.zeros(0, np.uint8))
+             sbi=np.frombuffer(sbi, np.uint8) if sbi is not None else np.zeros(0, np.uint8),
+             bytes_read=dec.bytes_read())
     dist.destroy_process_group()
 
 
@@ -85,6 +106,17 @@ def check_against_oracle(data, parts, granularity):
     assert bases == [int(sum(len(q["voff"]) for q in parts[:r])) for r in range(len(parts))]
     assert all(int(p["total"]) == len(want["voff"]) for p in parts)
     assert parts[0]["sbi"].tobytes() == s.splitting_index(granularity)
+
+
+def check_rank_local_reads(data, parts, slack):
+    """Every rank reads about its own FileSplit: its split's bytes plus the
+    guesser's window and the tail that finishes its last record (`slack`),
+    never the whole file."""
+    world = len(parts)
+    for r, (a, n) in enumerate(shard.file_splits(len(data), world)):
+        got = int(parts[r]["bytes_read"])
+        assert got <= n + slack, (r, got, n, slack)
+    assert sum(int(p["bytes_read"]) for p in parts) <= len(data) + world * slack
 
 
 def test_file_splits_cover_the_file():
@@ -114,3 +146,4 @@ def test_sharded_read_matches_whole_file(tmp_path, world, g, kw):
     data, _ = synth.make_bam(**kw)
     parts = run_sharded(data, world, g, tmp_path)
     check_against_oracle(data, parts, g)
+    check_rank_local_reads(data, parts, GUESS_BYTES + 4 * 65536 + (800_000 if kw.get("mode") == "long" else 0))
