@@ -1,165 +1,360 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X BAM read hot path (BASELINE.json metric).
 
-One "step" = one full pass of the hot path over one synthetic BAM resident in
-HBM: BGZF block discovery -> inflate (Huffman phase + LZ77 phase) -> record
-boundary scan -> fused field decode + sort keys + voffs.  Workload: config C2,
-a synthetic 10M x 150 bp paired-end coordinate-sorted BAM (generated on the
-box, zlib level 5 as htsjdk writes).  With N GPUs each rank owns one C2-sized
-BGZF shard (weak scaling; shards are independent, no data-path collective).
+One "step" = one pass of the hot path over a rank's FileVirtualSplit of ONE
+synthetic BAM, its compressed bytes already resident in HBM: BGZF block
+discovery -> inflate (Huffman phase + LZ77 phase) -> record-boundary chain ->
+fused field decode + sort keys + voffs into SoA columns in HBM
+(hbam_decode_span_device, the BAMRecordReader path).
 
-Prints ONE JSON line (rank 0).
+The file: N ranks write one BAM together.  Rank r generates records
+[r*R, (r+1)*R) of an N*R-record model (tools/gen_synth_bam.c, zlib level 5,
+BGZF runs ending at record boundaries, header on rank 0, EOF block on the
+last rank) and writes them at its offset of a shared file.  At N=1 this is
+config C2 (10M x 150 bp paired-end, ~1.4 GB compressed); at N>1 a C3-shaped
+file of N*C2 bytes.  Each rank then plans its split exactly as Hadoop-BAM
+does (FileInputFormat byte range -> BAMSplitGuesser -> empty-split merge,
+hbam/shard.py), copies only its split's bytes to its GPU, and decodes it:
+weak scaling, no data-path collective (metadata all_gathers only).
+
+Prints ONE JSON line (rank 0).  Side legs at N=1 (rank 0): CPU baseline
+(the oracle at 1 thread and on every host core), in-session PMC traffic of
+the dominant kernel (rocprofv3 child runs), the drop-in call end to end
+(hbam_open -> hbam_decode_span batches -> pinned host columns), the C3 / C5
+configs at 60 GB, C4 long reads, write-path legs.
 """
 import argparse
+import glob
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "hadoop-bam_amd"))
-sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 METRIC = "uncompressed BAM decode GB/s + records/sec per GPU and 8-GPU node"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+SEED = 0x48424D00
+ALL = (1 << 64) - 1
+SOA_BYTES_PER_RECORD = 37  # key 8 + voff 8 + rest_off 8 + refID 4 + pos 4 + flag 2 + bin 2 + mapq 1
+BGZF_EOF = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(data, info, seconds):
-    """Oracle (zlib inflate + htsjdk-rule record chain + keys) on the host, one
-    thread, on a prefix of the same BAM sized to ~`seconds` of work."""
-    import orc
+def host_cores():
+    """CPUs this process may use: the affinity set, capped by a cgroup quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def scratch_dir():
+    return "/dev/shm" if os.path.isdir("/dev/shm") and os.access("/dev/shm", os.W_OK) else tempfile.gettempdir()
+
+
+def pwrite_all(fd, arr, off):
+    mv = memoryview(arr).cast("B")
+    done = 0
+    while done < len(mv):
+        done += os.pwrite(fd, mv[done:], off + done)
+
+
+# ---------------------------------------------------------------------------
+# the file
+# ---------------------------------------------------------------------------
+def build_shared_bam(path, rank, world, records, all_gather, barrier):
+    """Each rank writes its segment of one BAM; returns (size, inflated bytes)."""
+    from hbam import synth
+    t = time.time()
+    seg, info = synth.make_bam_segment(world * records, rank * records, (rank + 1) * records,
+                                       with_header=rank == 0, eof_block=rank == world - 1, seed=SEED)
+    sizes = all_gather((int(seg.nbytes), int(info["uncompressed"])))
+    off = sum(s for s, _ in sizes[:rank])
+    size = sum(s for s, _ in sizes)
+    if rank == 0:
+        with open(path, "wb") as fh:
+            fh.truncate(size)
+    barrier()
+    fd = os.open(path, os.O_WRONLY)
+    try:
+        pwrite_all(fd, seg, off)
+    finally:
+        os.close(fd)
+    barrier()
+    log(f"[rank {rank}] wrote segment {seg.nbytes} B at {off} of {size} ({time.time() - t:.1f}s)")
+    return size, sum(u for _, u in sizes)
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline: the oracle (oracle/orc_scan.c) on the host's own cores
+# ---------------------------------------------------------------------------
+def cpu_baseline(path, size, seconds):
+    """The restated read path (zlib inflate + htsjdk record rules + keys) on
+    the host: all usable cores over the whole file (blocks cut into ranges,
+    one per thread) and one thread over a prefix sized to ~`seconds`.
+    Also returns the oracle's whole-file digest for the parity check."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
-    # calibrate on a small prefix (whole BGZF blocks), then scale up
-    blocks = []
-    p = 0
-    while p < len(data):
-        bs = int.from_bytes(data[p + 16:p + 18], "little") + 1
-        blocks.append((p, bs))
-        p += bs
-    def run(nb):
-        end = blocks[nb - 1][0] + blocks[nb - 1][1]
-        t = time.perf_counter()
-        s = orc.Stream(data[:end])
-        rc, r = s.decode_span(s.first_record_voff, (1 << 64) - 1)
-        dt = time.perf_counter() - t
-        return dt, s.data_len, len(r["key"])
-    nb = min(len(blocks), 200)
-    dt, u, n = run(nb)
-    target = max(nb, min(len(blocks), int(nb * seconds / max(dt, 1e-3))))
-    dt, u, n = run(target)
-    return {"value": round(u / dt / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-            "records_per_s": round(n / dt, 1),
-            "sample": f"first {target} BGZF blocks ({u} inflated bytes, {n} records) of the same C2 BAM, "
-                      f"oracle/hbam_oracle.c (system zlib) single thread, {dt:.1f} s"}
+    import orc
+    data = np.memmap(path, np.uint8, mode="r", shape=(size,))
+    cores = host_cores()
+    t = time.perf_counter()
+    full, _ = orc.scan(data, threads=cores, mode="decode")
+    dt_all = time.perf_counter() - t
+    if full["rc"] != 0:
+        raise RuntimeError(f"oracle scan failed: {full}")
+    # one thread: calibrate on 200 blocks, then ~`seconds` worth
+    t = time.perf_counter()
+    r1, _ = orc.scan(data, threads=1, mode="decode", max_blocks=200)
+    dt = time.perf_counter() - t
+    nb = max(200, min(int(full["blocks"]), int(200 * seconds / max(dt, 1e-3))))
+    t = time.perf_counter()
+    r1, _ = orc.scan(data, threads=1, mode="decode", max_blocks=nb)
+    dt1 = time.perf_counter() - t
+    model = cpu_model()
+    out = {"value": round(full["u_bytes"] / dt_all / 1e9, 4), "unit": "GB/s", "cores": cores, "kind": "port",
+           "records_per_s": round(full["records"] / dt_all, 1), "cpu_model": model,
+           "sample": f"whole file ({full['u_bytes']} inflated bytes, {full['records']} records) through "
+                     f"oracle/orc_scan.c (system zlib, htsjdk reader rules, STRICT) on {cores} threads "
+                     f"({model}), {dt_all:.2f} s",
+           "single_thread": {"value": round(r1["u_bytes"] / dt1 / 1e9, 4), "unit": "GB/s", "cores": 1,
+                             "records_per_s": round(r1["records"] / dt1, 1),
+                             "sample": f"first {nb} BGZF blocks ({r1['u_bytes']} inflated bytes, "
+                                       f"{r1['records']} records), 1 thread, {dt1:.1f} s"}}
+    return out, full
 
 
-def extra_configs(c2, c2_info):
-    """Side measurements reported next to the headline (not part of `value`):
-    C5-style .splitting-bai generation (g=4096) over the same C2 BAM through
-    the SplittingBAMIndexer entry point (hbam_build_splitting_index: inflate +
-    indexer-rule chain + entry emit, file resident in HBM), and a C4-like
-    long-read BAM (ONT-style 10-50 kb reads, records spanning blocks) through
-    the same device pipeline as the headline."""
+# ---------------------------------------------------------------------------
+# in-session PMC traffic of the dominant kernel (rocprofv3 child processes)
+# ---------------------------------------------------------------------------
+def pmc_child(path, vstart, vend):
+    import hbam
+    with hbam.BamFile(path=path) as f:
+        f.prefetch(vstart >> 16, f.size)
+        f.decode_span_device(vstart, vend, digest=False)
+
+
+def pmc_traffic(path, vstart, vend, kernel):
+    """HBM bytes per launch of `kernel` (its full-size dispatches): two
+    rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: their TCC slots do not
+    fit one pass) over a child process decoding the same split once.
+    Corrections per MI355X_MICROARCH.md 'HBM [CDNA4]': both counters are KiB;
+    FETCH_SIZE counts half of a wide streaming read on gfx950 (doubled)."""
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "profiles"))
+    import summarize
+    out = {}
+    base = tempfile.mkdtemp(prefix="hbam_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+        cmd = [prof, "--pmc", counter, "--output-format", "csv", "-d", os.path.join(base, sub), "-o", "run", "--",
+               sys.executable, os.path.abspath(__file__), "--pmc-child", path, "--pmc-span", str(vstart), str(vend)]
+        p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                             start_new_session=True)
+        try:
+            _, err = p.communicate(timeout=150)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, 9)
+            p.wait()
+            return {"error": f"{counter} pass timed out"}
+        if p.returncode != 0:
+            return {"error": f"{counter} pass rc={p.returncode}: {err.decode(errors='replace')[-300:]}"}
+        cs = summarize.counters(base, sub)
+        e = cs.get(kernel) or cs.get(kernel + "<true>") or cs.get(kernel + "<false>")
+        if not e or ("main:" + counter) not in e:
+            return {"error": f"{counter}: no dispatch of {kernel} in the counter file"}
+        out[counter] = e["main:" + counter]
+    shutil.rmtree(base, ignore_errors=True)
+    fetch = out["FETCH_SIZE"] * 1024 * 2
+    write = out["WRITE_SIZE"] * 1024
+    return {"bytes_per_launch": int(fetch + write), "fetch_bytes": int(fetch), "write_bytes": int(write)}
+
+
+# ---------------------------------------------------------------------------
+# side legs (N=1, rank 0)
+# ---------------------------------------------------------------------------
+def dropin_leg(path, first, records):
+    """The call a JVM makes (hbam.h): hbam_open(path) maps the file; each
+    hbam_decode_span batch copies its windows host->HBM, decodes them and
+    copies the 15 SoA columns plus the rest-of-record bytes into pinned host
+    memory (BAMRecordReader.nextKeyValue's data, 1M records per batch)."""
+    import hbam
+    res = {}
+    for label, batch in (("batches_1M", 1 << 20),):
+        with hbam.BamFile(path=path) as f:
+            t = time.perf_counter()
+            n, k, nbytes = f.scan_batches(first, ALL, batch)
+            dt = time.perf_counter() - t
+            u = f.file_stats()[1]
+        assert n == records, (n, records)
+        res[label] = {"records": n, "batches": k, "rest_bytes_to_host": nbytes, "seconds": round(dt, 3),
+                      "uncompressed_GBps": round(u / dt / 1e9, 3), "records_per_s": round(n / dt, 1)}
+    return res
+
+
+def c3_c5_leg(target_gb, cores):
+    """C3 / C5 at their stated size: a >= target_gb BAM (header segment +
+    one C2-sized record segment repeated + EOF block: the repeats keep the
+    build to seconds; every byte is still read, inflated and decoded).
+    C3: decoded with the file streamed host->HBM window by window (4 GiB
+    windows, default hbam_opts), then again resident after a prefetch.
+    C5: .splitting-bai at g=4096 over it (resident).  Both checked against
+    the oracle run over BGZF ranges on every host core."""
+    import numpy as np
     import hbam
     from hbam import synth
-    res = {}
-    f = hbam.BamFile(c2.tobytes() if hasattr(c2, "tobytes") else c2)
-    t = time.perf_counter()
-    sbi = f.splitting_index(4096)
-    dt = time.perf_counter() - t
-    res["c5_splitting_bai_g4096_on_c2"] = {
-        "entries": len(sbi) // 8, "seconds": round(dt, 4),
-        "uncompressed_GBps": round(c2_info["uncompressed"] / dt / 1e9, 3),
-        "note": "first call: includes inflating every block (resident compressed file)"}
-    f.close()
-    data, info = synth.make_bam(12000, mode="long", as_numpy=True, seed=0x48424D04)
-    g = hbam.Gpu(0)
-    g.load(data)
-    g.run(timing=True)
-    ts = []
-    for _ in range(3):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import orc
+    r = 10_000_000
+    t = time.time()
+    head, hi = synth.make_bam_segment(2 * r, 0, r, with_header=True, eof_block=False, seed=SEED + 3)
+    body, bi = synth.make_bam_segment(2 * r, r, 2 * r, with_header=False, eof_block=False, seed=SEED + 3)
+    k = max(1, -(-(int(target_gb * 1e9) - head.nbytes) // body.nbytes))
+    size = head.nbytes + k * body.nbytes + len(BGZF_EOF)
+    path = os.path.join(scratch_dir(), f"hbam_c3_{os.getpid()}.bam")
+    try:
+        with open(path, "wb") as fh:
+            fh.truncate(size)
+        fd = os.open(path, os.O_WRONLY)
+        try:
+            pwrite_all(fd, head, 0)
+            for i in range(k):
+                pwrite_all(fd, body, head.nbytes + i * body.nbytes)
+            pwrite_all(fd, np.frombuffer(BGZF_EOF, np.uint8), head.nbytes + k * body.nbytes)
+        finally:
+            os.close(fd)
+        del head, body
+        n_rec = r * (k + 1)
+        u_tot = hi["uncompressed"] + k * bi["uncompressed"]
+        build_s = time.time() - t
+        log(f"[c3] built {size} B ({n_rec} records) in {build_s:.1f}s")
+        res = {"file": {"compressed_bytes": size, "uncompressed_bytes": u_tot, "records": n_rec,
+                        "layout": f"header segment + 1 segment x {k} + EOF (10M records each)",
+                        "build_seconds": round(build_s, 1)}}
+        with hbam.BamFile(path=path) as f:
+            first = f.header()["first_record_voff"]
+            t = time.perf_counter()
+            st = f.decode_span_device(first, ALL, timing=True, digest=True)
+            dt = time.perf_counter() - t
+            assert st["records"] == n_rec, (st["records"], n_rec)
+            res["c3_streamed_from_host"] = {
+                "seconds": round(dt, 3), "uncompressed_GBps": round(u_tot / dt / 1e9, 3),
+                "records_per_s": round(n_rec / dt, 1), "windows": st["windows"],
+                "note": "windows copied from the mapped file (pageable) inside the timed call"}
+            t = time.perf_counter()
+            f.prefetch(0, size)
+            pf = time.perf_counter() - t
+            t = time.perf_counter()
+            st2 = f.decode_span_device(first, ALL, timing=True, digest=True)
+            dt2 = time.perf_counter() - t
+            res["c3_resident"] = {"seconds": round(dt2, 3), "uncompressed_GBps": round(u_tot / dt2 / 1e9, 3),
+                                  "records_per_s": round(n_rec / dt2, 1), "windows": st2["windows"],
+                                  "prefetch_seconds": round(pf, 3),
+                                  "stages_ms": {x: round(st2[x], 1) for x in ("ms_locate", "ms_huff", "ms_lz77",
+                                                                             "ms_chain", "ms_decode")}}
+            t = time.perf_counter()
+            sbi = f.splitting_index(4096)
+            dti = time.perf_counter() - t
+        data = np.memmap(path, np.uint8, mode="r", shape=(size,))
         t = time.perf_counter()
-        st = g.run(timing=True)
-        ts.append(time.perf_counter() - t)
-    dt = min(ts)
-    res["c4_long_reads"] = {
-        "records": int(st["records"]), "compressed_bytes": info["compressed"],
-        "uncompressed_bytes": info["uncompressed"], "seconds": round(dt, 5),
-        "uncompressed_GBps": round(info["uncompressed"] / dt / 1e9, 3),
-        "stages_ms": {k: round(st[k], 3) for k in ("ms_locate", "ms_huff", "ms_lz77", "ms_chain", "ms_decode")}}
-    g.close()
-    return res
+        dec, _ = orc.scan(data, threads=cores, mode="decode")
+        dto = time.perf_counter() - t
+        t = time.perf_counter()
+        ires, want = orc.scan(data, threads=cores, mode="index", granularity=4096)
+        dtoi = time.perf_counter() - t
+        del data
+        res["c3_parity"] = {"records": st["records"] == dec["records"] == n_rec,
+                            "key_xor": st["key_xor"] == st2["key_xor"] == dec["key_xor"],
+                            "voff_sum": st["voff_sum"] == st2["voff_sum"] == dec["voff_sum"],
+                            "oracle_seconds": round(dto, 1), "oracle_threads": cores,
+                            "oracle_uncompressed_GBps": round(u_tot / dto / 1e9, 3)}
+        res["c5_splitting_bai_g4096"] = {
+            "entries": len(sbi) // 8, "seconds": round(dti, 3), "uncompressed_GBps": round(u_tot / dti / 1e9, 3),
+            "identical_to_oracle": sbi == want, "oracle_seconds": round(dtoi, 1), "oracle_threads": cores}
+        return res
+    finally:
+        try:
+            os.unlink(path)
+        except OSError:
+            pass
 
 
-def host_and_copy_legs(g, data, info, pass_ms):
-    """Measurements around the headline (rank 0, N=1; never `value`):
-    * SAMRecordWritable.write of the whole decoded C2 span on the GPU
-      (k_wr_copy + k_wr_bin_patch; 2 B of HBM traffic per encoded byte);
-    * the PCIe-inclusive rate: the compressed file copied host->HBM from
-      pinned memory (hbam_gpu_reload, HIP events) plus one device pass,
-      serial, the bound if the copy were fully overlapped, and the measured
-      overlapped pass (hbam_gpu_run_streamed: pieces copied on a copy stream
-      while landed pieces are located + inflated), checked equal to the
-      device-resident results;
-    * measured hipMemcpy device-to-device bandwidth (2 B per byte),
-      the practical ceiling the HBM-bound kernels are compared with."""
-    res = {}
-    ms, nb = g.encode_writables(iters=10)
-    res["writable_encode"] = {
-        "bytes": nb, "ms": round(ms, 4), "GBps_encoded": round(nb / ms / 1e6, 2),
-        "roofline": {"bound": "hbm", "achieved": round(2 * nb / ms / 1e6, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(2 * nb / ms / 1e6 / HBM_PEAK_GBS, 4)}}
-    h2d = min(g.reload(data.ctypes.data, data.nbytes, pinned=True) for _ in range(3))
-    pageable = g.reload(data.ctypes.data, data.nbytes, pinned=False)
-    res["pcie_inclusive"] = {
-        "h2d_ms_pinned": round(h2d, 3), "h2d_GBps_pinned": round(data.nbytes / h2d / 1e6, 2),
-        "h2d_ms_pageable": round(pageable, 3), "pass_ms": round(pass_ms, 3),
-        "serial_uncompressed_GBps": round(info["uncompressed"] / (h2d + pass_ms) / 1e6, 2),
-        "overlapped_bound_uncompressed_GBps": round(info["uncompressed"] / max(h2d, pass_ms) / 1e6, 2)}
-    # copy overlapped with locate + inflate of the pieces already in HBM
+def long_read_leg():
+    """C4-like: ONT-style 10-50 kb reads (records spanning many blocks, heavy
+    aux tags), resident, through the same device pipeline."""
     import hbam
-    import numpy as np
-    k_ref, v_ref = g.fetch(int(info["n_records"]))
-    with hbam.PinnedBuffer(data.nbytes) as pb:
-        pb.array[:] = data
-        best = {}
-        for piece in (32 << 20, 64 << 20):
-            ts = []
-            for _ in range(3):
-                st = g.run_streamed(pb.ptr, data.nbytes, piece)
-                ts.append(st["ms_total"])
-            best[piece] = min(ts)
-        k_s, v_s = g.fetch(int(info["n_records"]))
-    piece, ms_s = min(best.items(), key=lambda kv: kv[1])
-    res["pcie_inclusive"].update({
-        "streamed_ms": round(ms_s, 3), "streamed_piece_bytes": piece,
-        "streamed_uncompressed_GBps": round(info["uncompressed"] / ms_s / 1e6, 2),
-        "streamed_records_per_s": round(info["n_records"] / ms_s * 1e3, 1),
-        "streamed_matches_resident": bool(np.array_equal(k_s, k_ref) and np.array_equal(v_s, v_ref))})
-    res["bgzf_write"] = bgzf_write_leg(g, data, info)
-    d2d = g.d2d_bandwidth(1 << 32, 5)
-    res["d2d_copy_GBps_measured"] = round(d2d, 1)
-    res["writable_encode"]["frac_of_measured_d2d"] = round(2 * nb / ms / 1e6 / d2d, 4)
-    return res
+    from hbam import synth
+    data, info = synth.make_bam(12000, mode="long", as_numpy=True, seed=SEED + 4)
+    g = hbam.Gpu(0)
+    try:
+        g.load(data)
+        g.run(timing=True)
+        ts = []
+        for _ in range(3):
+            t = time.perf_counter()
+            st = g.run(timing=True)
+            ts.append(time.perf_counter() - t)
+    finally:
+        g.close()
+    dt = min(ts)
+    return {"records": int(st["records"]), "compressed_bytes": info["compressed"],
+            "uncompressed_bytes": info["uncompressed"], "seconds": round(dt, 5),
+            "uncompressed_GBps": round(info["uncompressed"] / dt / 1e9, 3),
+            "stages_ms": {k: round(st[k], 3) for k in ("ms_locate", "ms_huff", "ms_lz77", "ms_chain", "ms_decode")}}
 
 
-def bgzf_write_leg(g, data, info):
-    """BGZF write path: the resident inflated C2 stream
-    recompressed on the GPU with the file's block boundaries at zlib level 5
-    (hbam_gpu_bgzf_compress: k_deflate_blocks + k_dfl_crc + k_dfl_frame),
-    checked byte-identical to the generated file; the CPU leg is the oracle
-    (system zlib, htsjdk's deflater lifecycle) on the first 200 blocks."""
+def write_legs(path, size, info_u):
+    """SAMRecordWritable.write of the decoded file on the GPU, the measured
+    D2D copy ceiling, and the BGZF write path (the inflated file recompressed
+    at level 5 with its own block boundaries, byte-identical to the file)."""
     import zlib
     import numpy as np
+    import hbam
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orc
-    g.bgzf_compress(level=5, eof=False, iters=0)  # allocation + warm-up
-    ms, nb = g.bgzf_compress(level=5, eof=False, iters=1)
-    same = nb == data.nbytes and bool(np.array_equal(g.fetch_compressed(0, nb), data))
-    u, c = info["uncompressed"], info["compressed"]
+    data = np.fromfile(path, np.uint8)
+    g = hbam.Gpu(0)
+    res = {}
+    try:
+        g.load(data)
+        g.run()
+        ms, nb = g.encode_writables(iters=10)
+        d2d = g.d2d_bandwidth(1 << 32, 5)
+        res["writable_encode"] = {
+            "bytes": nb, "ms": round(ms, 4), "GBps_encoded": round(nb / ms / 1e6, 2),
+            "roofline": {"bound": "hbm", "achieved": round(2 * nb / ms / 1e6, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(2 * nb / ms / 1e6 / HBM_PEAK_GBS, 4)},
+            "frac_of_measured_d2d": round(2 * nb / ms / 1e6 / d2d, 4)}
+        res["d2d_copy_GBps_measured"] = round(d2d, 1)
+        g.bgzf_compress(level=5, eof=False, iters=0)
+        ms, nbw = g.bgzf_compress(level=5, eof=False, iters=1)
+        same = nbw == data.nbytes and bool(np.array_equal(g.fetch_compressed(0, nbw), data))
+    finally:
+        g.close()
     raw = data[:min(data.nbytes, 200 * 65536 * 2)].tobytes()
     p, pay, lens = 0, [], []
     while len(lens) < 200 and p + 18 <= len(raw):
@@ -174,46 +369,34 @@ def bgzf_write_leg(g, data, info):
     t = time.perf_counter()
     orc.bgzf_compress(sample, lens, level=5, eof=False)
     dt = time.perf_counter() - t
-    return {"level": 5, "ms": round(ms, 2), "uncompressed_GBps": round(u / ms / 1e6, 4),
-            "identical_to_file": same, "bytes_out": int(nb),
-            "roofline": {"bound": "latency (serial LZ77 recurrence per block)", "achieved": round((u + c) / ms / 1e6, 4),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round((u + c) / ms / 1e6 / HBM_PEAK_GBS, 7)},
-            "cpu_baseline": {"value": round(len(sample) / dt / 1e9, 5), "unit": "GB/s", "cores": 1, "kind": "port",
-                             "sample": f"first {len(lens)} blocks ({len(sample)} B) through oracle orc_bgzf_compress "
-                                       f"(system zlib 1.2.11, level 5), {dt:.2f} s"}}
+    res["bgzf_write"] = {
+        "level": 5, "ms": round(ms, 2), "uncompressed_GBps": round(info_u / ms / 1e6, 4),
+        "identical_to_file": same, "bytes_out": int(nbw),
+        "cpu_baseline": {"value": round(len(sample) / dt / 1e9, 5), "unit": "GB/s", "cores": 1, "kind": "port",
+                         "sample": f"first {len(lens)} blocks ({len(sample)} B) through oracle orc_bgzf_compress "
+                                   f"(system zlib, level 5), {dt:.2f} s"}}
+    return res
 
 
-def pmc_traffic(kernels):
-    """HBM bytes per launch of `kernels` (summed) from the newest committed
-    rocprofv3 PMC summary (profiles/*/summary.json, written by
-    profiles/collect.sh + summarize.py: FETCH_SIZE x1024 x2 gfx950 correction,
-    WRITE_SIZE x1024).  None when no summary is committed."""
-    import glob
-    best = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "summary.json")))
-    if not best:
-        return None, None
-    try:
-        ks = json.load(open(best[-1]))["kernels"]
-        tot = 0.0
-        for k in kernels:  # phase A is templated on LDS staging: C2 runs the staged instance
-            e = ks[k] if k in ks else ks[k + "<true>"]
-            tot += e["main_fetch_bytes_corrected"] + e["main_write_bytes"]
-        return int(tot), os.path.relpath(best[-1], ROOT)
-    except (KeyError, ValueError, OSError):
-        return None, None
-
-
+# ---------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--records", type=int, default=10_000_000)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--records", type=int, default=10_000_000, help="records per rank (C2: 10M)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--save-bam", default=None)
-    ap.add_argument("--no-extra", action="store_true", help="skip the C4 / index side measurements (the io legs always run at N=1)")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the in-session rocprofv3 PMC passes")
+    ap.add_argument("--no-extra", action="store_true", help="skip every side leg (drop-in, C3/C5, C4, write)")
+    ap.add_argument("--c3-gb", type=float, default=60.0, help="size of the C3/C5 file (0: skip that leg)")
+    ap.add_argument("--pmc-child", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-span", type=int, nargs=2, default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    if args.pmc_child:
+        pmc_child(args.pmc_child, *args.pmc_span)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -225,103 +408,159 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl")
 
-    import numpy as np
-    import hbam
-    from hbam import synth
-
-    t0 = time.time()
-    data, info = synth.make_bam(args.records, seed=0x48424D00 + 7919 * rank, as_numpy=True)
-    log(f"[rank {rank}] generated C2 shard: {info} in {time.time() - t0:.1f}s")
-    if args.save_bam and rank == 0:
-        data.tofile(args.save_bam)
-
-    g = hbam.Gpu(local_rank)
-    g.load(data)
+    def all_gather(obj):
+        if dist is None:
+            return [obj]
+        out = [None] * world
+        dist.all_gather_object(out, obj)
+        return out
 
     def barrier():
+        # hbam calls return after their streams drain; torch's stream is idle
         if dist is not None:
             import torch
             torch.cuda.synchronize()
             dist.barrier()
 
-    for _ in range(args.warmup):
-        st = g.run(timing=True)
-    barrier()
-    stats = []
-    t = time.perf_counter()
-    for _ in range(args.steps):
-        stats.append(g.run(timing=True))
-    barrier()
-    elapsed = time.perf_counter() - t
-    if dist is not None:
-        import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        tot = torch.tensor([float(info["uncompressed"]), float(stats[-1]["records"]), float(info["compressed"])],
-                           dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(tot)
-        u_all, n_all, c_all = (float(x) for x in tot.tolist())
-    else:
-        u_all, n_all, c_all = float(info["uncompressed"]), float(stats[-1]["records"]), float(info["compressed"])
+    import hbam
+    from hbam import shard
 
-    st = stats[-1]
-    assert st["records"] == args.records, (st["records"], args.records)
-    ms_step = elapsed / args.steps * 1e3
-    value = u_all * args.steps / elapsed / 1e9
+    tag = all_gather(f"{os.getpid()}_{int(time.time())}")[0]
+    path = os.path.join(scratch_dir(), f"hbam_bench_{tag}.bam")
+    try:
+        size, u_file = build_shared_bam(path, rank, world, args.records, all_gather, barrier)
+        f = hbam.BamFile(path=path, device=local_rank)
+        first = f.header()["first_record_voff"]
+        split = shard.ShardedBamReader(f, size, first, rank, world, all_gather).split()
+        vs, ve = split if split is not None else (0, 0)
+        lo = vs >> 16
+        hi = min(size, (ve >> 16) + (256 << 10))
+        if split is not None:
+            f.prefetch(lo, hi)  # inputs resident in HBM before the timed region
+        log(f"[rank {rank}] split [{vs:#x}, {ve:#x}) -> bytes [{lo}, {hi}) resident")
 
-    # dominant kernel pair: inflate (phase A huff + phase B lz77), launched as
-    # pairs over chunks of BGZF blocks; HIP events on the pipeline stream.
-    n_launch = max(1, st["inflate_launches"])
-    infl_ms = sum(s_["ms_huff"] + s_["ms_lz77"] for s_ in stats) / len(stats) / n_launch
-    huff_ms = sum(s_["ms_huff"] for s_ in stats) / len(stats) / n_launch
-    lz_ms = sum(s_["ms_lz77"] for s_ in stats) / len(stats) / n_launch
-    alg_bytes = (info["compressed"] + info["uncompressed"]) / n_launch  # C read + U written per launch pair
-    achieved = alg_bytes / (infl_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(("hbam::k_inflate_huff", "hbam::k_inflate_lz77"))
-    out = {
-        "metric": METRIC,
-        "value": round(value, 3),
-        "unit": "GB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_step, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (tools/gen_synth_bam.c, zlib level 5 BGZF, generated on the box)",
-        "config": {"workload": "C2: synthetic 10M x 150bp paired-end coordinate-sorted BAM per GPU",
-                   "records_per_gpu": args.records, "compressed_bytes_per_gpu": info["compressed"],
-                   "uncompressed_bytes_per_gpu": info["uncompressed"], "bgzf_blocks_per_gpu": info["blocks"],
-                   "parallelism": f"bgzf-shard x{world}"},
-        "records_per_s": round(n_all * args.steps / elapsed, 1),
-        "link_fallbacks": int(sum(s_["link_fallbacks"] for s_ in stats)),
-        "link_rewalks": int(sum(s_["link_rewalks"] for s_ in stats)),
-        "stages_ms": {k: round(st[k], 3) for k in ("ms_locate", "ms_inflate", "ms_huff", "ms_lz77", "ms_chain",
-                                                    "ms_decode", "ms_total")},
-        "roofline": {"bound": "hbm", "kernel": "k_inflate_huff+k_inflate_lz77 (one launch pair)",
-                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "launches_per_pass": n_launch, "avg_launch_ms": round(infl_ms, 3),
-                     "huff_avg_launch_ms": round(huff_ms, 3), "lz77_avg_launch_ms": round(lz_ms, 3),
-                     "alg_bytes_per_launch": int(alg_bytes)},
-        "cpu_baseline": None,
-    }
-    if rank == 0 and world == 1:
-        out["io"] = host_and_copy_legs(g, data, info, ms_step)
-    if rank == 0 and world == 1 and not args.no_extra:
-        g.close()
-        out["extra"] = extra_configs(data, info)
-    if rank == 0 and not args.no_cpu_baseline:
-        try:
-            out["cpu_baseline"] = cpu_baseline(data.tobytes(), info, args.cpu_seconds)
-        except Exception as e:  # reported, never substituted for the GPU number
-            out["cpu_baseline"] = {"error": str(e)}
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+        def step(timing=True, digest=False):
+            if split is None:
+                return None
+            return f.decode_span_device(vs, ve, timing=timing, digest=digest)
+
+        for _ in range(args.warmup):
+            step()
+        barrier()
+        stats = []
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            stats.append(step())
+        barrier()
+        elapsed = time.perf_counter() - t
+        check = step(timing=False, digest=True)  # untimed: the digest for the parity check
+        mine = (0, 0, 0, 0, 0) if check is None else (int(check["records"]), int(check["inflated_bytes"]),
+                                                       int(check["compressed_bytes"]), int(check["key_xor"]),
+                                                       int(check["voff_sum"]))
+        if dist is not None:
+            import torch
+            tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
+        parts = all_gather(mine)
+        n_all = sum(p[0] for p in parts)
+        u_all = sum(p[1] for p in parts)
+        kx = 0
+        for p in parts:
+            kx ^= p[3]
+        vsum = sum(p[4] for p in parts) & ALL
+        assert n_all == world * args.records, (n_all, world * args.records)
+
+        st = stats[-1] if stats and stats[-1] is not None else check
+        ms_step = elapsed / args.steps * 1e3
+        value = u_all * args.steps / elapsed / 1e9
+        out = None
+        if rank == 0:
+            # dominant kernel: by its HIP-event time over the timed steps
+            n_launch = max(1, st["inflate_launches"])
+            avg = lambda k: sum(s_[k] for s_ in stats) / len(stats)
+            kt = {"hbam::k_inflate_huff": avg("ms_huff"), "hbam::k_inflate_lz77": avg("ms_lz77")}
+            dom = max(kt, key=kt.get)
+            dom_ms = kt[dom]
+            b_alg = st["compressed_bytes"] + st["inflated_bytes"] + SOA_BYTES_PER_RECORD * st["records"]
+            achieved = b_alg / (dom_ms * 1e-3) / 1e9
+            out = {
+                "metric": METRIC,
+                "value": round(value, 3),
+                "unit": "GB/s",
+                "n_gpus": world,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": round(ms_step, 3),
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": "u8",
+                "data": "synthetic (tools/gen_synth_bam.c: Illumina-like qualities, zlib level 5 BGZF), "
+                        "generated on the box",
+                "config": {"workload": ("C2: synthetic 10M x 150bp paired-end coordinate-sorted BAM" if world == 1
+                                        else f"C3-shaped: one BAM of {world} x C2 records split by BGZF ranges"),
+                           "records_per_gpu": args.records, "file_bytes": size, "uncompressed_bytes": u_file,
+                           "split_bytes_rank0": hi - lo,
+                           "parallelism": f"FileVirtualSplit per rank x{world} (BAMSplitGuesser)"},
+                "records_per_s": round(n_all * args.steps / elapsed, 1),
+                "parity": {"records": n_all, "key_xor": f"{kx:#018x}", "voff_sum": f"{vsum:#018x}"},
+                "link_fallbacks": int(sum(s_["link_fallbacks"] for s_ in stats)),
+                "link_rewalks": int(sum(s_["link_rewalks"] for s_ in stats)),
+                "stages_ms": {k: round(st[k], 3) for k in ("ms_locate", "ms_inflate", "ms_huff", "ms_lz77",
+                                                            "ms_chain", "ms_decode", "ms_total")},
+                "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                             "launches_per_pass": n_launch, "avg_launch_ms": round(dom_ms / n_launch, 4),
+                             "alg_bytes_per_launch": int(b_alg / n_launch),
+                             "alg_bytes_rule": "(C + U + 37 N) of the pass / launches (SURVEY 8d)",
+                             "kernel_ms_per_pass": {k: round(v, 3) for k, v in kt.items()},
+                             "whole_pass": {"achieved": round(b_alg / (st["ms_total"] * 1e-3) / 1e9, 2),
+                                            "frac": round(b_alg / (st["ms_total"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                                          5)}},
+                "cpu_baseline": None,
+            }
+        f.close()
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            try:
+                cb, full = cpu_baseline(path, size, args.cpu_seconds)
+                out["cpu_baseline"] = cb
+                out["parity"]["matches_oracle"] = bool(full["records"] == n_all and full["key_xor"] == kx
+                                                       and full["voff_sum"] == vsum)
+            except Exception as e:  # reported, never substituted for the GPU number
+                out["cpu_baseline"] = {"error": repr(e)}
+        if rank == 0 and world == 1 and not args.no_pmc:
+            try:
+                tr = pmc_traffic(path, vs, ve, out["roofline"]["kernel"])
+                if tr and "bytes_per_launch" in tr:
+                    out["roofline"]["traffic"] = tr["bytes_per_launch"]
+                    out["roofline"]["traffic_detail"] = dict(tr, source="rocprofv3 --pmc child runs, this session")
+                elif tr:
+                    out["roofline"]["traffic_error"] = tr["error"]
+            except Exception as e:
+                out["roofline"]["traffic_error"] = repr(e)
+        if rank == 0 and world == 1 and not args.no_extra:
+            extra = {}
+            for name, fn in (("dropin_end_to_end", lambda: dropin_leg(path, first, n_all)),
+                             ("write_path", lambda: write_legs(path, size, u_file)),
+                             ("c4_long_reads", long_read_leg),
+                             ("c3_c5_60GB", lambda: c3_c5_leg(args.c3_gb, host_cores()) if args.c3_gb > 0 else None)):
+                t = time.time()
+                try:
+                    extra[name] = fn()
+                except Exception as e:
+                    extra[name] = {"error": repr(e)}
+                log(f"[extra] {name} {time.time() - t:.1f}s")
+            out["extra"] = extra
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+    finally:
+        barrier()
+        if rank == 0:
+            try:
+                os.unlink(path)
+            except OSError:
+                pass
     if dist is not None:
         dist.destroy_process_group()
 

@@ -404,6 +404,25 @@ class BamFile:
                 return
             v = r["next_voff"]
 
+    def scan_batches(self, vstart, vend, max_records):
+        """The split through hbam_decode_span in bounded batches, as a JNI
+        caller iterates it, leaving each batch in the library's pinned host
+        columns (no Python copies): (records, batches, rest bytes)."""
+        b = Batch()
+        v, n, k, nbytes = vstart, 0, 0, 0
+        while v < vend:
+            rc = _L.hbam_decode_span(self._h, v, vend, max_records, C.byref(b))
+            if rc != OK:
+                raise self._err(rc)
+            if b.n == 0:
+                break
+            n += b.n
+            k += 1
+            nbytes += b.data_len
+            v = b.next_voff
+        self._last_n = b.n
+        return n, k, nbytes
+
     def encode_writables(self):
         """SAMRecordWritable.write of every record of the last decode_span
         (GPU): (bytes, offsets[n+1])."""
