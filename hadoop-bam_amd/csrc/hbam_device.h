@@ -41,8 +41,15 @@ static_assert(sizeof(BlockInfo) == 32, "BlockInfo is 32 bytes");
 // Per-block result of inflate phase A.
 struct HuffOut {
   uint32_t ntok;
-  int32_t status;
+  int32_t status;       // kOk, an error code, or kHuffPending between rounds
+  uint32_t resume_bit;  // kHuffPending: the next DEFLATE block header (bit, relative to the 16 B-aligned cdata base)
+  uint32_t outpos;      // kHuffPending: bytes inflated so far
 };
+// Phase A runs in rounds: a block whose next DEFLATE block needs a header
+// stops there (kHuffPending); the next round's k_huff_tables parses that
+// header at high occupancy and the decode resumes with the tables prebuilt.
+constexpr int32_t kHuffPending = -2;
+constexpr uint32_t kInflateRounds = 4;  // zlib: <= 4 DEFLATE blocks of 16383 symbols per 64 KiB BGZF block
 
 // Phase-A table prebuild (k_huff_tables -> k_inflate_huff), per block of a chunk.
 constexpr uint32_t kHuffTableImage = 11008;  // bytes of the LDS table image
@@ -50,7 +57,7 @@ struct HuffTableInfo {
   uint32_t status;     // 0: tables + B0 valid; else decode the block's headers inline
   uint32_t B0;         // bit of the first symbol (relative to the 16 B-aligned cdata base)
   uint32_t final_blk;  // BFINAL of the first DEFLATE block
-  uint32_t pad;
+  uint32_t est_bits;   // expected compressed bits of that block (block_bits_estimate)
 };
 
 // Record-chain transition rules.

@@ -259,6 +259,8 @@ struct HuffLds {
   uint8_t cl_lens[20];
 };
 constexpr uint32_t kTableImage = offsetof(HuffLds, offs);
+// dyn_header_par's per-lane symbol scratch (ClLds) may alias lit[]: the
+// litlen table is built only after the code lengths are decoded
 static_assert(kTableImage % 16 == 0, "table image is copied in 16 B units");
 static_assert(kTableImage == kHuffTableImage, "hbam_device.h kHuffTableImage must match HuffLds");
 
@@ -846,6 +848,57 @@ __device__ __forceinline__ int dyn_header(HuffLds& L, SReader& R, uint32_t E) {
   return DH_OK;
 }
 
+// Expected compressed bits of a non-final DEFLATE block, from its code
+// lengths (symbol probabilities taken as 2^-length): zlib ends a block after
+// lit_bufsize - 1 = 16383 symbols (deflate.c _tr_tally at the default
+// memLevel 8), literals and length/distance pairs alike.  It sizes the first
+// all-lane pass over the block, so that the slices do not reach far into the
+// next block (decoded there with the wrong tables and thrown away); only the
+// speed depends on it -- a short guess continues with another pass.  All 64
+// lanes of a wave call it; lens[0..hlit) litlen, lens[hlit..hlit+hdist) dist.
+constexpr uint32_t kZlibBlockSymbols = 16383;
+__device__ uint32_t block_bits_estimate(const uint8_t* lens, uint32_t hlit, uint32_t hdist) {
+  const uint32_t lane = lane_id();
+  float wl = 0.f, al = 0.f, wlen = 0.f, wd = 0.f, ad = 0.f;
+  for (uint32_t s = lane; s < hlit; s += 64) {
+    const uint32_t l = lens[s];
+    if (l == 0 || s == 256) continue;
+    const float w = ldexpf(1.0f, -(int)l);
+    wl += w;
+    if (s < 256) {
+      al += w * (float)l;
+    } else if (s < 286) {
+      al += w * (float)(l + kLenExtra[s - 257]);
+      wlen += w;
+    }
+  }
+  for (uint32_t d = lane; d < hdist && d < 30; d += 64) {
+    const uint32_t l = lens[hlit + d];
+    if (l == 0) continue;
+    const float w = ldexpf(1.0f, -(int)l);
+    wd += w;
+    ad += w * (float)(l + kDistExtra[d]);
+  }
+#pragma unroll
+  for (int k = 32; k > 0; k >>= 1) {
+    wl += __shfl_xor(wl, k, 64);
+    al += __shfl_xor(al, k, 64);
+    wlen += __shfl_xor(wlen, k, 64);
+    wd += __shfl_xor(wd, k, 64);
+    ad += __shfl_xor(ad, k, 64);
+  }
+  const float edist = wd > 0.f ? ad / wd : 0.f;
+  const float per_sym = wl > 0.f ? (al + wlen * edist) / wl : 8.f;
+  return rfl((uint32_t)fminf((float)kZlibBlockSymbols * per_sym, 1e9f));
+}
+// End of the first all-lane pass over a DEFLATE block whose symbols start at
+// bit b0: an eighth over the estimate (a final block runs to the end).
+__device__ __forceinline__ uint32_t pass_end(uint32_t b0, uint32_t est, bool final_blk, uint32_t E) {
+  if (final_blk || est == 0) return E;
+  const uint64_t e = (uint64_t)b0 + est + (est >> 3) + 1024;
+  return e < E ? (uint32_t)e : E;
+}
+
 // Dynamic header with the code-length symbols decoded by all 64 lanes of the
 // wave (k_huff_tables): lane l speculatively decodes the kClSlice bits from
 // p + l*kClSlice of a window, a sync loop restarts slices from their
@@ -860,6 +913,7 @@ constexpr uint32_t kClMaxSym = kClSlice;  // a slice holds at most one symbol pe
 struct ClLds {
   uint16_t ent[64][kClMaxSym];  // sym | extra << 5 | bits << 12
 };
+static_assert(sizeof(ClLds) <= sizeof(HuffLds::lit), "ClLds aliases HuffLds::lit in k_inflate_huff");
 
 __device__ __forceinline__ uint32_t peek32(const uint32_t* W, uint32_t p) {
   return __builtin_amdgcn_alignbit(W[(p >> 5) + 1], W[p >> 5], p & 31);
@@ -995,10 +1049,14 @@ __device__ int dyn_header_par(HuffLds& L, ClLds& C, const uint32_t* __restrict__
 // bit B0; anything else (stored / fixed block, malformed or long header) is
 // left to k_inflate_huff's inline path, which owns the error semantics.
 constexpr uint32_t kTabStageBytes = 1024;
+// Round 0 parses the header at the start of the block; later rounds the one
+// where the previous decode round stopped (hout kHuffPending); blocks with
+// nothing pending get status 2.
 __global__ __launch_bounds__(64) void k_huff_tables(const uint8_t* __restrict__ file,
                                                     const BlockInfo* __restrict__ blocks, uint32_t b0,
                                                     uint8_t* __restrict__ tables,
-                                                    HuffTableInfo* __restrict__ tinfo) {
+                                                    HuffTableInfo* __restrict__ tinfo,
+                                                    const HuffOut* __restrict__ hout, uint32_t round) {
   __shared__ __attribute__((aligned(16))) HuffLds L;
   __shared__ __attribute__((aligned(16))) uint4 s_in[kTabStageBytes / 16 + 1];
   __shared__ ClLds C;
@@ -1006,29 +1064,43 @@ __global__ __launch_bounds__(64) void k_huff_tables(const uint8_t* __restrict__ 
   const uint32_t bi = b0 + blockIdx.x;
   const BlockInfo blk = blocks[bi];
   HuffTableInfo ti{1u, 0u, 0u, 0u};
-  if (blk.isize != 0) {
-    const uint64_t sbyte = blk.coff + 18;
-    const uint64_t abase = sbyte & ~15ull;
-    const uint32_t nreal = min((uint32_t)((blk.coff + blk.csize - abase + 15) >> 4), kTabStageBytes / 16);
-    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(file + abase);
+  const uint64_t sbyte = blk.coff + 18;
+  const uint64_t abase = sbyte & ~15ull;
+  uint32_t hbit = 8u * (uint32_t)(sbyte - abase);  // the header, relative to abase
+  bool todo = blk.isize != 0;
+  if (round > 0) {
+    const HuffOut ho = hout[bi];
+    todo = todo && ho.status == kHuffPending;
+    hbit = ho.resume_bit;
+    if (!todo) ti.status = 2u;
+  }
+  if (todo) {
+    // stage 1 KiB from the 16 B unit holding the header
+    const uint32_t sb = (hbit >> 3) & ~15u;
+    const uint32_t cend = (uint32_t)(blk.coff + blk.csize - abase);  // block end, relative to abase
+    const uint32_t nreal = min((cend - sb + 15) >> 4, kTabStageBytes / 16);
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(file + abase + sb);
     for (uint32_t i = lane; i <= nreal; i += 64) s_in[i] = src[i];  // +1 pad chunk (file is padded)
     wave_sync();
     SReader R;
     R.W = reinterpret_cast<const uint32_t*>(s_in);
-    const uint32_t Ereal = 8u * ((uint32_t)(sbyte - abase) + (blk.csize - 26));
+    const uint32_t Ereal = 8u * ((uint32_t)(sbyte - abase) + (blk.csize - 26)) - 8u * sb;
     const uint32_t E = min(Ereal, 128u * nreal);
-    R.seek(8u * (uint32_t)(sbyte - abase));
+    R.seek(hbit - 8u * sb);
     R.fill();
     if (R.pos() + 3 <= E && (((uint32_t)R.buf >> 1) & 3u) == 2u) {
       const uint32_t fin = (uint32_t)R.buf & 1u;
       R.consume(3);
       uint32_t b0pos = 0;
-      if (dyn_header_par(L, C, R.W, R.pos(), E, &b0pos) == DH_OK) {
+      const uint32_t hp = R.pos();
+      if (dyn_header_par(L, C, R.W, hp, E, &b0pos) == DH_OK) {
         wave_sync();
+        const uint32_t h = rfl(peek32(R.W, hp));
+        const uint32_t est = block_bits_estimate(L.lens, (h & 31) + 257, ((h >> 5) & 31) + 1);
         uint4* __restrict__ dst = reinterpret_cast<uint4*>(tables + (uint64_t)blockIdx.x * kTableImage);
         const uint4* img = reinterpret_cast<const uint4*>(&L);
         for (uint32_t i = lane; i < kTableImage / 16; i += 64) dst[i] = img[i];
-        ti = HuffTableInfo{0u, b0pos, fin, 0u};
+        ti = HuffTableInfo{0u, b0pos + 8u * sb, fin, est};
       }
     }
   }
@@ -1039,6 +1111,7 @@ __global__ __launch_bounds__(64) void k_huff_tables(const uint8_t* __restrict__ 
 struct HuffCtl {
   uint32_t act;                 // kActDecode / kActDone
   uint32_t B0, out0, tok0;      // all-lane pass: first symbol bit, output / token position
+  uint32_t Bend;                // its region end (pass_end; E for a final block)
   uint32_t fe, fx, ftok, fbytes, m3any;  // its result
   uint32_t xx[kHuffWaves], xe[kHuffWaves];  // exit / event of each wave's last lane
   uint32_t red[2 * kHuffWaves];
@@ -1048,14 +1121,15 @@ constexpr uint32_t kHuffLdsBytes = (sizeof(HuffLds) + 15) & ~15u;
 constexpr uint32_t kHuffCtlBytes = (sizeof(HuffCtl) + 15) & ~15u;
 constexpr uint32_t kHuffStaticBytes = kHuffLdsBytes + kHuffCtlBytes;
 
-constexpr int kHuffWavesPerSimd = 5;  // VGPR cap 96; measured best on C2
+constexpr int kHuffWavesPerSimd = 4;  // VGPR cap 128 (no spills); LDS admits 4 staged workgroups per CU
 template <bool STAGE>
 __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huff(const uint8_t* __restrict__ file,
                                                                const BlockInfo* __restrict__ blocks, uint32_t b0,
                                                                uint64_t chunk_ustart, uint32_t* __restrict__ tokens,
                                                                HuffOut* __restrict__ hout,
                                                                const uint8_t* __restrict__ tables,
-                                                               const HuffTableInfo* __restrict__ tinfo) {
+                                                               const HuffTableInfo* __restrict__ tinfo,
+                                                               uint32_t round, uint32_t defer) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   HuffLds& L = *reinterpret_cast<HuffLds*>(smem);
   HuffCtl& C = *reinterpret_cast<HuffCtl*>(smem + kHuffLdsBytes);
@@ -1065,8 +1139,13 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
   const BlockInfo blk = blocks[bi];
   const uint32_t isize = blk.isize;
   if (isize == 0) {  // inflate(buf,off,0) returns 0 without reading: nothing to validate
-    if (tid == 0) { hout[bi].ntok = 0; hout[bi].status = kOk; }
+    if (tid == 0 && round == 0) { hout[bi].ntok = 0; hout[bi].status = kOk; }
     return;
+  }
+  HuffOut h0{0u, kOk, 0u, 0u};
+  if (round > 0) {  // only blocks a previous round left pending
+    h0 = hout[bi];
+    if (h0.status != kHuffPending) return;
   }
   uint32_t* tok_out = tokens + (blk.ustart - chunk_ustart);
   const uint64_t sbyte = blk.coff + 18;  // cdata start
@@ -1110,12 +1189,15 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
   R.buf = 0;
   R.cnt = R.wd = 0;
 
-  uint32_t outpos = 0, ntok = 0;
+  uint32_t outpos = h0.outpos, ntok = h0.ntok;
+  bool pending = false;  // stopped before the next DEFLATE block's header (defer)
+  uint32_t resume_bit = 0;
   int err = kOk;
   bool look = false;       // output exactly full: zlib's lookahead
   bool final_blk = false;  // BFINAL of the current DEFLATE block
   bool resume = false;     // an all-lane pass result waits in C
   bool pre = ti.status == 0;  // first DEFLATE block's header + tables come from k_huff_tables
+  uint32_t est = 0, bend = E;  // wave 0: the current block's size estimate, the pass region end
 
   // zlib's lookahead once the output is exactly full: decode on until a
   // symbol needs room; returns true when it ends at a (non-final) EOB so the
@@ -1155,7 +1237,7 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
     }
   };
 
-  if (wave == 0) R.seek(8u * (uint32_t)(sbyte - abase));
+  if (wave == 0) R.seek(round > 0 ? h0.resume_bit : 8u * (uint32_t)(sbyte - abase));
   for (;;) {
     if (wave == 0) {
       uint32_t act = kActDone;
@@ -1166,6 +1248,20 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
           const uint32_t fe = rfl(C.fe), fxs = rfl(C.fx), m3any = rfl(C.m3any);
           ntok = rfl(ntok + C.ftok);
           outpos = rfl(outpos + C.fbytes);
+          if (!m3any && bend < E && fxs < E && outpos < isize) {
+            // the pass ended at its region end inside the block: go on with
+            // the same tables over the next stretch
+            bend = min(E, fxs + (est >> 2) + 4096u);
+            if (lane == 0) {
+              C.B0 = fxs;
+              C.Bend = bend;
+              C.out0 = outpos;
+              C.tok0 = ntok;
+            }
+            act = kActDecode;
+            resume = true;
+            break;
+          }
           if (!m3any) {  // walked to the end of CDATA without an end-of-block
             if (outpos < isize) err = kErrFormat;
             else if (outpos == isize) { look = true; R.seek(fxs); }
@@ -1175,6 +1271,11 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
           } else if (fe == EV_EOB) {
             R.seek(fxs);
             if (final_blk) { err = kErrFormat; break; }  // EOB before ISIZE bytes
+            if (defer) {  // the next header is the next round's (k_huff_tables)
+              pending = true;
+              resume_bit = fxs;
+              break;
+            }
             continue;
           } else if (fe == EV_FULLX) {
             look = true;
@@ -1190,10 +1291,13 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
           pre = false;
           final_blk = ti.final_blk != 0;
           R.seek(ti.B0);
+          est = ti.est_bits;
+          bend = pass_end(ti.B0, est, final_blk, E);
           if (lane == 0) {
             C.B0 = ti.B0;
-            C.out0 = 0;
-            C.tok0 = 0;
+            C.Bend = bend;
+            C.out0 = outpos;
+            C.tok0 = ntok;
           }
           act = kActDecode;
           resume = true;
@@ -1237,6 +1341,7 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
             continue;
           }
           if (type == 3) { err = kErrIO; break; }
+          const uint32_t hp = R.pos();
           if (type == 1) {  // fixed Huffman
             for (int s = lane; s < 320; s += 64) {
               uint8_t l;
@@ -1251,13 +1356,24 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
               break;
             }
             pair_literals(L);
-          } else {  // dynamic Huffman
-            const int dh = dyn_header(L, R, E);
-            if (dh == DH_TRUNC) { if (!look) err = kErrFormat; break; }
-            if (dh != DH_OK) { err = kErrIO; break; }
+            est = block_bits_estimate(L.lens, 288, 32);
+          } else {  // dynamic Huffman: code lengths decoded by the 64 lanes of the wave
+            uint32_t endp = 0;
+            int dh = dyn_header_par(L, *reinterpret_cast<ClLds*>(L.lit), W, R.pos(), E, &endp);
+            if (rfl(dh) == DH_OK) {
+              R.seek(endp);
+            } else {  // an anomaly: the serial parse owns zlib's error semantics
+              dh = dyn_header(L, R, E);
+              if (dh == DH_TRUNC) { if (!look) err = kErrFormat; break; }
+              if (dh != DH_OK) { err = kErrIO; break; }
+            }
+            const uint32_t h = rfl(peek32(W, hp));
+            est = block_bits_estimate(L.lens, (h & 31) + 257, ((h >> 5) & 31) + 1);
           }
           if (!look) {  // hand the symbol stream to the workgroup
+            bend = pass_end(R.pos(), est, final_blk, E);
             if (lane == 0) {
+              C.Bend = bend;
               C.B0 = R.pos();
               C.out0 = outpos;
               C.tok0 = ntok;
@@ -1278,11 +1394,11 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
     if (C.act != kActDecode) break;
 
     // ---- all-lane decode of this DEFLATE block's symbols
-    const uint32_t B0 = C.B0, out0 = C.out0, tok0 = C.tok0;
-    const uint32_t R = E > B0 ? E - B0 : 0u;
+    const uint32_t B0 = C.B0, out0 = C.out0, tok0 = C.tok0, Bend = C.Bend;
+    const uint32_t R = Bend > B0 ? Bend - B0 : 0u;
     const uint32_t S = (R + kHuffThreads - 1) / kHuffThreads;
-    uint32_t a = min(B0 + tid * S, E);
-    const uint32_t stop = tid == kHuffThreads - 1 ? E : min(B0 + (tid + 1) * S, E);
+    uint32_t a = min(B0 + tid * S, Bend);
+    const uint32_t stop = tid == kHuffThreads - 1 ? Bend : min(B0 + (tid + 1) * S, Bend);
     MergePts mp;
     uint32_t mj = 0, x, nt, nb;
     uint32_t ev = lane_decode<LD_SPEC>(L, W, a, stop, E, x, nt, nb, mp, mj, nullptr, 0, 0);
@@ -1338,9 +1454,12 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
     __syncthreads();
   }
   if (tid == 0) {
-    if (err == kOk && outpos < isize) err = kErrFormat;  // "Did not inflate expected amount"
-    hout[bi].ntok = ntok;
-    hout[bi].status = err;
+    if (wave == 0 && pending && err == kOk) {
+      hout[bi] = HuffOut{ntok, kHuffPending, resume_bit, outpos};
+    } else {
+      if (err == kOk && outpos < isize) err = kErrFormat;  // "Did not inflate expected amount"
+      hout[bi] = HuffOut{ntok, err, 0u, outpos};
+    }
   }
 }
 
@@ -2756,16 +2875,18 @@ hipError_t scan_u32_to_u64(void* tmp, size_t* tmp_bytes, const uint32_t* in, uin
 }
 
 hipError_t launch_huff_tables(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                              uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s) {
+                              uint8_t* tables, HuffTableInfo* tinfo, const HuffOut* hout, uint32_t round,
+                              hipStream_t s) {
   if (nb == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_huff_tables, dim3(nb), dim3(64), 0, s, file, blocks, b0, tables, tinfo);
+  hipLaunchKernelGGL(k_huff_tables, dim3(nb), dim3(64), 0, s, file, blocks, b0, tables, tinfo, hout, round);
   return hipGetLastError();
 }
 // phase A proper; the chunk's tables must be built (launch_huff_tables).
 // max_stage = largest staged span of the chunk's blocks (huff_stage_bytes)
 hipError_t launch_inflate_huff_prebuilt(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
                                         uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
-                                        const uint8_t* tables, const HuffTableInfo* tinfo, hipStream_t s) {
+                                        const uint8_t* tables, const HuffTableInfo* tinfo, uint32_t round,
+                                        uint32_t defer, hipStream_t s) {
   if (nb == 0) return hipSuccess;
   static bool attr_set = false;
   if (!attr_set) {
@@ -2777,10 +2898,10 @@ hipError_t launch_inflate_huff_prebuilt(const uint8_t* file, const BlockInfo* bl
   const uint32_t staged_lds = kHuffStaticBytes + ((max_stage + 15) & ~15u);
   if (staged_lds <= kHuffStageMaxLds)
     hipLaunchKernelGGL(k_inflate_huff<true>, dim3(nb), dim3(kHuffThreads), staged_lds, s, file, blocks, b0,
-                       chunk_ustart, tokens, hout, tables, tinfo);
+                       chunk_ustart, tokens, hout, tables, tinfo, round, defer);
   else
     hipLaunchKernelGGL(k_inflate_huff<false>, dim3(nb), dim3(kHuffThreads), kHuffStaticBytes, s, file, blocks, b0,
-                       chunk_ustart, tokens, hout, tables, tinfo);
+                       chunk_ustart, tokens, hout, tables, tinfo, round, defer);
   return hipGetLastError();
 }
 hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb, uint64_t chunk_ustart,

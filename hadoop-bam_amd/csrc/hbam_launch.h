@@ -67,11 +67,17 @@ hipError_t scan_u32_to_u64(void* tmp, size_t* tmp_bytes, const uint32_t* in, uin
                            hipStream_t s);
 // inflate phase A in two launches: the first DEFLATE block's header + tables
 // of every block of a chunk (k_huff_tables), then the decode reading them
+// (round 0: the header at each block's start; round r > 0: where decode
+// round r-1 left the block kHuffPending)
 hipError_t launch_huff_tables(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                              uint8_t* tables, HuffTableInfo* tinfo, hipStream_t s);
+                              uint8_t* tables, HuffTableInfo* tinfo, const HuffOut* hout, uint32_t round,
+                              hipStream_t s);
+// (defer: stop a block before its next DEFLATE header, kHuffPending, for
+// the next round; the last round decodes every remaining header inline)
 hipError_t launch_inflate_huff_prebuilt(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
                                         uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
-                                        const uint8_t* tables, const HuffTableInfo* tinfo, hipStream_t s);
+                                        const uint8_t* tables, const HuffTableInfo* tinfo, uint32_t round,
+                                        uint32_t defer, hipStream_t s);
 // LDS bytes phase A stages for a block: its cdata from the 16 B-aligned start,
 // footer included, plus one 16 B pad (must match k_inflate_huff).
 inline uint32_t huff_stage_bytes(const BlockInfo& b) {

@@ -429,11 +429,19 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
     // tables of chunk j on stream_t_ (they overlap phase A of chunk j-1; the
     // parity buffer is free once phase A of chunk j-2 is done)
     if (j >= 2) HIPCHK(hipStreamWaitEvent(stream_t_, hdone_ev_[par], 0));
-    HIPCHK(launch_huff_tables(fbase, dblocks_.p, cb, ce - cb, tables_[par].p, tinfo_[par].p, stream_t_));
+    HIPCHK(launch_huff_tables(fbase, dblocks_.p, cb, ce - cb, tables_[par].p, tinfo_[par].p, hout_.p, 0, stream_t_));
     HIPCHK(hipEventRecord(tab_ev_[par], stream_t_));
     HIPCHK(hipStreamWaitEvent(stream_, tab_ev_[par], 0));
-    HIPCHK(launch_inflate_huff_prebuilt(fbase, dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, max_stage,
-                                        tables_[par].p, tinfo_[par].p, stream_));
+    // rounds: each decode stops a block before its next DEFLATE header, which
+    // the next round's table build parses (the last round decodes inline)
+    for (uint32_t r = 0; r < kInflateRounds; ++r) {
+      if (r > 0)
+        HIPCHK(launch_huff_tables(fbase, dblocks_.p, cb, ce - cb, tables_[par].p, tinfo_[par].p, hout_.p, r,
+                                  stream_));
+      HIPCHK(launch_inflate_huff_prebuilt(fbase, dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, max_stage,
+                                          tables_[par].p, tinfo_[par].p, r, r + 1 < kInflateRounds ? 1u : 0u,
+                                          stream_));
+    }
     HIPCHK(hipEventRecord(hdone_ev_[par], stream_));
     if (timing) HIPCHK(hipEventRecord(tev_[3 * j + 1], stream_));
     HIPCHK(hipEventRecord(sync_ev_[par], stream_));
