@@ -549,6 +549,12 @@ int hbam_guess_bgzf_block_starts(hbam_ctx* ctx, const uint64_t* begs, const uint
 
 int hbam_get_splits(hbam_ctx* ctx, const uint64_t* starts, const uint64_t* lengths, uint64_t n, const uint8_t* sbi,
                     uint64_t sbi_len, uint64_t* vstarts, uint64_t* vends, uint64_t* nout) {
+  return hbam_get_splits_bai(ctx, starts, lengths, n, sbi, sbi_len, nullptr, 0, vstarts, vends, nout);
+}
+
+int hbam_get_splits_bai(hbam_ctx* ctx, const uint64_t* starts, const uint64_t* lengths, uint64_t n,
+                        const uint8_t* sbi, uint64_t sbi_len, const uint8_t* bai, uint64_t bai_len, uint64_t* vstarts,
+                        uint64_t* vends, uint64_t* nout) {
   *nout = 0;
   if (!ctx || !ctx->f) return HBAM_E_STATE;
   ctx->cursor.reset();
@@ -559,7 +565,7 @@ int hbam_get_splits(hbam_ctx* ctx, const uint64_t* starts, const uint64_t* lengt
     sp[i].length = lengths[i];
   }
   std::vector<FileVirtualSplit> out;
-  int rc = BAMInputFormat::getSplits(*ctx->f, sp, sbi, sbi_len, &out);
+  int rc = BAMInputFormat::getSplits(*ctx->f, sp, sbi, sbi_len, &out, bai, bai_len);
   if (rc != HBAM_OK) {
     ctx->err = ctx->f->error();
     return rc;

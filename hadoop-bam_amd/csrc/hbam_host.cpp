@@ -651,8 +651,153 @@ int BAMInputFormat::addProbabilisticSplits(BamFile& f, const std::vector<FileSpl
   return kOk;
 }
 
+// ---------------------------------------------------------------------------
+// BAI split calculator
+// ---------------------------------------------------------------------------
+int LinearBAMIndex::read(const uint8_t* d, uint64_t len, std::string* err) {
+  lin_.clear();
+  uint64_t p = 0;
+  auto need = [&](uint64_t k) { return p + k <= len; };
+  auto i32 = [&]() {
+    const int32_t v = rd_i32(d + p);
+    p += 4;
+    return v;
+  };
+  if (!need(8) || memcmp(d, "BAI\1", 4) != 0) {
+    *err = "Invalid file header in BAM index";
+    return kErrIO;
+  }
+  p = 4;
+  const int32_t n_ref = i32();
+  if (n_ref < 0) {
+    *err = "Invalid BAM index: negative reference count";
+    return kErrIO;
+  }
+  lin_.resize((size_t)n_ref);
+  for (int32_t r = 0; r < n_ref; ++r) {
+    if (!need(4)) { *err = "Premature end of BAM index"; return kErrIO; }
+    const int32_t n_bin = i32();
+    for (int32_t b = 0; b < n_bin; ++b) {
+      if (!need(8)) { *err = "Premature end of BAM index"; return kErrIO; }
+      p += 4;
+      const int32_t n_chunk = i32();
+      if (n_chunk < 0 || !need(16ull * (uint64_t)n_chunk)) { *err = "Premature end of BAM index"; return kErrIO; }
+      p += 16ull * (uint64_t)n_chunk;
+    }
+    if (!need(4)) { *err = "Premature end of BAM index"; return kErrIO; }
+    const int32_t n_intv = i32();
+    if (n_intv < 0 || !need(8ull * (uint64_t)n_intv)) { *err = "Premature end of BAM index"; return kErrIO; }
+    if (n_bin > 0) {
+      auto& v = lin_[(size_t)r];
+      v.resize((size_t)n_intv);
+      for (int32_t k = 0; k < n_intv; ++k) memcpy(&v[(size_t)k], d + p + 8ull * (uint64_t)k, 8);
+    }
+    p += 8ull * (uint64_t)n_intv;
+  }
+  return kOk;
+}
+
+// BAMInputFormat.addBAISplits (BAMInputFormat.java:322-465), for the
+// FileSplits of one file in order.  Quirks kept: a contig's last linear
+// entry is stepped over (`bin + 1 >= ctgBins` advances first), the last
+// FileSplit is planned after the loop, and a split that no linear entry
+// starts in gets a guessed start (BAMSplitGuesser, on the GPU) that also
+// ends the split before it.  Where the Java code would throw a
+// NullPointerException (no contig with linear entries, a guessed first
+// split) this returns kErrIO.
+int BAMInputFormat::addBAISplits(BamFile& f, const std::vector<FileSplit>& splits, const LinearBAMIndex& idx,
+                                 std::vector<FileVirtualSplit>* out) {
+  const int32_t dict = f.n_ref();
+  const size_t n = splits.size();
+  size_t splitsEnd = 0;
+  int32_t ctgIdx = -1;
+  uint32_t bin = 0;
+  const std::vector<uint64_t>* linIdx = nullptr;
+  size_t ctgBins = 0;
+  auto npe = [&](const char* what) {
+    f.error() = std::string("BAI split calculator: ") + what;
+    return kErrIO;
+  };
+  do {  // :353-357 the first contig with linear entries
+    ++ctgIdx;
+    linIdx = idx.getLinearIndex(ctgIdx);
+    if (!linIdx) return npe("no reference sequence with a linear index");
+    ctgBins = linIdx->size();
+  } while (ctgBins == 0);
+  uint64_t nextStart = (*linIdx)[bin], lastStart = 0;
+  int64_t cur = -1;  // newSplit (index into out)
+  bool lastWasGuessed = false;
+  BAMSplitGuesser guesser(f);
+  while (splitsEnd < n) {  // :363-445
+    const FileSplit& fs = splits[splitsEnd];
+    ++splitsEnd;
+    if (splitsEnd >= n) break;
+    const uint64_t fSplitEnd = (fs.start + fs.length) << 16;
+    lastStart = nextStart;
+    while (nextStart < fSplitEnd && ctgIdx < dict) {  // :380-407
+      if (bin + 1 >= ctgBins) {
+        do {
+          ctgIdx += 1;
+          bin = 0;
+          if (ctgIdx >= dict) break;
+          linIdx = idx.getLinearIndex(ctgIdx);
+          if (!linIdx) return npe("no linear index for a dictionary sequence");
+          ctgBins = linIdx->size();
+        } while (ctgBins == 0);
+      }
+      if (ctgIdx < dict && linIdx->size() > bin) {
+        nextStart = (*linIdx)[bin];
+        bin++;
+      }
+    }
+    FileVirtualSplit v;
+    v.path = fs.path;
+    if (fs.start == 0) {  // :409-418 from the first record
+      v.vStart = f.first_record_voff();
+      v.vEnd = nextStart - 1;
+      out->push_back(v);
+      cur = (int64_t)out->size() - 1;
+    } else if (lastStart != nextStart) {  // :423-431 a linear entry starts in this split
+      if (lastWasGuessed) {
+        (*out)[(size_t)cur].setEndVirtualOffset(lastStart - 1);
+        lastWasGuessed = false;
+      }
+      v.vStart = lastStart;
+      v.vEnd = nextStart - 1;
+      out->push_back(v);
+      cur = (int64_t)out->size() - 1;
+    } else {  // :432-444 guess the start
+      std::vector<uint64_t> b{fs.start}, e{fs.start + fs.length}, g;
+      int rc = guesser.guessNextBAMRecordStarts(b, e, &g);
+      if (rc != kOk) return rc;
+      const uint64_t alignedBeg = g[0];
+      if (cur < 0) return npe("a guessed split with no split before it");
+      (*out)[(size_t)cur].setEndVirtualOffset(alignedBeg - 1);
+      lastStart = alignedBeg;
+      nextStart = alignedBeg;
+      v.vStart = alignedBeg;
+      v.vEnd = alignedBeg + 1;
+      out->push_back(v);
+      cur = (int64_t)out->size() - 1;
+      lastWasGuessed = true;
+    }
+    lastStart = nextStart;
+  }
+  if (splitsEnd == n && n > 0) {  // :447-459 the last split
+    if (lastWasGuessed) (*out)[(size_t)cur].setEndVirtualOffset(lastStart - 1);
+    const FileSplit& fs = splits[splitsEnd - 1];
+    FileVirtualSplit v;
+    v.path = fs.path;
+    v.vStart = lastStart;
+    v.vEnd = (fs.start + fs.length) << 16;
+    out->push_back(v);
+  }
+  return kOk;
+}
+
 int BAMInputFormat::getSplits(BamFile& f, const std::vector<FileSplit>& splits, const uint8_t* sbi,
-                              uint64_t sbi_len, std::vector<FileVirtualSplit>* out) {
+                              uint64_t sbi_len, std::vector<FileVirtualSplit>* out, const uint8_t* bai,
+                              uint64_t bai_len) {
   out->clear();
   if (sbi) {
     SplittingBAMIndex idx;
@@ -662,9 +807,20 @@ int BAMInputFormat::getSplits(BamFile& f, const std::vector<FileSplit>& splits, 
       int rc = addIndexedSplits(f, splits, idx, out, &bad);
       if (rc != kOk) return rc;
       if (!bad) return kOk;
-      out->clear();  // "Index ... was not good. Generating probabilistic splits."
+      out->clear();  // "Index ... was not good. Generating probabilistic splits." (:303-306)
+      return addProbabilisticSplits(f, splits, out);
     }
-    // readIndex IOException: getSplits' catch falls back to probabilistic splits (:245-257)
+  }
+  // no usable .splitting-bai (addIndexedSplits' IOException, :245-257): the
+  // BAI split calculator when enabled and the .bai exists, else probabilistic
+  if (bai) {
+    LinearBAMIndex idx;
+    std::string err;
+    if (idx.read(bai, bai_len, &err) != kOk) {  // htsjdk's parse error is not an IOException: it propagates
+      f.error() = err;
+      return kErrIO;
+    }
+    return addBAISplits(f, splits, idx, out);
   }
   return addProbabilisticSplits(f, splits, out);
 }

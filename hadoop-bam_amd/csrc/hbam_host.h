@@ -242,13 +242,34 @@ int guess_bgzf_batch(BamFile& f, const std::vector<uint64_t>& begs, const std::v
                      std::vector<uint64_t>* out, std::string* err);
 
 // BAMInputFormat split planning (BAMInputFormat.java:222-318, 469-530).
-class BAMInputFormat {
+// The linear index of a .bai (SAM spec 5.2; htsjdk CachingBAMFileIndex as
+// LinearBAMIndex reads it, src/main/java/htsjdk/samtools/LinearBAMIndex.java):
+// per reference its 16 kbp-window virtual offsets; a reference with no bins
+// has none.
+class LinearBAMIndex {
  public:
-  // sbi: bytes of <file>.splitting-bai or nullptr (no index -> probabilistic)
-  static int getSplits(BamFile& f, const std::vector<FileSplit>& splits, const uint8_t* sbi, uint64_t sbi_len,
-                       std::vector<FileVirtualSplit>* out);
+  int read(const uint8_t* d, uint64_t len, std::string* err);
+  // nullptr past the last reference (htsjdk's query returns null there)
+  const std::vector<uint64_t>* getLinearIndex(int32_t ctg) const {
+    return ctg >= 0 && (size_t)ctg < lin_.size() ? &lin_[(size_t)ctg] : nullptr;
+  }
 
  private:
+  std::vector<std::vector<uint64_t>> lin_;
+};
+
+class BAMInputFormat {
+ public:
+  // sbi: bytes of <file>.splitting-bai or nullptr (no index -> probabilistic);
+  // bai: bytes of the file's .bai or nullptr -- with the BAI split calculator
+  // enabled (hadoopbam.bam.enable-bai-splitter) it plans when the
+  // .splitting-bai is absent or bad (BAMInputFormat.java:241-257)
+  static int getSplits(BamFile& f, const std::vector<FileSplit>& splits, const uint8_t* sbi, uint64_t sbi_len,
+                       std::vector<FileVirtualSplit>* out, const uint8_t* bai = nullptr, uint64_t bai_len = 0);
+
+ private:
+  static int addBAISplits(BamFile& f, const std::vector<FileSplit>& splits, const LinearBAMIndex& idx,
+                          std::vector<FileVirtualSplit>* out);
   static int addIndexedSplits(BamFile& f, const std::vector<FileSplit>& splits, const SplittingBAMIndex& idx,
                               std::vector<FileVirtualSplit>* out, bool* bad_index);
   static int addProbabilisticSplits(BamFile& f, const std::vector<FileSplit>& splits,

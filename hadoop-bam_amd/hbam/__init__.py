@@ -92,6 +92,7 @@ _sig("hbam_build_splitting_index", C.c_int, [P, i32, C.POINTER(P), C.POINTER(u64
 _sig("hbam_guess_record_starts", C.c_int, [P, P, P, u64, P])
 _sig("hbam_guess_bgzf_block_starts", C.c_int, [P, P, P, u64, P])
 _sig("hbam_get_splits", C.c_int, [P, P, P, u64, P, u64, P, P, C.POINTER(u64)])
+_sig("hbam_get_splits_bai", C.c_int, [P, P, P, u64, P, u64, P, u64, P, P, C.POINTER(u64)])
 _sig("hbam_blocks", C.c_int, [P, P, P, P, P, u64, C.POINTER(u64)])
 _sig("hbam_read_inflated", C.c_int, [P, u64, u64, P])
 _sig("hbam_get_key0", i64, [i32, i32])
@@ -475,7 +476,11 @@ class BamFile:
             raise self._err(rc)
         return [int(x) for x in out[:n]]
 
-    def get_splits(self, starts, lengths, sbi: bytes = None):
+    def get_splits(self, starts, lengths, sbi: bytes = None, bai: bytes = None):
+        """BAMInputFormat.getSplits for one file's FileSplits: from the
+        .splitting-bai (sbi), else -- with bai given, the BAI split
+        calculator enabled -- from the .bai's linear index, else
+        probabilistic.  [(vStart, vEnd)]."""
         n = len(starts)
         s = np.ascontiguousarray(starts, np.uint64)
         ln = np.ascontiguousarray(lengths, np.uint64)
@@ -483,9 +488,10 @@ class BamFile:
         ve = np.zeros(max(n, 1), np.uint64)
         nout = u64()
         sb = C.create_string_buffer(sbi, len(sbi)) if sbi is not None else None
-        rc = _L.hbam_get_splits(self._h, s.ctypes.data, ln.ctypes.data, n, sb,
-                                len(sbi) if sbi is not None else 0, vs.ctypes.data, ve.ctypes.data,
-                                C.byref(nout))
+        bb = C.create_string_buffer(bai, len(bai)) if bai is not None else None
+        rc = _L.hbam_get_splits_bai(self._h, s.ctypes.data, ln.ctypes.data, n, sb,
+                                    len(sbi) if sbi is not None else 0, bb, len(bai) if bai is not None else 0,
+                                    vs.ctypes.data, ve.ctypes.data, C.byref(nout))
         if rc != OK:
             raise self._err(rc)
         return [(int(vs[i]), int(ve[i])) for i in range(nout.value)]

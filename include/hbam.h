@@ -167,6 +167,14 @@ int hbam_guess_bgzf_block_starts(hbam_ctx *ctx, const uint64_t *begs, const uint
 int hbam_get_splits(hbam_ctx *ctx, const uint64_t *starts, const uint64_t *lengths, uint64_t n,
                     const uint8_t *sbi, uint64_t sbi_len, uint64_t *vstarts, uint64_t *vends,
                     uint64_t *nout);
+/* The same with the BAI split calculator enabled (hadoopbam.bam.enable-bai-splitter,
+ * BAMInputFormat.java:241-257, 322-465): with no usable .splitting-bai, splits
+ * come from the linear index of the file's .bai (bai bytes; NULL: no .bai ->
+ * probabilistic splits), a split no linear entry starts in getting a guessed
+ * start.  At most n splits. */
+int hbam_get_splits_bai(hbam_ctx *ctx, const uint64_t *starts, const uint64_t *lengths, uint64_t n,
+                        const uint8_t *sbi, uint64_t sbi_len, const uint8_t *bai, uint64_t bai_len,
+                        uint64_t *vstarts, uint64_t *vends, uint64_t *nout);
 
 /* ---- SAMRecordWritable codec (map-output serialization for the shuffle) ---- */
 /* SAMRecordWritable.write (SAMRecordWritable.java:55-64) of every record of
