@@ -390,6 +390,9 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the in-session rocprofv3 PMC passes")
     ap.add_argument("--no-extra", action="store_true", help="skip every side leg (drop-in, C3/C5, C4, write)")
     ap.add_argument("--c3-gb", type=float, default=60.0, help="size of the C3/C5 file (0: skip that leg)")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="gloo + --one-device: rehearse the N-rank sequence on a one-GPU box")
+    ap.add_argument("--one-device", action="store_true", help="every rank on device 0 (rehearsal only)")
     ap.add_argument("--pmc-child", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--pmc-span", type=int, nargs=2, default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -401,12 +404,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    device = 0 if args.one_device else local_rank
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(device)
+        dist.init_process_group(args.dist_backend)
 
     def all_gather(obj):
         if dist is None:
@@ -429,7 +433,7 @@ def main():
     path = os.path.join(scratch_dir(), f"hbam_bench_{tag}.bam")
     try:
         size, u_file = build_shared_bam(path, rank, world, args.records, all_gather, barrier)
-        f = hbam.BamFile(path=path, device=local_rank)
+        f = hbam.BamFile(path=path, device=device)
         first = f.header()["first_record_voff"]
         split = shard.ShardedBamReader(f, size, first, rank, world, all_gather).split()
         vs, ve = split if split is not None else (0, 0)
@@ -459,7 +463,8 @@ def main():
                                                        int(check["voff_sum"]))
         if dist is not None:
             import torch
-            tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+            tt = torch.tensor([elapsed], dtype=torch.float64,
+                              device=f"cuda:{device}" if args.dist_backend == "nccl" else "cpu")
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             elapsed = float(tt.item())
         parts = all_gather(mine)

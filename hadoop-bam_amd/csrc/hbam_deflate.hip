@@ -7,8 +7,8 @@
 //                     (levels 1-3) / deflate_slow (4-9) + trees.c restated in hbam_deflate.h (byte-identical
 //                     output), hash chains / symbol buffer / trees in a
 //                     per-lane arena in HBM, cdata into a 64 KiB slot.
-//   k_dfl_crc         one workgroup per block: CRC-32 of the payload
-//                     (per-thread slices combined with x^(8n) mod P).
+//   k_dfl_crc         one 1024-thread workgroup per block: CRC-32 of the
+//                     payload (64-byte parts, slice-by-8, combined pairwise).
 //   k_dfl_frame       one workgroup per block: 18-byte BGZF header, cdata
 //                     (or htsjdk's level-0 fallback: one stored block) and
 //                     the CRC32 / ISIZE footer at the block's file offset.
@@ -35,7 +35,8 @@ constexpr uint32_t kMaxLanes = 65536;  // concurrent arenas (~184 KiB each)
 constexpr uint32_t kCrcPoly = 0xedb88320u;
 constexpr uint32_t kWavesTarget = 5120;  // 5 waves per SIMD (84 VGPRs: occupancy 5; measured best)
 
-__device__ inline uint32_t crc_mul(uint32_t a, uint32_t b) {
+__device__ inline uint32_t crc_mul(uint32_t a, uint32_t b) {  // a * b mod P (reflected)
+  if (a == 0) return 0;
   uint32_t m = 1u << 31, p = 0;
   for (;;) {
     if (a & m) {
@@ -44,17 +45,6 @@ __device__ inline uint32_t crc_mul(uint32_t a, uint32_t b) {
     }
     m >>= 1;
     b = (b & 1) ? (b >> 1) ^ kCrcPoly : b >> 1;
-  }
-  return p;
-}
-
-__device__ inline uint32_t crc_x8n(uint64_t n) {  // x^(8n) mod P (zlib x2nmodp(n, 3))
-  uint32_t p = 1u << 31, x2n = 1u << 30;
-  for (int k = 0; k < 3; ++k) x2n = crc_mul(x2n, x2n);
-  while (n) {
-    if (n & 1) p = crc_mul(x2n, p);
-    n >>= 1;
-    x2n = crc_mul(x2n, x2n);
   }
   return p;
 }
@@ -88,46 +78,85 @@ __global__ __launch_bounds__(64) void k_deflate_blocks(const uint8_t* __restrict
   ovf[b] = o ? 1 : 0;
 }
 
-__global__ __launch_bounds__(256) void k_dfl_crc(const uint8_t* __restrict__ in, const uint64_t* __restrict__ ustart,
-                                                 const uint32_t* __restrict__ lens, uint32_t* __restrict__ crc) {
-  __shared__ uint32_t tab[256];
-  __shared__ uint32_t part[256];
-  const uint32_t b = blockIdx.x;
+// CRC-32 (zlib crc32) of each block's payload.  1024 threads per block: the
+// payload is viewed as front-padded with zeros to 64 KiB (a raw CRC -- zero
+// initial state -- ignores leading zeros; zlib's ~0 initial state is the
+// same as complementing the first four bytes), so thread t owns the 64 bytes
+// [64t, 64t + 64) of that view and every part has the same length: the parts
+// are combined pairwise in 10 rounds, round k multiplying by the constant
+// x^(8*64*2^k) mod P.  Each part is computed slice-by-8 from LDS tables; the
+// tables and multipliers are built once on the host (crc_constants).
+constexpr uint32_t kCrcThreads = 1024;
+constexpr uint32_t kCrcPart = 65536 / kCrcThreads;  // bytes per thread
+constexpr uint32_t kCrcRounds = 10;                  // log2(kCrcThreads)
+constexpr uint32_t kCrcConstWords = 8 * 256 + kCrcRounds;
+
+__global__ __launch_bounds__(1024) void k_dfl_crc(const uint8_t* __restrict__ in, const uint64_t* __restrict__ ustart,
+                                                  const uint32_t* __restrict__ lens,
+                                                  const uint32_t* __restrict__ consts, uint32_t* __restrict__ crc) {
+  __shared__ uint32_t tab[8][256];
+  __shared__ uint32_t part[kCrcThreads];
+  const uint32_t b = blockIdx.x, t = threadIdx.x;
   const uint32_t len = lens[b];
   const uint8_t* p = in + ustart[b];
-  {
-    uint32_t c = threadIdx.x;
-    for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
-    tab[threadIdx.x] = c;
-  }
+  for (uint32_t i = t; i < 8 * 256; i += kCrcThreads) (&tab[0][0])[i] = consts[i];
   __syncthreads();
-  // 8-byte slices per thread, read as whole words (byte loads strided by the
-  // slice length re-fetched each line ~48x)
-  const uint32_t slice = ((len + 255) / 256 + 7) & ~7u;
-  const uint32_t s0 = min(len, threadIdx.x * slice), s1 = min(len, s0 + slice);
+  if (len < 4) {  // too short for the complement form: one thread, byte by byte
+    if (t == 0) {
+      uint32_t r = 0xffffffffu;
+      for (uint32_t i = 0; i < len; ++i) r = tab[0][(r ^ p[i]) & 0xff] ^ (r >> 8);
+      crc[b] = r ^ 0xffffffffu;
+    }
+    return;
+  }
+  // this thread's bytes of the payload: [64t - pad, 64t + 64 - pad) clipped to [0, len)
+  const int64_t pad = 65536 - (int64_t)len;
+  const int64_t r0 = max<int64_t>(0, (int64_t)kCrcPart * t - pad);
+  const int64_t r1 = max<int64_t>(0, (int64_t)kCrcPart * (t + 1) - pad);
   uint32_t r = 0;
-  uint32_t i = s0;
-  for (; i + 8 <= s1; i += 8) {
+  int64_t i = r0;
+  for (; i + 8 <= r1; i += 8) {
     uint64_t v = dfl::ld8(p + i);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      r = tab[(r ^ (uint32_t)v) & 0xff] ^ (r >> 8);
-      v >>= 8;
-    }
+    if (i < 4) v ^= (uint64_t)(0xffffffffu >> (8 * i));  // the initial ~0: payload bytes i..3
+    const uint32_t lo = (uint32_t)v ^ r, hi = (uint32_t)(v >> 32);
+    r = tab[7][lo & 0xff] ^ tab[6][(lo >> 8) & 0xff] ^ tab[5][(lo >> 16) & 0xff] ^ tab[4][lo >> 24] ^
+        tab[3][hi & 0xff] ^ tab[2][(hi >> 8) & 0xff] ^ tab[1][(hi >> 16) & 0xff] ^ tab[0][hi >> 24];
   }
-  for (; i < s1; ++i) r = tab[(r ^ p[i]) & 0xff] ^ (r >> 8);
-  part[threadIdx.x] = r;
+  for (; i < r1; ++i) r = tab[0][(r ^ p[i] ^ (i < 4 ? 0xffu : 0u)) & 0xff] ^ (r >> 8);
+  part[t] = r;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t R = 0xffffffffu;
-    const uint32_t xs = slice ? crc_x8n(slice) : 0;
-    for (uint32_t t = 0; t < 256; ++t) {
-      const uint32_t a = min(len, t * slice), e = min(len, a + slice);
-      if (e == a) continue;
-      R = crc_mul(e - a == slice ? xs : crc_x8n(e - a), R) ^ part[t];
-    }
-    crc[b] = R ^ 0xffffffffu;
+  for (uint32_t k = 0, s = 1; s < kCrcThreads; ++k, s <<= 1) {  // pairwise combine
+    if ((t & (2 * s - 1)) == 0) part[t] = crc_mul(consts[8 * 256 + k], part[t]) ^ part[t + s];
+    __syncthreads();
   }
+  if (t == 0) crc[b] = part[0] ^ 0xffffffffu;
+}
+
+// Host: the slice-by-8 tables and x^(8*64*2^k) mod P, k < kCrcRounds.
+static uint32_t host_crc_mul(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+  for (uint32_t m = 1u << 31; m; m >>= 1) {
+    if (a & m) p ^= b;
+    b = (b & 1) ? (b >> 1) ^ kCrcPoly : b >> 1;
+  }
+  return p;
+}
+static std::vector<uint32_t> crc_constants() {
+  std::vector<uint32_t> c(kCrcConstWords);
+  for (uint32_t n = 0; n < 256; ++n) {
+    uint32_t v = n;
+    for (int k = 0; k < 8; ++k) v = (v & 1) ? (v >> 1) ^ kCrcPoly : v >> 1;
+    c[n] = v;
+  }
+  for (uint32_t k = 1; k < 8; ++k)
+    for (uint32_t n = 0; n < 256; ++n) c[256 * k + n] = (c[256 * (k - 1) + n] >> 8) ^ c[c[256 * (k - 1) + n] & 0xff];
+  uint32_t x = 1u << 30;  // x^1
+  for (int k = 0; k < 3; ++k) x = host_crc_mul(x, x);  // x^8
+  uint32_t xp = 1u << 31;  // x^(8 * kCrcPart)
+  for (uint32_t n = kCrcPart; n; n >>= 1, x = host_crc_mul(x, x))
+    if (n & 1) xp = host_crc_mul(x, xp);
+  for (uint32_t k = 0; k < kCrcRounds; ++k, xp = host_crc_mul(xp, xp)) c[8 * 256 + k] = xp;
+  return c;
 }
 
 // BGZF framing ([htsjdk] BlockCompressedOutputStream.writeGzipBlock)
@@ -183,7 +212,7 @@ BgzfCompressor::BgzfCompressor(int device) : device_(device) {}
 
 BgzfCompressor::~BgzfCompressor() {
   for (void* p : {(void*)tables_, (void*)arenas_, (void*)slots_, (void*)csize_, (void*)ovf_, (void*)crc_,
-                  (void*)offs_, (void*)out_, (void*)ustart_, (void*)lens_})
+                  (void*)offs_, (void*)out_, (void*)ustart_, (void*)lens_, (void*)crc_tab_})
     if (p) (void)hipFree(p);
 }
 
@@ -214,7 +243,14 @@ int BgzfCompressor::compress(const uint8_t* d_in, const std::vector<uint64_t>& u
       err_ = "BGZF payload above 65536 bytes";
       return kArgErr;
     }
+  out_len_ = 0;
+  fallbacks_ = 0;
   DCHK(hipSetDevice(device_));
+  if (!crc_tab_) {
+    const std::vector<uint32_t> c = crc_constants();
+    DCHK(hipMalloc(reinterpret_cast<void**>(&crc_tab_), c.size() * 4));
+    DCHK(hipMemcpy(crc_tab_, c.data(), c.size() * 4, hipMemcpyHostToDevice));
+  }
   if (!tables_) {
     dfl::Tables t;
     dfl::build_tables(&t);
@@ -242,9 +278,15 @@ int BgzfCompressor::compress(const uint8_t* d_in, const std::vector<uint64_t>& u
   DCHK(grow_buf(&ustart_, &ustart_n_, std::max<uint64_t>(nb, 1) * 8));
   DCHK(grow_buf(&lens_, &lens_n_, std::max<uint64_t>(nb, 1) * 4));
   DCHK(grow_buf(&out_, &out_n_, worst + 16));
-  hipEvent_t e0, e1;
-  DCHK(hipEventCreate(&e0));
-  DCHK(hipEventCreate(&e1));
+  struct Ev {  // destroyed on every return path
+    hipEvent_t e = nullptr;
+    ~Ev() {
+      if (e) (void)hipEventDestroy(e);
+    }
+  } ev0, ev1;
+  DCHK(hipEventCreate(&ev0.e));
+  DCHK(hipEventCreate(&ev1.e));
+  const hipEvent_t e0 = ev0.e, e1 = ev1.e;
   DCHK(hipEventRecord(e0, s));
   std::vector<uint32_t> cs(nb);
   std::vector<uint8_t> ov(nb);
@@ -253,12 +295,10 @@ int BgzfCompressor::compress(const uint8_t* d_in, const std::vector<uint64_t>& u
   if (nb) {
     DCHK(hipMemcpyAsync(ustart_, ustart.data(), nb * 8, hipMemcpyHostToDevice, s));
     DCHK(hipMemcpyAsync(lens_, lens.data(), nb * 4, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_dfl_crc, dim3((uint32_t)nb), dim3(256), 0, s, d_in, ustart_, lens_, crc_);
+    hipLaunchKernelGGL(k_dfl_crc, dim3((uint32_t)nb), dim3(kCrcThreads), 0, s, d_in, ustart_, lens_, crc_tab_,
+                       crc_);
     DCHK(hipGetLastError());
-    static const uint32_t waves = [] {
-      const char* e = getenv("HBAM_DFL_WAVES");  // experiment knob
-      return e ? (uint32_t)std::max(1, atoi(e)) : kWavesTarget;
-    }();
+    const uint32_t waves = kWavesTarget;
     for (uint64_t b0 = 0; b0 < nb; b0 += lanes) {
       const uint32_t n = (uint32_t)std::min<uint64_t>(lanes, nb - b0);
       // about kWavesTarget waves in flight over 256 CUs x 4 SIMDs
@@ -273,16 +313,12 @@ int BgzfCompressor::compress(const uint8_t* d_in, const std::vector<uint64_t>& u
         offs[b] = o;
         if (ov[b] && lens[b] + 5 > dfl::kOutCap) {
           err_ = "incompressible BGZF payload does not fit one stored block";
-          (void)hipEventDestroy(e0);
-          (void)hipEventDestroy(e1);
           return kFormatErr;
         }
         o += 26 + (ov[b] ? lens[b] + 5 : cs[b]);
       }
       if (o + (eof ? 28 : 0) > worst) {  // cannot happen (see the bound above); never write past out_
         err_ = "BGZF output bound exceeded";
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
         return kFormatErr;
       }
       DCHK(hipMemcpyAsync(offs_ + b0, offs.data() + b0, (size_t)n * 8, hipMemcpyHostToDevice, s));
@@ -294,16 +330,13 @@ int BgzfCompressor::compress(const uint8_t* d_in, const std::vector<uint64_t>& u
   offs[nb] = o;
   static const uint8_t kEof[28] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43,
                                    2,    0,    0x1b, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  out_len_ = o + (eof ? 28 : 0);
   if (eof) DCHK(hipMemcpyAsync(out_ + o, kEof, 28, hipMemcpyHostToDevice, s));
   DCHK(hipEventRecord(e1, s));
   DCHK(hipEventSynchronize(e1));
   float t = 0;
   DCHK(hipEventElapsedTime(&t, e0, e1));
   if (ms) *ms = t;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  fallbacks_ = 0;
+  out_len_ = o + (eof ? 28 : 0);  // only once the output is complete
   for (uint8_t v : ov) fallbacks_ += v;
   return 0;
 }

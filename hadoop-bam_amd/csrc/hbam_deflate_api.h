@@ -37,6 +37,7 @@ class BgzfCompressor {
   dfl::Arena* arenas_ = nullptr;
   uint8_t *slots_ = nullptr, *ovf_ = nullptr, *out_ = nullptr;
   uint32_t *csize_ = nullptr, *crc_ = nullptr, *lens_ = nullptr;
+  uint32_t* crc_tab_ = nullptr;  // k_dfl_crc constants: slice-by-8 tables + combine multipliers
   uint64_t *offs_ = nullptr, *ustart_ = nullptr;
   size_t arenas_n_ = 0, slots_n_ = 0, csize_n_ = 0, ovf_n_ = 0, crc_n_ = 0, offs_n_ = 0, out_n_ = 0, ustart_n_ = 0,
          lens_n_ = 0;

@@ -1,24 +1,27 @@
 // hbam_kernels.hip -- gfx950 kernels for the Hadoop-BAM read hot path.
 //
-//   bgzf_scan / bgzf_verify / bgzf_walk   BGZF block discovery
+//   bgzf_scan -> sort -> bgzf_verify (bgzf_walk fallback)   BGZF block discovery
 //        ([htsjdk] BlockCompressedInputStream.readBlock; heuristic twin
 //         BaseSplitGuesser.java:31-108)
-//   inflate_huff   (phase A) one wavefront per BGZF block: DEFLATE bit
-//        stream -> LZ77 tokens.  Huffman tables, canonical-decode arrays and a
-//        2 KiB compressed-input ring live in LDS (~8.4 KiB per wave); the
-//        decode state is wave-uniform (SGPRs); tokens are collected in one VGPR
-//        across the 64 lanes (v_writelane) and stored 256 B at a time.
+//   huff_tables    one wave per block: a DEFLATE block's header + Huffman
+//        tables, built ahead of the decode at high occupancy (in rounds: the
+//        first block of each BGZF block, then the one the decode stopped at)
+//   inflate_huff   (phase A) one 256-thread workgroup per BGZF block: the
+//        symbol stream -> LZ77 tokens by 256 speculative slices, a sync pass
+//        and an emit pass; the compressed block and the tables sit in LDS.
 //        ([htsjdk] BlockGunzipper.unzipBlock -> java.util.zip.Inflater)
-//   inflate_lz77   (phase B) one 256-thread workgroup per BGZF block: tokens
-//        -> bytes in a 64 KiB LDS image, block-wide prefix sums place tokens,
-//        back-references resolve in dependency rounds, then 16 B coalesced
-//        stores into the contiguous inflated stream.
-//   rec_guess / rec_link / rec_count / rec_emit   BAM record-boundary scan
-//        ([htsjdk] BAMRecordCodec.decode chain; SplittingBAMIndexer.java:340-368)
-//   rec_decode     fused field decode + sort key + voff
+//   inflate_lz77   (phase B) one 1024-thread workgroup per BGZF block: tokens
+//        -> a u16 LDS map (literal or source position), resolved by pointer
+//        chasing with path compression, 16 B coalesced stores into the
+//        contiguous inflated stream.
+//   rec_cand / rec_walk / rec_search / rec_linkfix / rec_check   BAM
+//        record-boundary chain ([htsjdk] BAMRecordCodec.decode;
+//        SplittingBAMIndexer.java:340-368) with the STRICT isValid rules
+//   rec_out        fused field decode + sort key + voff
 //        (LazyBAMRecordFactory.java:37-50; BAMRecordReader.java:81-121;
-//         util/MurmurHash3.java:32-102)
+//         util/MurmurHash3.java:32-102); long_hash for rests > 2 KiB
 //   sbi_emit       .splitting-bai entries (SplittingBAMIndexer.java:262-287)
+//   wr_copy / wr_bin_patch / wr_decode   SAMRecordWritable.write / readFields
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stddef.h>

@@ -11,8 +11,7 @@ import re
 import numpy as np
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# HBAM_LIB selects an experiment build (lib/variants/*.so); default the in-tree lib
-LIB_PATH = os.environ.get("HBAM_LIB") or os.path.join(_PKG, "lib", "libhbam.so")
+LIB_PATH = os.path.join(_PKG, "lib", "libhbam.so")
 HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "hbam.h")
 
 if not os.path.exists(LIB_PATH):

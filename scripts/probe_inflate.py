@@ -19,4 +19,4 @@ print("A WGs", nA, "deflate blocks", int(buf[2]), "per BGZF", int(buf[2]) / max(
 for i, nm in names.items():
     d = nA if i < 16 else nB
     print(f"{nm:24s} {int(buf[i]) / max(d, 1):12.0f} cycles/WG")
-print("sync re-decodes", int(buf[12]), "non-merge", int(buf[9]), "non-merge with spec event", int(buf[10]), "non-merge with 4 boundaries recorded", int(buf[11]))
+print("sync re-decodes", int(buf[12]), "non-merge", int(buf[9]), "merge", int(buf[10]), "non-merge with spec tokens", int(buf[11]))
