@@ -208,7 +208,7 @@ JNIEXPORT jlongArray FN(guessRecordStarts)(JNIEnv *env, jclass c, jlong h, jlong
 }
 
 JNIEXPORT jlongArray FN(getSplits)(JNIEnv *env, jclass c, jlong h, jlongArray starts, jlongArray lengths,
-                                   jbyteArray sbi) {
+                                   jbyteArray sbi, jbyteArray bai) {
   jsize n, m;
   uint64_t *s = from_longs(env, starts, &n);
   if (!s) return NULL;
@@ -220,14 +220,18 @@ JNIEXPORT jlongArray FN(getSplits)(JNIEnv *env, jclass c, jlong h, jlongArray st
   jlongArray r = NULL;
   jbyte *ib = sbi ? (*env)->GetByteArrayElements(env, sbi, NULL) : NULL;
   const jsize ilen = sbi ? (*env)->GetArrayLength(env, sbi) : 0;
+  jbyte *bb = bai ? (*env)->GetByteArrayElements(env, bai, NULL) : NULL;
+  const jsize blen = bai ? (*env)->GetArrayLength(env, bai) : 0;
   uint64_t *vs = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(n ? n : 1));
   uint64_t *ve = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(n ? n : 1));
   uint64_t nout = 0;
   int rc = m != n ? HBAM_E_ARG
            : (!vs || !ve)
                ? HBAM_E_NOMEM
-               : hbam_get_splits(CTX(h), s, l, (uint64_t)n, (const uint8_t *)ib, (uint64_t)ilen, vs, ve, &nout);
+               : hbam_get_splits_bai(CTX(h), s, l, (uint64_t)n, (const uint8_t *)ib, (uint64_t)ilen,
+                                     (const uint8_t *)bb, (uint64_t)blen, vs, ve, &nout);
   if (ib) (*env)->ReleaseByteArrayElements(env, sbi, ib, JNI_ABORT);
+  if (bb) (*env)->ReleaseByteArrayElements(env, bai, bb, JNI_ABORT);
   if (rc != HBAM_OK) {
     throw_for(env, rc, hbam_last_error(CTX(h)));
   } else {

@@ -98,10 +98,13 @@ public final class HbamNative {
   public static native long[] guessRecordStarts(long ctx, long[] begs, long[] ends) throws IOException;
 
   /**
-   * hbam_get_splits: the FileVirtualSplits of one file's FileSplits, from the
-   * .splitting-bai (sbi, or null: probabilistic).  Returns {vStart0, vEnd0, vStart1, ...}.
+   * hbam_get_splits_bai: the FileVirtualSplits of one file's FileSplits, from
+   * the .splitting-bai (sbi), else -- when hadoopbam.bam.enable-bai-splitter
+   * is set and the file has a .bai (bai) -- the BAI split calculator, else
+   * probabilistic.  null for a missing file.  Returns {vStart0, vEnd0, vStart1, ...}.
    */
-  public static native long[] getSplits(long ctx, long[] starts, long[] lengths, byte[] sbi) throws IOException;
+  public static native long[] getSplits(long ctx, long[] starts, long[] lengths, byte[] sbi, byte[] bai)
+      throws IOException;
 
   /**
    * hbam_encode_writables: SAMRecordWritable.write of every record of the last
