@@ -1589,6 +1589,10 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
     return;
   }
 
+  // 0. empty map: 0 marks a position no token writes (inside a match)
+  for (uint32_t c = tid; c < (kMapMax + 32) / 8; c += kLzThreads)
+    reinterpret_cast<uint4*>(map)[c] = make_uint4(0u, 0u, 0u, 0u);
+
   // 1. wave w expands tokens [w*TW, (w+1)*TW); its output range starts at
   //    the byte total of the waves before it (coalesced token loads).
   const uint32_t wid = tid >> 6, lane = tid & 63;
@@ -1611,14 +1615,10 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
   for (int w = 0; w < kLzWaves; ++w) P += (uint32_t)w < wid ? scratch[w] : 0u;
   const uint32_t whi = min(P + wsum, isize);  // end of this wave's range (the last token may run past ISIZE)
 
-  // 2. map fill, 64 tokens (one per lane) at a time.  A token is an
-  //    arithmetic run of entries base + k*delta (match: source position, 1;
-  //    literal pair: tag|b0, b1-b0).  (i) every 8-entry aligned chunk that
-  //    starts inside a token is written whole by that token with one
-  //    ds_write_b128 -- entries past the token's end are wrong but belong to
-  //    later tokens of the same wave; (ii) then each token writes its head
-  //    (its entries before its first chunk boundary) one by one, overwriting
-  //    them.  Chunks never cross the wave's range end, so waves stay disjoint.
+  // 2. token heads, 64 tokens (one per lane) at a time: a literal writes its
+  //    1-2 entries (tag | byte), a match only its distance at its first
+  //    position.  Every lane stores at most two entries, whatever the
+  //    match lengths of its wave.
   uint16_t* m = map + o0;
   uint32_t ring[kLzRing];  // tokens of the next kLzRing groups (L2 hits after step 1)
 #pragma unroll
@@ -1633,30 +1633,82 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
     const uint32_t incl = wave_incl_scan_dpp(len);
     const uint32_t pos = P + incl - len;
     P += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    const uint32_t end = min(pos + len, whi);
-    uint32_t base, delta;
-    if (t >> 31) {
-      base = pos - (((t >> 16) & 0x7fffu) + 1);  // dist <= pos: checked in phase A
-      delta = 1;
-    } else {
-      base = kLitTag | (t & 0xffu);
-      delta = (((t >> 8) & 0xffu) - (t & 0xffu)) & 0xffffu;
-    }
-    const uint32_t hb = min(end, ((o0 + pos + 7) & ~7u) - o0);  // head end = first chunk start
-    for (uint32_t q = hb; q < end; q += 8) {
-      const uint32_t v0 = base + (q - pos) * delta;
-      if (q + 8 <= whi) {
-        const uint32_t d0 = (v0 & 0xffffu) | ((v0 + delta) << 16);
-        const uint32_t inc = (2u * delta) * 0x10001u;
-        *reinterpret_cast<uint4*>(m + q) = make_uint4(d0, d0 + inc, d0 + 2u * inc, d0 + 3u * inc);
+    if (len != 0 && pos < whi) {
+      if (t >> 31) {
+        m[pos] = (uint16_t)(((t >> 16) & 0x7fffu) + 1);  // dist <= pos: checked in phase A
       } else {
-        uint32_t v = v0;
-        for (uint32_t r = q; r < whi; ++r, v += delta) m[r] = (uint16_t)v;
+        m[pos] = (uint16_t)(kLitTag | (t & 0xffu));
+        if (len == 2 && pos + 1 < whi) m[pos + 1] = (uint16_t)(kLitTag | ((t >> 8) & 0xffu));
       }
     }
-    wave_sync();  // (i) before (ii): they overlap across lanes
-    uint32_t v = base;
-    for (uint32_t r = pos; r < hb; ++r, v += delta) m[r] = (uint16_t)v;
+  }
+  __syncthreads();
+
+  // 3. match bodies: every 0 entry belongs to the match whose distance is the
+  //    nearest non-zero entry before it that is not a literal, so a
+  //    carry-forward over the map turns distances into source positions
+  //    (q - dist).  Wave w owns 8-entry chunks [512w, 512w + 512) in eight
+  //    coalesced rows of 64 chunks; pass (a) finds each wave's last non-zero
+  //    entry, pass (b) rewrites the chunks with the carry of the waves
+  //    before, of the lanes before (ballot) and of the earlier rows.
+  {
+    constexpr uint32_t kRowChunks = 64, kWaveChunks = 8 * kRowChunks;
+    const uint32_t nchunk = (o0 + isize + 7) >> 3;
+    uint4* mc = reinterpret_cast<uint4*>(map);
+    uint32_t wlast = 0;  // (a) last non-zero entry of this wave's chunks
+    for (uint32_t r = 0; r < 8; ++r) {
+      const uint32_t c = wid * kWaveChunks + r * kRowChunks + lane;
+      const uint4 e = c < nchunk ? mc[c] : make_uint4(0u, 0u, 0u, 0u);
+      const uint32_t w4[4] = {e.x, e.y, e.z, e.w};
+      uint32_t rl = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        rl = (w4[j] & 0xffffu) ? (w4[j] & 0xffffu) : rl;
+        rl = (w4[j] >> 16) ? (w4[j] >> 16) : rl;
+      }
+      const uint64_t b = __ballot(rl != 0);
+      const uint32_t top = b ? 63u - (uint32_t)__builtin_clzll(b) : 0u;
+      const uint32_t rowlast = (uint32_t)__shfl((int)rl, (int)top, 64);
+      wlast = b ? rowlast : wlast;
+    }
+    if (lane == 0) scratch[wid] = wlast;
+    __syncthreads();
+    uint32_t carry = 0;  // last non-zero entry before this wave's chunks
+    for (uint32_t w = 0; w < wid; ++w) carry = scratch[w] ? scratch[w] : carry;
+    const uint64_t below = (1ull << lane) - 1;
+    for (uint32_t r = 0; r < 8; ++r) {  // (b)
+      const uint32_t c = wid * kWaveChunks + r * kRowChunks + lane;
+      const uint4 e = c < nchunk ? mc[c] : make_uint4(0u, 0u, 0u, 0u);
+      uint32_t w4[4] = {e.x, e.y, e.z, e.w};
+      uint32_t rl = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        rl = (w4[j] & 0xffffu) ? (w4[j] & 0xffffu) : rl;
+        rl = (w4[j] >> 16) ? (w4[j] >> 16) : rl;
+      }
+      const uint64_t b = __ballot(rl != 0);
+      const uint64_t bb = b & below;
+      const uint32_t src = bb ? 63u - (uint32_t)__builtin_clzll(bb) : 0u;
+      const uint32_t from = (uint32_t)__shfl((int)rl, (int)src, 64);
+      uint32_t cur = bb ? from : carry;
+      const uint32_t top = b ? 63u - (uint32_t)__builtin_clzll(b) : 0u;
+      const uint32_t rowlast = (uint32_t)__shfl((int)rl, (int)top, 64);
+      carry = b ? rowlast : carry;
+      if (c < nchunk) {
+        // position of entry 0 of this chunk, relative to the block (index - o0)
+        const uint32_t q0 = 8u * c - o0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint32_t lo = w4[j] & 0xffffu, hi = w4[j] >> 16;
+          cur = lo ? lo : cur;
+          lo = (cur != 0 && cur < kLitTag) ? (q0 + 2u * j - cur) & 0xffffu : lo;
+          cur = hi ? hi : cur;
+          hi = (cur != 0 && cur < kLitTag) ? (q0 + 2u * j + 1u - cur) & 0xffffu : hi;
+          w4[j] = lo | (hi << 16);
+        }
+        mc[c] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      }
+    }
   }
   __syncthreads();
 

@@ -11,7 +11,8 @@ import re
 import numpy as np
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG, "lib", "libhbam.so")
+# HBAM_LIB: load another in-tree build of the same ABI (scripts/probe_inflate.py compares variants)
+LIB_PATH = os.environ.get("HBAM_LIB") or os.path.join(_PKG, "lib", "libhbam.so")
 HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "hbam.h")
 
 if not os.path.exists(LIB_PATH):

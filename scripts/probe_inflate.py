@@ -1,22 +1,43 @@
-import sys, os, ctypes as C
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "hadoop-bam_amd"))
-import numpy as np, hbam
-from hbam import synth
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
-data, info = synth.make_bam(n, as_numpy=True)
-g = hbam.Gpu(0); g.load(data); g.run()
-L = hbam._L
-L.hbam_probe_read.argtypes = [C.c_void_p, C.c_int]
-buf = np.zeros(32, np.uint64)
-L.hbam_probe_read(buf.ctypes.data, 1)
-st = g.run(timing=True)
-L.hbam_probe_read(buf.ctypes.data, 1)
-print(info, {k: round(st[k], 2) for k in ("ms_huff", "ms_lz77", "ms_total")})
-nA, nB = int(buf[15]), int(buf[16])
-names = {0: "A stage", 1: "A hdr(wave0)+barrier", 3: "A spec", 4: "A sync loop", 5: "A scan", 6: "A emit", 7: "A total",
-         17: "B sum", 18: "B fill", 19: "B resolve", 20: "B store", 21: "B total"}
-print("A WGs", nA, "deflate blocks", int(buf[2]), "per BGZF", int(buf[2]) / max(nA, 1), "sync iters/defl", int(buf[8]) / max(int(buf[2]), 1))
-for i, nm in names.items():
-    d = nA if i < 16 else nB
-    print(f"{nm:24s} {int(buf[i]) / max(d, 1):12.0f} cycles/WG")
-print("sync re-decodes", int(buf[12]), "non-merge", int(buf[9]), "merge", int(buf[10]), "non-merge with spec tokens", int(buf[11]))
+"""Stage times of one resident pass over a synthetic C2-shaped BAM.
+
+usage: python scripts/probe_inflate.py [records] [lib.so ...]
+Each extra argument is an alternative libhbam.so (HBAM_LIB) run in its own
+child process on the same file, so variants compare on identical input.
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(ROOT, "hadoop-bam_amd"))
+
+
+def one(n, reps=5):
+    import numpy as np
+    import hbam
+    from hbam import synth
+    data, info = synth.make_bam(n, as_numpy=True)
+    g = hbam.Gpu(0)
+    g.load(data)
+    g.run()
+    best = None
+    for _ in range(reps):
+        st = g.run(timing=True)
+        if best is None or st["ms_total"] < best["ms_total"]:
+            best = st
+    out = {k: round(v, 3) for k, v in best.items() if k.startswith("ms_")}
+    out["records"] = n
+    out["lib"] = os.environ.get("HBAM_LIB", "default")
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+    libs = sys.argv[2:]
+    if os.environ.get("HBAM_PROBE_CHILD") or not libs:
+        one(n)
+    else:
+        for lib in libs:
+            env = dict(os.environ, HBAM_LIB=os.path.abspath(lib), HBAM_PROBE_CHILD="1")
+            subprocess.run([sys.executable, __file__, str(n)], env=env, check=True, timeout=300)
