@@ -701,6 +701,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
   return v;
 }
 
+// Inclusive wave max-scan on DPP (as wave_incl_scan_dpp; 0 is the identity).
+__device__ __forceinline__ uint32_t wave_incl_max_dpp(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true));   // row_shr:1
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true));   // row_shr:2
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true));   // row_shr:4
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true));   // row_shr:8
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return v;
+}
+
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const uint32_t lane = lane_id();
 #pragma unroll
@@ -1484,6 +1495,8 @@ constexpr int kLzWaves = kLzThreads / 64;
 constexpr uint32_t kMapMax = 65280;
 constexpr uint32_t kLitTag = 0xFF00u;
 constexpr int kLzRing = 4;  // phase-B fill: 64-token groups loaded ahead (4 vs 8 measured equal)
+constexpr int kLzTokGroups = 32;  // token groups a wave keeps in registers (32 K tokens per block)
+constexpr int kLzChase = 2;  // positions chased together per thread (4: slower, longer chains)
 
 // exclusive scan over the workgroup; returns the prefix, *total = sum
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
@@ -1594,17 +1607,31 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
     reinterpret_cast<uint4*>(map)[c] = make_uint4(0u, 0u, 0u, 0u);
 
   // 1. wave w expands tokens [w*TW, (w+1)*TW); its output range starts at
-  //    the byte total of the waves before it (coalesced token loads).
+  //    the byte total of the waves before it.  Up to kLzTokGroups groups of
+  //    64 tokens stay in registers from this load to step 2 (all loads in
+  //    flight at once); a wave with more re-reads them (L2) through a ring.
   const uint32_t wid = tid >> 6, lane = tid & 63;
   const uint32_t TW = (ntok + kLzWaves - 1) / kLzWaves;
   const uint32_t tw0 = min(wid * TW, ntok), tw1 = min(tw0 + TW, ntok);
+  const bool inreg = TW <= 64u * kLzTokGroups;  // uniform over the workgroup
+  uint32_t tr[kLzTokGroups];
   uint32_t wsum = 0;
-  for (uint32_t i0 = tw0 + lane; i0 < tw1 + lane; i0 += 8 * 64) {  // 8 loads in flight
-    uint32_t tv[8];
+  if (inreg) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) tv[k] = i0 + 64 * k < tw1 ? tk[i0 + 64 * k] : 0u;
+    for (int k = 0; k < kLzTokGroups; ++k) {
+      const uint32_t i = tw0 + lane + 64u * k;
+      tr[k] = i < tw1 ? tk[i] : 0u;  // 0 = a literal token of length 0
+    }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) wsum += i0 + 64 * k < tw1 ? tok_len(tv[k]) : 0u;
+    for (int k = 0; k < kLzTokGroups; ++k) wsum += tok_len(tr[k]);
+  } else {
+    for (uint32_t i0 = tw0 + lane; i0 < tw1 + lane; i0 += 8 * 64) {  // 8 loads in flight
+      uint32_t tv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) tv[k] = i0 + 64 * k < tw1 ? tk[i0 + 64 * k] : 0u;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) wsum += tok_len(tv[k]);
+    }
   }
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) wsum += __shfl_xor(wsum, d, 64);
@@ -1620,16 +1647,8 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
   //    position.  Every lane stores at most two entries, whatever the
   //    match lengths of its wave.
   uint16_t* m = map + o0;
-  uint32_t ring[kLzRing];  // tokens of the next kLzRing groups (L2 hits after step 1)
-#pragma unroll
-  for (int k = 0; k < kLzRing; ++k) ring[k] = tw0 + lane + 64 * k < tw1 ? tk[tw0 + lane + 64 * k] : 0u;
-  for (uint32_t gi = tw0; gi < tw1 && P < whi; gi += 64) {  // wave-uniform
-    const uint32_t i = gi + lane;
-    const uint32_t t = ring[0];
-#pragma unroll
-    for (int k = 0; k + 1 < kLzRing; ++k) ring[k] = ring[k + 1];
-    ring[kLzRing - 1] = i + 64 * kLzRing < tw1 ? tk[i + 64 * kLzRing] : 0u;
-    const uint32_t len = i < tw1 ? tok_len(t) : 0u;
+  auto head = [&](uint32_t t) {
+    const uint32_t len = tok_len(t);
     const uint32_t incl = wave_incl_scan_dpp(len);
     const uint32_t pos = P + incl - len;
     P += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -1641,62 +1660,76 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
         if (len == 2 && pos + 1 < whi) m[pos + 1] = (uint16_t)(kLitTag | ((t >> 8) & 0xffu));
       }
     }
+  };
+  if (inreg) {
+#pragma unroll
+    for (int k = 0; k < kLzTokGroups; ++k) {
+      if (tw0 + 64u * k >= tw1) break;  // wave-uniform
+      head(tr[k]);
+    }
+  } else {
+    uint32_t ring[kLzRing];  // tokens of the next kLzRing groups (L2 hits after step 1)
+#pragma unroll
+    for (int k = 0; k < kLzRing; ++k) ring[k] = tw0 + lane + 64 * k < tw1 ? tk[tw0 + lane + 64 * k] : 0u;
+    for (uint32_t gi = tw0; gi < tw1 && P < whi; gi += 64) {  // wave-uniform
+      const uint32_t i = gi + lane;
+      const uint32_t t = ring[0];
+#pragma unroll
+      for (int k = 0; k + 1 < kLzRing; ++k) ring[k] = ring[k + 1];
+      ring[kLzRing - 1] = i + 64 * kLzRing < tw1 ? tk[i + 64 * kLzRing] : 0u;
+      head(i < tw1 ? t : 0u);
+    }
   }
   __syncthreads();
 
   // 3. match bodies: every 0 entry belongs to the match whose distance is the
   //    nearest non-zero entry before it that is not a literal, so a
   //    carry-forward over the map turns distances into source positions
-  //    (q - dist).  Wave w owns 8-entry chunks [512w, 512w + 512) in eight
-  //    coalesced rows of 64 chunks; pass (a) finds each wave's last non-zero
-  //    entry, pass (b) rewrites the chunks with the carry of the waves
-  //    before, of the lanes before (ballot) and of the earlier rows.
+  //    (q - dist).  Wave w owns 8-entry chunks [512w, 512w + 512), eight
+  //    coalesced rows of 64 chunks held in registers.  The carry is a running
+  //    max of keys (chunk + 1) << 16 | last non-zero entry of the chunk:
+  //    keys grow with the position, so max-scans over rows, lanes (DPP) and
+  //    waves (LDS) find the nearest non-zero entry before each chunk.
   {
     constexpr uint32_t kRowChunks = 64, kWaveChunks = 8 * kRowChunks;
     const uint32_t nchunk = (o0 + isize + 7) >> 3;
     uint4* mc = reinterpret_cast<uint4*>(map);
-    uint32_t wlast = 0;  // (a) last non-zero entry of this wave's chunks
-    for (uint32_t r = 0; r < 8; ++r) {
-      const uint32_t c = wid * kWaveChunks + r * kRowChunks + lane;
-      const uint4 e = c < nchunk ? mc[c] : make_uint4(0u, 0u, 0u, 0u);
-      const uint32_t w4[4] = {e.x, e.y, e.z, e.w};
-      uint32_t rl = 0;
+    uint4 rows[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        rl = (w4[j] & 0xffffu) ? (w4[j] & 0xffffu) : rl;
-        rl = (w4[j] >> 16) ? (w4[j] >> 16) : rl;
-      }
-      const uint64_t b = __ballot(rl != 0);
-      const uint32_t top = b ? 63u - (uint32_t)__builtin_clzll(b) : 0u;
-      const uint32_t rowlast = (uint32_t)__shfl((int)rl, (int)top, 64);
-      wlast = b ? rowlast : wlast;
+    for (int r = 0; r < 8; ++r) {
+      const uint32_t c = wid * kWaveChunks + r * kRowChunks + lane;
+      rows[r] = c < nchunk ? mc[c] : make_uint4(0u, 0u, 0u, 0u);
     }
-    if (lane == 0) scratch[wid] = wlast;
-    __syncthreads();
-    uint32_t carry = 0;  // last non-zero entry before this wave's chunks
-    for (uint32_t w = 0; w < wid; ++w) carry = scratch[w] ? scratch[w] : carry;
-    const uint64_t below = (1ull << lane) - 1;
-    for (uint32_t r = 0; r < 8; ++r) {  // (b)
-      const uint32_t c = wid * kWaveChunks + r * kRowChunks + lane;
-      const uint4 e = c < nchunk ? mc[c] : make_uint4(0u, 0u, 0u, 0u);
-      uint32_t w4[4] = {e.x, e.y, e.z, e.w};
+    uint32_t key[8], kmax = 0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const uint32_t w4[4] = {rows[r].x, rows[r].y, rows[r].z, rows[r].w};
       uint32_t rl = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         rl = (w4[j] & 0xffffu) ? (w4[j] & 0xffffu) : rl;
         rl = (w4[j] >> 16) ? (w4[j] >> 16) : rl;
       }
-      const uint64_t b = __ballot(rl != 0);
-      const uint64_t bb = b & below;
-      const uint32_t src = bb ? 63u - (uint32_t)__builtin_clzll(bb) : 0u;
-      const uint32_t from = (uint32_t)__shfl((int)rl, (int)src, 64);
-      uint32_t cur = bb ? from : carry;
-      const uint32_t top = b ? 63u - (uint32_t)__builtin_clzll(b) : 0u;
-      const uint32_t rowlast = (uint32_t)__shfl((int)rl, (int)top, 64);
-      carry = b ? rowlast : carry;
+      const uint32_t c = wid * kWaveChunks + r * kRowChunks + lane;
+      key[r] = rl ? ((c + 1u) << 16) | rl : 0u;
+      kmax = max(kmax, key[r]);
+    }
+    const uint32_t wmax = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_dpp(kmax), 63);
+    if (lane == 0) scratch[wid] = wmax;
+    __syncthreads();
+    uint32_t carry = 0;  // key of the last non-zero entry before this wave's chunks
+    for (uint32_t w = 0; w < wid; ++w) carry = max(carry, scratch[w]);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const uint32_t incl = wave_incl_max_dpp(key[r]);
+      const uint32_t excl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x138, 0xf, 0xf, true);  // wave_shr:1
+      uint32_t cur = max(carry, excl) & 0xffffu;
+      carry = max(carry, (uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
+      const uint32_t c = wid * kWaveChunks + r * kRowChunks + lane;
       if (c < nchunk) {
         // position of entry 0 of this chunk, relative to the block (index - o0)
         const uint32_t q0 = 8u * c - o0;
+        uint32_t w4[4] = {rows[r].x, rows[r].y, rows[r].z, rows[r].w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           uint32_t lo = w4[j] & 0xffffu, hi = w4[j] >> 16;
@@ -1712,31 +1745,38 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
   }
   __syncthreads();
 
-  // 3. resolve, increasing positions first; results written back in place
-  //    (path compression).  Each round (1024 consecutive positions) costs one
-  //    dependent LDS latency per chase step, so the raw entries of this
-  //    thread's next positions (written by fill, rewritten only by this
-  //    thread) are loaded kLzPf rounds ahead.
-  // two rounds per pass: the chases of positions q and q + 1024 are
-  // independent, so their dependent LDS loads overlap (any visiting order is
-  // correct: entries always point to smaller positions and a chase ends at a
-  // literal, resolved or not)
-  for (uint32_t q = tid; q < isize; q += 2 * kLzThreads) {
-    const uint32_t q2 = q + kLzThreads;
-    const bool has2 = q2 < isize;
-    uint32_t v1 = m[q], v2 = has2 ? m[q2] : kLitTag;
-    while ((v1 < kLitTag) | (v2 < kLitTag)) {
-      const uint32_t n1 = v1 < kLitTag ? m[v1] : v1;
-      const uint32_t n2 = v2 < kLitTag ? m[v2] : v2;
-      v1 = n1;
-      v2 = n2;
+  // 4. resolve, increasing positions first; results written back in place
+  //    (path compression).  Each chase step is one dependent LDS load, so a
+  //    thread chases kLzChase positions 1024 apart at once (their loads
+  //    overlap).  Any visiting order is correct: entries always point to
+  //    smaller positions and a chase ends at a literal, resolved or not.
+  // Branch-free steps: a resolved lane re-reads its own entry and keeps its
+  // value (a select, not an exec-masked read).
+  for (uint32_t q = tid; q < isize; q += kLzChase * kLzThreads) {
+    uint32_t v[kLzChase], at[kLzChase];
+#pragma unroll
+    for (int k = 0; k < kLzChase; ++k) {
+      at[k] = q + k * kLzThreads < isize ? q + k * kLzThreads : q;
+      v[k] = m[at[k]];
     }
-    m[q] = (uint16_t)v1;
-    if (has2) m[q2] = (uint16_t)v2;
+    for (;;) {
+      bool more = false;
+#pragma unroll
+      for (int k = 0; k < kLzChase; ++k) more |= v[k] < kLitTag;
+      if (!__builtin_amdgcn_ballot_w64(more)) break;
+      uint32_t n[kLzChase];
+#pragma unroll
+      for (int k = 0; k < kLzChase; ++k) n[k] = m[v[k] < kLitTag ? v[k] : at[k]];
+#pragma unroll
+      for (int k = 0; k < kLzChase; ++k) v[k] = v[k] < kLitTag ? n[k] : v[k];
+    }
+#pragma unroll
+    for (int k = 0; k < kLzChase; ++k)
+      if (q + k * kLzThreads < isize) m[q + k * kLzThreads] = (uint16_t)v[k];
   }
   __syncthreads();
 
-  // 4. 16 B stores; low bytes of 16 entries packed with v_perm
+  // 5. 16 B stores; low bytes of 16 entries packed with v_perm
   for (uint32_t s = tid; s < nseg; s += kLzThreads) {
     const uint64_t ga = g0 + 16ull * s;
     if (ga >= blk.ustart && ga + 16 <= gend) {
