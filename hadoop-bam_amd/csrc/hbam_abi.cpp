@@ -135,6 +135,7 @@ int decode_device(BamFile& f, uint64_t vstart, uint64_t vend, int32_t flags, hba
       st->ms_inflate += p.times.inflate;
       st->ms_huff += p.times.huff;
       st->ms_lz77 += p.times.lz77;
+      st->ms_tables += p.times.tables;
       st->ms_chain += p.times.chain;
       st->ms_decode += p.times.decode;
     }

@@ -27,9 +27,9 @@ Pipeline::Pipeline(int device) : device_(device) {
   }
   if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&stream_b_, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&stream_t_, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&stream_copy_, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&stream_loc_, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&stream_t_, hipStreamNonBlocking) != hipSuccess)
+      hipStreamCreateWithFlags(&stream_loc_, hipStreamNonBlocking) != hipSuccess)
     err_ = "hipStreamCreate failed";
   for (auto& e : ev_) (void)hipEventCreate(&e);
   for (auto& e : sync_ev_) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -42,11 +42,11 @@ Pipeline::~Pipeline() {
   (void)hipDeviceSynchronize();
   for (auto& e : ev_) (void)hipEventDestroy(e);
   for (auto& e : sync_ev_) (void)hipEventDestroy(e);
-  for (auto& e : tev_) (void)hipEventDestroy(e);
-  for (auto& e : copy_ev_) (void)hipEventDestroy(e);
   for (auto& e : tab_ev_) (void)hipEventDestroy(e);
   for (auto& e : hdone_ev_) (void)hipEventDestroy(e);
-  for (hipStream_t s : {stream_b_, stream_copy_, stream_loc_, stream_t_, stream_})
+  for (auto& e : tev_) (void)hipEventDestroy(e);
+  for (auto& e : copy_ev_) (void)hipEventDestroy(e);
+  for (hipStream_t s : {stream_b_, stream_t_, stream_copy_, stream_loc_, stream_})
     if (s) (void)hipStreamDestroy(s);
 }
 
@@ -374,11 +374,15 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
   if (b0 >= b1) return kOk;
   const uint8_t* fbase = dfile_ - base_;
   if (timing) HIPCHK(hipEventRecord(ev_[2], stream_));
-  float huff_ms = 0, lz_ms = 0;
-  // Chunks of up to kInflateChunkBlocks blocks.  Phase A of chunk j runs on
-  // stream_, phase B on stream_b_ after it; token buffers alternate by chunk
-  // parity, so phase A of chunk j+1 overlaps phase B of chunk j (phase A needs
-  // ~12 KiB of LDS per workgroup and fits beside a phase-B workgroup on a CU).
+  // Chunks of up to kInflateChunkBlocks blocks: per chunk the table build and
+  // phase A in rounds, then phase B.  Production runs overlap them: phase A
+  // on stream_, phase B on stream_b_ after it, the round-0 tables of chunk j
+  // on stream_t_ beside phase A of chunk j-1, token and table buffers by
+  // chunk parity (~0.7 ms per C2 pass faster than one stream).  A timed run
+  // (measurement) puts every launch on stream_, each bracketed by events, so
+  // its per-kernel times are kernel durations, as rocprofv3 reports them.
+  const bool serial = timing;
+  hipStream_t sB = serial ? stream_ : stream_b_, sT = serial ? stream_ : stream_t_;
   struct Chunk { uint32_t b, e; };
   std::vector<Chunk> chunks;
   uint32_t b = b0;
@@ -395,9 +399,10 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
   }
   const bool any = !chunks.empty();
   const size_t nc = chunks.size();
-  if (timing && tev_.size() < 3 * nc) {
+  const size_t per_chunk = 2 * (2 * kInflateRounds + 1);  // event pairs: tables + phase A per round, phase B
+  if (timing && tev_.size() < per_chunk * nc) {
     const size_t old = tev_.size();
-    tev_.resize(3 * nc);
+    tev_.resize(per_chunk * nc);
     for (size_t i = old; i < tev_.size(); ++i) HIPCHK(hipEventCreate(&tev_[i]));
   }
   // size every buffer up front: a reallocation inside the loop could free a
@@ -407,74 +412,76 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
     max_u = std::max(max_u, hblocks_[c.e - 1].ustart + hblocks_[c.e - 1].isize - hblocks_[c.b].ustart);
     max_nb = std::max<uint64_t>(max_nb, c.e - c.b);
   }
+  const int nbuf = nc > 1 && !serial ? 2 : 1;
   if (any) {
-    for (int i = 0; i < (nc > 1 ? 2 : 1); ++i) HIPCHK(tokens_[i].reserve(max_u + 16));  // phase B reads tokens as uint4
-    for (int i = 0; i < (nc > 1 ? 2 : 1); ++i) {
+    for (int i = 0; i < nbuf; ++i) {
+      HIPCHK(tokens_[i].reserve(max_u + 16));  // phase B reads tokens as uint4
       HIPCHK(tables_[i].reserve(max_nb * kHuffTableImage));
       HIPCHK(tinfo_[i].reserve(max_nb));
     }
-    // phase B and the table builds see everything queued on stream_ before this call
-    HIPCHK(hipEventRecord(sync_ev_[0], stream_));
-    HIPCHK(hipStreamWaitEvent(stream_b_, sync_ev_[0], 0));
-    HIPCHK(hipStreamWaitEvent(stream_t_, sync_ev_[0], 0));
+    if (!serial) {  // phase B and the table builds see everything queued on stream_ before this call
+      HIPCHK(hipEventRecord(sync_ev_[0], stream_));
+      HIPCHK(hipStreamWaitEvent(stream_b_, sync_ev_[0], 0));
+      HIPCHK(hipStreamWaitEvent(stream_t_, sync_ev_[0], 0));
+    }
   }
+  size_t ne = 0;  // events recorded (serial)
+  auto mark = [&]() -> hipError_t { return serial ? hipEventRecord(tev_[ne++], stream_) : hipSuccess; };
   for (size_t j = 0; j < nc; ++j) {
     const uint32_t cb = chunks[j].b, ce = chunks[j].e;
-    const int par = (int)(j & 1);
+    const int par = serial ? 0 : (int)(j & 1);
     const uint64_t cu = hblocks_[cb].ustart;
     uint32_t max_stage = 0;
     for (uint32_t k = cb; k < ce; ++k) max_stage = std::max(max_stage, huff_stage_bytes(hblocks_[k]));
-    if (j >= 2) HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + par], 0));  // B(j-2) released the buffer
-    if (timing) HIPCHK(hipEventRecord(tev_[3 * j], stream_));
-    // tables of chunk j on stream_t_ (they overlap phase A of chunk j-1; the
-    // parity buffer is free once phase A of chunk j-2 is done)
-    if (j >= 2) HIPCHK(hipStreamWaitEvent(stream_t_, hdone_ev_[par], 0));
-    HIPCHK(launch_huff_tables(fbase, dblocks_.p, cb, ce - cb, tables_[par].p, tinfo_[par].p, hout_.p, 0, stream_t_));
-    HIPCHK(hipEventRecord(tab_ev_[par], stream_t_));
-    HIPCHK(hipStreamWaitEvent(stream_, tab_ev_[par], 0));
+    if (!serial && j >= 2) {
+      HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + par], 0));  // B(j-2) released the token buffer
+      HIPCHK(hipStreamWaitEvent(stream_t_, hdone_ev_[par], 0));   // A(j-2) released the table buffer
+    }
     // rounds: each decode stops a block before its next DEFLATE header, which
     // the next round's table build parses (the last round decodes inline)
     for (uint32_t r = 0; r < kInflateRounds; ++r) {
-      if (r > 0)
-        HIPCHK(launch_huff_tables(fbase, dblocks_.p, cb, ce - cb, tables_[par].p, tinfo_[par].p, hout_.p, r,
-                                  stream_));
+      HIPCHK(mark());
+      HIPCHK(launch_huff_tables(fbase, dblocks_.p, cb, ce - cb, tables_[par].p, tinfo_[par].p, hout_.p, r,
+                                r == 0 ? sT : stream_));
+      HIPCHK(mark());
+      if (r == 0 && !serial) {
+        HIPCHK(hipEventRecord(tab_ev_[par], stream_t_));
+        HIPCHK(hipStreamWaitEvent(stream_, tab_ev_[par], 0));
+      }
+      HIPCHK(mark());
       HIPCHK(launch_inflate_huff_prebuilt(fbase, dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, max_stage,
                                           tables_[par].p, tinfo_[par].p, r, r + 1 < kInflateRounds ? 1u : 0u,
                                           stream_));
+      HIPCHK(mark());
     }
-    HIPCHK(hipEventRecord(hdone_ev_[par], stream_));
-    if (timing) HIPCHK(hipEventRecord(tev_[3 * j + 1], stream_));
-    HIPCHK(hipEventRecord(sync_ev_[par], stream_));
-    HIPCHK(hipStreamWaitEvent(stream_b_, sync_ev_[par], 0));
-    HIPCHK(launch_inflate_lz77(dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, du_.p, stream_b_));
-    if (timing) HIPCHK(hipEventRecord(tev_[3 * j + 2], stream_b_));
-    HIPCHK(hipEventRecord(sync_ev_[2 + par], stream_b_));
+    if (!serial) {
+      HIPCHK(hipEventRecord(hdone_ev_[par], stream_));
+      HIPCHK(hipEventRecord(sync_ev_[par], stream_));
+      HIPCHK(hipStreamWaitEvent(stream_b_, sync_ev_[par], 0));
+    }
+    HIPCHK(mark());
+    HIPCHK(launch_inflate_lz77(dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, du_.p, sB));
+    HIPCHK(mark());
+    if (!serial) HIPCHK(hipEventRecord(sync_ev_[2 + par], stream_b_));
     for (uint32_t k = cb; k < ce; ++k) inflated_[k] = 1;
     ++inflate_launches_;
   }
-  if (any) {  // everything after this call on stream_ sees phase B done
+  if (any && !serial) {  // everything after this call on stream_ sees phase B done
     HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + ((nc - 1) & 1)], 0));
     if (nc >= 2) HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + ((nc - 2) & 1)], 0));
   }
+  float tab_ms = 0, huff_ms = 0, lz_ms = 0;
   if (timing && any) {
-    // phase A: its launch on stream_; phase B: from max(A done, previous B done)
-    HIPCHK(hipEventSynchronize(tev_[3 * nc - 1]));
-    for (size_t j = 0; j < nc; ++j) {
-      float a = 0, c = 0;
-      (void)hipEventElapsedTime(&a, tev_[3 * j], tev_[3 * j + 1]);
-      hipEvent_t from = tev_[3 * j + 1];
-      if (j > 0) {
-        float d = 0;
-        (void)hipEventElapsedTime(&d, tev_[3 * j + 1], tev_[3 * j - 1]);
-        if (d > 0) from = tev_[3 * j - 1];
-      }
-      (void)hipEventElapsedTime(&c, from, tev_[3 * j + 2]);
-      huff_ms += a;
-      lz_ms += c;
+    HIPCHK(hipEventSynchronize(tev_[ne - 1]));
+    for (size_t i = 0; i < ne; i += 2) {
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, tev_[i], tev_[i + 1]);
+      const size_t k = (i / 2) % (2 * kInflateRounds + 1);  // position of the pair within its chunk
+      (k == 2 * kInflateRounds ? lz_ms : (k & 1) ? huff_ms : tab_ms) += ms;
     }
   }
   if (!any) {
-    times.inflate = times.huff = times.lz77 = 0;
+    times.inflate = times.huff = times.lz77 = times.tables = 0;
     return kOk;
   }
   if (!check) return kOk;  // the caller checks hout_ once all blocks are queued
@@ -488,6 +495,7 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
   HIPCHK(hipStreamSynchronize(stream_));
   if (timing) {
     (void)hipEventElapsedTime(&times.inflate, ev_[2], ev_[3]);
+    times.tables = tab_ms;
     times.huff = huff_ms;
     times.lz77 = lz_ms;
   }
@@ -599,7 +607,7 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
   a.validate = mode != kReader ? 0 : stringency_ == kStrict ? 2 : stringency_ == kLenient ? 1 : 0;
   a.ref_len = n_ref_len_ == (uint32_t)std::max(n_ref_, 0) && n_ref_len_ ? ref_len_.p : nullptr;
   if (timing) HIPCHK(hipEventRecord(ev_[0], stream_));
-  float infl_ms = 0, huff_ms = 0, lz_ms = 0;
+  float infl_ms = 0, huff_ms = 0, lz_ms = 0, tab_ms = 0;
   bool lists = true;  // chain v2 lists hold every record start (no overflow)
   for (int it = 0;; ++it) {
     if (it >= kMaxChainIters) return fail(kErrState, "record chain did not converge");
@@ -608,6 +616,7 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
       infl_ms += times.inflate;
       huff_ms += times.huff;
       lz_ms += times.lz77;
+      tab_ms += times.tables;
     }
     if (rc != kOk) return rc;
     a.u = du_.p;
@@ -773,6 +782,7 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
     times.inflate = infl_ms;
     times.huff = huff_ms;
     times.lz77 = lz_ms;
+    times.tables = tab_ms;
   }
   return kOk;
 }

@@ -82,6 +82,7 @@ struct SpanDev {
 
 struct StageTimes {  // milliseconds of the last decode (HIP events)
   float locate = 0, inflate = 0, huff = 0, lz77 = 0, chain = 0, decode = 0;
+  float tables = 0;  // k_huff_tables (huff: k_inflate_huff only)
 };
 
 // Record-level validation ([htsjdk] ValidationStringency, the
@@ -204,7 +205,6 @@ class Pipeline {
 
   int device_ = 0;
   hipStream_t stream_ = nullptr;
-  hipStream_t stream_b_ = nullptr;  // inflate phase B (overlaps phase A of the next chunk)
   hipStream_t stream_copy_ = nullptr;  // run_streamed: host->HBM pieces
   hipStream_t stream_loc_ = nullptr;   // run_streamed: per-piece block discovery
   std::vector<hipEvent_t> copy_ev_;
@@ -231,13 +231,15 @@ class Pipeline {
 
   DevBuf<uint8_t> du_;
   std::vector<uint8_t> inflated_;  // per block flag
-  DevBuf<uint32_t> tokens_[2];  // double-buffered LZ77 token streams (chunk parity)
+  DevBuf<uint32_t> tokens_[2];  // LZ77 token streams, by chunk parity (overlapped inflate)
   DevBuf<HuffOut> hout_;
   DevBuf<uint8_t> tables_[2];     // phase-A prebuilt table images (per chunk, by chunk parity)
-  DevBuf<HuffTableInfo> tinfo_[2];
-  hipStream_t stream_t_ = nullptr;  // table prebuild of chunk j+1 beside phase A of chunk j
+  hipStream_t stream_b_ = nullptr;  // inflate phase B (overlaps phase A of the next chunk)
+  hipStream_t stream_t_ = nullptr;  // round-0 table build of chunk j beside phase A of chunk j-1
   hipEvent_t tab_ev_[2];            // tables of the chunk of that parity built
   hipEvent_t hdone_ev_[2];          // phase A of the chunk of that parity done (tables free)
+  hipEvent_t sync_ev_[4];           // [0,1] phase A done, [2,3] phase B done, per token buffer
+  DevBuf<HuffTableInfo> tinfo_[2];
 
   // span scratch
   DevBuf<uint64_t> g_, x_, x2_, entry_, base_arr_, summary_, dead_;
@@ -260,7 +262,6 @@ class Pipeline {
   DevBuf<uint64_t> scalars_;             // next_pos / digests read back by the host
 
   hipEvent_t ev_[8];
-  hipEvent_t sync_ev_[4];           // [0,1] phase A done, [2,3] phase B done, per token buffer
   std::vector<hipEvent_t> tev_;     // timing events of overlapped inflate chunks
 };
 

@@ -62,7 +62,7 @@ class GpuStats(C.Structure):
                 ("ms_locate", C.c_float), ("ms_inflate", C.c_float), ("ms_huff", C.c_float),
                 ("ms_lz77", C.c_float), ("ms_chain", C.c_float), ("ms_decode", C.c_float),
                 ("ms_total", C.c_float), ("status", i32), ("link_fallbacks", i32),
-                ("inflate_launches", i32), ("link_rewalks", i32), ("windows", i32), ("reserved", i32)]
+                ("inflate_launches", i32), ("link_rewalks", i32), ("windows", i32), ("ms_tables", C.c_float)]
 
 
 def _sig(name, res, args):

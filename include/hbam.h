@@ -243,7 +243,7 @@ typedef struct hbam_gpu_stats {
   int32_t inflate_launches;   /* phase A + B launch pairs of this run */
   int32_t link_rewalks;       /* parallel-link re-walk rounds of this run */
   int32_t windows;            /* HBM windows the span was decoded in */
-  int32_t reserved;
+  float ms_tables;            /* k_huff_tables (ms_huff: k_inflate_huff, ms_lz77: k_inflate_lz77) */
 } hbam_gpu_stats;
 
 /* hbam_decode_span with the records left in HBM (no host copies): counts,
