@@ -1170,10 +1170,15 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
     // image), kStageBatch 16 B loads in flight per thread before their LDS
     // stores: the copy costs about one memory latency instead of one per
     // loop trip.
-    const uint32_t nq = STAGE ? (uint32_t)((blk.coff + blk.csize - abase + 15) >> 4) + 1 : 0u;
+    // A later round reads nothing before the bit where the last one stopped,
+    // so only the 16 B units from there on are staged.
+    const uint32_t nq_all = STAGE ? (uint32_t)((blk.coff + blk.csize - abase + 15) >> 4) + 1 : 0u;
+    const uint32_t q0 = round > 0 ? min(h0.resume_bit >> 7, nq_all) : 0u;
+    const uint32_t nq = nq_all - q0;
     const uint32_t nt = ti.status == 0 ? kTableImage / 16 : 0u;
-    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(file + abase);
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(file + abase) + q0;
     const uint4* __restrict__ tsrc = reinterpret_cast<const uint4*>(tables + (uint64_t)blockIdx.x * kTableImage);
+    uint4* sdst = s_in + q0;
     uint4* tdst = reinterpret_cast<uint4*>(&L);
     constexpr int kStageBatch = 4;
     for (uint32_t i0 = tid; i0 < nq + nt; i0 += kStageBatch * kHuffThreads) {
@@ -1187,7 +1192,7 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
 #pragma unroll
       for (int k = 0; k < kStageBatch; ++k) {
         const uint32_t i = i0 + k * kHuffThreads;
-        if (i < nq) s_in[i] = v[k];
+        if (i < nq) sdst[i] = v[k];
         else if (i < nq + nt) tdst[i - nq] = v[k];
       }
     }
