@@ -389,6 +389,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the in-session rocprofv3 PMC passes")
     ap.add_argument("--no-extra", action="store_true", help="skip every side leg (drop-in, C3/C5, C4, write)")
+    ap.add_argument("--serial", action="store_true",
+                    help="every step in the measurement launch order (one stream, events per launch): the "
+                         "command profiles/collect.sh traces, so rocprofv3's per-kernel averages are the "
+                         "durations the roofline uses")
     ap.add_argument("--c3-gb", type=float, default=60.0, help="size of the C3/C5 file (0: skip that leg)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo + --one-device: rehearse the N-rank sequence on a one-GPU box")
@@ -449,11 +453,11 @@ def main():
             return f.decode_span_device(vs, ve, timing=timing, digest=digest)
 
         for _ in range(args.warmup):
-            step(timing=False)
+            step(timing=args.serial)
         barrier()
         t = time.perf_counter()
         for _ in range(args.steps):
-            step(timing=False)  # production launch order (phase A / phase B overlapped), no events
+            step(timing=args.serial)  # production launch order (phase A / phase B overlapped), no events
         barrier()
         elapsed = time.perf_counter() - t
         # untimed measurement passes: every launch on one stream between its own
@@ -508,6 +512,7 @@ def main():
                 "scaling": "weak",
                 "vs_baseline": None,
                 "dtype": "u8",
+                "launch_order": "serial (measurement)" if args.serial else "overlapped (production)",
                 "data": "synthetic (tools/gen_synth_bam.c: Illumina-like qualities, zlib level 5 BGZF), "
                         "generated on the box",
                 "config": {"workload": ("C2: synthetic 10M x 150bp paired-end coordinate-sorted BAM" if world == 1

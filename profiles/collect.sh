@@ -6,6 +6,8 @@
 # then summarises everything into $OUT/summary.json (profiles/summarize.py).
 # Only the C2 headline runs under the profiler (--no-extra): the side
 # measurements would add launches of other sizes to the per-kernel averages.
+# --serial: every step in the measurement launch order (one stream), so the
+# per-kernel averages are the kernel durations bench.py's roofline uses.
 # Usage (from the repo root on the box): bash profiles/collect.sh <tag> [bench args...]
 set -o pipefail
 TAG=${1:-r01}; shift
@@ -13,8 +15,8 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-BENCH="python3 $R/bench.py --no-cpu-baseline --no-extra --no-pmc $*"
-PMCB="python3 $R/bench.py --no-cpu-baseline --no-extra --no-pmc --steps 1 --warmup 0 $*"
+BENCH="python3 $R/bench.py --no-cpu-baseline --no-extra --no-pmc --serial $*"
+PMCB="python3 $R/bench.py --no-cpu-baseline --no-extra --no-pmc --serial --steps 1 --warmup 0 $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $BENCH \
   > $OUT/trace_bench.json 2> $OUT/trace.err || { echo "trace pass failed"; tail -5 $OUT/trace.err; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $PMCB \
