@@ -2442,6 +2442,7 @@ constexpr int kGuessLookahead = 4;  // plausible records required past a guess w
 constexpr uint64_t kRetry = ~0ull - 2;  // g[]: the candidate's walk failed, search on
 constexpr uint32_t kListPlausible = 0x80000000u;  // wcnt flag: the list came from a plausible() walk
 constexpr uint32_t kListCountMask = 0x7fffffffu;
+constexpr int kSpliceMax = 8;  // records a re-walk may take before joining the old list
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_rec_walk(ChainEnv E, const uint64_t* __restrict__ cand,
@@ -2459,6 +2460,52 @@ __global__ __launch_bounds__(256) void k_rec_walk(ChainEnv E, const uint64_t* __
   }
   const BlockInfo b = E.blocks[E.k0 + i];
   const uint64_t bend = b.ustart + b.isize;
+  if (validate && f != kForceEmpty && f != kNone && f >= b.ustart && f < bend) {
+    // The true entry usually joins the block's first (plausible) walk after a
+    // record or two: splice the records before the join onto the old list
+    // instead of re-walking the block -- a re-walk is one lane's chain of
+    // ~190 dependent loads (~0.2 ms per link round on C2).
+    const uint32_t oc = wcnt[i];
+    const uint32_t n_old = oc & kListCountMask;
+    if ((oc & kListPlausible) && n_old > 0 && n_old <= kListCap) {
+      uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
+      uint16_t pre[kSpliceMax];
+      uint32_t m = 0, j = 0;
+      uint64_t q = f;
+      bool merged = false, done = false;
+#pragma unroll
+      for (int k = 0; k <= kSpliceMax; ++k) {
+        if (!done) {
+          while (j < n_old && b.ustart + L[j] < q) ++j;
+          uint64_t nq = 0;
+          if (j < n_old && b.ustart + L[j] == q) {
+            merged = true;
+            done = true;
+          } else if (k == kSpliceMax || q >= bend || !plausible(E, q) || !chain_step<MODE>(E, q, &nq)) {
+            done = true;
+          } else {
+            pre[k] = (uint16_t)(q - b.ustart);
+            m = k + 1;
+            q = nq;
+          }
+        }
+      }
+      const uint32_t tail = n_old - j;
+      if (merged && m + tail <= kListCap) {
+        if (m < j) {
+          for (uint32_t k = 0; k < tail; ++k) L[m + k] = L[j + k];
+        } else if (m > j) {
+          for (uint32_t k = tail; k-- > 0;) L[m + k] = L[j + k];
+        }
+#pragma unroll
+        for (int k = 0; k < kSpliceMax; ++k)
+          if ((uint32_t)k < m) L[k] = pre[k];
+        g_out[i] = f;  // x_out[i] stands: the joined walk's exit
+        wcnt[i] = (m + tail) | kListPlausible;
+        return;
+      }
+    }
+  }
   if (validate && f != kForceEmpty && f != kNone) {
     // a link-round entry may itself come from a wrong walk upstream (fixed in
     // the same round): re-walk only if the chain from it is plausible to the
