@@ -298,10 +298,7 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
                                                      uint32_t* tab, uint32_t* cnt, uint16_t* sorted, uint32_t* sub,
                                                      int subcap) {
   const uint32_t lane = lane_id();
-  if (lane < 16) {
-    cnt[lane] = 0;
-    L.base[lane] = 0;
-  }
+  if (lane < 16) cnt[lane] = 0;
   wave_sync();
   for (int s = lane; s < nsym; s += 64) {
     const uint32_t l = lens[s];
@@ -336,15 +333,20 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
   const uint32_t rmask = (1u << root) - 1;
   const uint64_t ltmask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   bool any_long = false;
+  // next canonical rank per code length: wave-uniform, kept in registers (an
+  // LDS counter costs a dependent LDS round trip per length and group)
+  uint32_t basev[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) basev[q] = 0;
   for (int c0 = 0; c0 < nsym; c0 += 64) {
     const int s = c0 + (int)lane;
     const uint32_t l = s < nsym ? lens[s] : 0;
     uint32_t rank = 0;
+#pragma unroll
     for (uint32_t q = 1; q < 16; ++q) {
       const uint64_t m = __ballot(l == q);
-      if (m == 0) continue;
-      if (l == q) rank = L.base[q] + (uint32_t)__popcll(m & ltmask);
-      if (lane == 0) L.base[q] += (uint32_t)__popcll(m);
+      rank = l == q ? basev[q] + (uint32_t)__popcll(m & ltmask) : rank;
+      basev[q] += (uint32_t)__popcll(m);
     }
     if (l) {
       sorted[L.offs[l] + rank] = (uint16_t)s;
@@ -2442,7 +2444,6 @@ constexpr int kGuessLookahead = 4;  // plausible records required past a guess w
 constexpr uint64_t kRetry = ~0ull - 2;  // g[]: the candidate's walk failed, search on
 constexpr uint32_t kListPlausible = 0x80000000u;  // wcnt flag: the list came from a plausible() walk
 constexpr uint32_t kListCountMask = 0x7fffffffu;
-constexpr int kSpliceMax = 8;  // records a re-walk may take before joining the old list
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_rec_walk(ChainEnv E, const uint64_t* __restrict__ cand,
@@ -2452,6 +2453,25 @@ __global__ __launch_bounds__(256) void k_rec_walk(ChainEnv E, const uint64_t* __
                                                   bool validate) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nb = E.k1 - E.k0;
+  if (force) {
+    // A re-walk round forces a few blocks; each is one lane's chain of ~190
+    // dependent loads from HBM.  The whole wave first pulls every forced
+    // block of the wave (+ the lookahead past its end) into L2 with
+    // independent loads, so the chain then runs at L2 latency.
+    const uint64_t fi = i < nb ? force[i] : kNone;
+    uint64_t todo = __ballot(fi != kNone && fi != kForceEmpty);
+    uint32_t acc = 0;
+    const uint32_t lane = lane_id();
+    while (todo) {
+      const uint32_t src = (uint32_t)__ffsll((long long)todo) - 1;
+      todo &= todo - 1;
+      const BlockInfo wb = E.blocks[E.k0 + blockIdx.x * blockDim.x + (threadIdx.x & ~63u) + src];
+      const uint64_t lo = wb.ustart & ~127ull;
+      const uint64_t hi = min(wb.ustart + wb.isize + 4096, E.e_inf);
+      for (uint64_t a = lo + 128ull * lane; a < hi; a += 128ull * 64) acc += ldu32(E.u, a);
+    }
+    if (acc == 0x9e3779b9u && E.k0 == 0xffffffffu) atomicOr(overflow, 0u);  // keeps the loads (never true)
+  }
   if (i >= nb) return;
   uint64_t f = kNone;  // guess
   if (force) {
@@ -2460,52 +2480,6 @@ __global__ __launch_bounds__(256) void k_rec_walk(ChainEnv E, const uint64_t* __
   }
   const BlockInfo b = E.blocks[E.k0 + i];
   const uint64_t bend = b.ustart + b.isize;
-  if (validate && f != kForceEmpty && f != kNone && f >= b.ustart && f < bend) {
-    // The true entry usually joins the block's first (plausible) walk after a
-    // record or two: splice the records before the join onto the old list
-    // instead of re-walking the block -- a re-walk is one lane's chain of
-    // ~190 dependent loads (~0.2 ms per link round on C2).
-    const uint32_t oc = wcnt[i];
-    const uint32_t n_old = oc & kListCountMask;
-    if ((oc & kListPlausible) && n_old > 0 && n_old <= kListCap) {
-      uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
-      uint16_t pre[kSpliceMax];
-      uint32_t m = 0, j = 0;
-      uint64_t q = f;
-      bool merged = false, done = false;
-#pragma unroll
-      for (int k = 0; k <= kSpliceMax; ++k) {
-        if (!done) {
-          while (j < n_old && b.ustart + L[j] < q) ++j;
-          uint64_t nq = 0;
-          if (j < n_old && b.ustart + L[j] == q) {
-            merged = true;
-            done = true;
-          } else if (k == kSpliceMax || q >= bend || !plausible(E, q) || !chain_step<MODE>(E, q, &nq)) {
-            done = true;
-          } else {
-            pre[k] = (uint16_t)(q - b.ustart);
-            m = k + 1;
-            q = nq;
-          }
-        }
-      }
-      const uint32_t tail = n_old - j;
-      if (merged && m + tail <= kListCap) {
-        if (m < j) {
-          for (uint32_t k = 0; k < tail; ++k) L[m + k] = L[j + k];
-        } else if (m > j) {
-          for (uint32_t k = tail; k-- > 0;) L[m + k] = L[j + k];
-        }
-#pragma unroll
-        for (int k = 0; k < kSpliceMax; ++k)
-          if ((uint32_t)k < m) L[k] = pre[k];
-        g_out[i] = f;  // x_out[i] stands: the joined walk's exit
-        wcnt[i] = (m + tail) | kListPlausible;
-        return;
-      }
-    }
-  }
   if (validate && f != kForceEmpty && f != kNone) {
     // a link-round entry may itself come from a wrong walk upstream (fixed in
     // the same round): re-walk only if the chain from it is plausible to the
