@@ -2,6 +2,7 @@
 // classes on top of the gfx950 pipeline.  Host code here plans windows,
 // parses the header and copies results; every per-record / per-byte loop of
 // the hot path runs in hbam_kernels.hip.
+#include "hbam_mem.h"
 #include "hbam_host.h"
 
 #include <fcntl.h>
@@ -35,20 +36,19 @@ bool PinnedVec<T>::resize(size_t n) {
     return true;
   }
   size_t c = std::max(n, cap_ + cap_ / 2);
-  T* q = nullptr;
-  if (hipHostMalloc(reinterpret_cast<void**>(&q), std::max<size_t>(c, 1) * sizeof(T), hipHostMallocDefault) !=
-      hipSuccess)
-    return false;
+  void* q = nullptr;
+  size_t got = 0;
+  if (hbam::pinned_alloc(&q, std::max<size_t>(c, 1) * sizeof(T), &got) != hipSuccess) return false;
   if (p_ && n_) memcpy(q, p_, n_ * sizeof(T));
-  if (p_) (void)hipHostFree(p_);
-  p_ = q;
-  cap_ = c;
+  if (p_) hbam::pinned_free(p_, cap_ * sizeof(T));
+  p_ = static_cast<T*>(q);
+  cap_ = got / sizeof(T);
   n_ = n;
   return true;
 }
 template <typename T>
 void PinnedVec<T>::release() {
-  if (p_) (void)hipHostFree(p_);
+  if (p_) hbam::pinned_free(p_, cap_ * sizeof(T));
   p_ = nullptr;
   n_ = cap_ = 0;
 }

@@ -1,0 +1,100 @@
+// hbam_mem.cpp -- the block caches of hbam_mem.h.
+#include "hbam_mem.h"
+
+#include <map>
+#include <mutex>
+
+namespace hbam {
+namespace {
+
+// Blocks below kMinCached bytes are not worth caching (hipMalloc is cheap
+// for them); the caps bound what a process keeps after its splits close.
+constexpr size_t kMinCached = 1ull << 20;
+constexpr size_t kDevCap = 32ull << 30;     // of 288 GB HBM per MI355X
+constexpr size_t kPinnedCap = 8ull << 30;
+
+struct Cache {
+  std::mutex mu;
+  std::multimap<size_t, std::pair<void*, int>> blocks;  // size -> (pointer, device)
+  size_t total = 0;
+
+  // smallest cached block in [bytes, 2 * bytes] on `dev`
+  void* take(size_t bytes, int dev, size_t* got) {
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto it = blocks.lower_bound(bytes); it != blocks.end() && it->first <= 2 * bytes; ++it) {
+      if (it->second.second != dev) continue;
+      void* p = it->second.first;
+      *got = it->first;
+      total -= it->first;
+      blocks.erase(it);
+      return p;
+    }
+    return nullptr;
+  }
+  bool put(void* p, size_t bytes, int dev, size_t cap) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (total + bytes > cap) return false;
+    blocks.emplace(bytes, std::make_pair(p, dev));
+    total += bytes;
+    return true;
+  }
+};
+
+// never destroyed: blocks cached at exit go with the process (freeing them
+// from a static destructor could run after the HIP runtime is torn down)
+Cache& dev_cache() {
+  static Cache* c = new Cache();
+  return *c;
+}
+Cache& pinned_cache() {
+  static Cache* c = new Cache();
+  return *c;
+}
+
+int current_device() {
+  int d = 0;
+  return hipGetDevice(&d) == hipSuccess ? d : -1;
+}
+
+}  // namespace
+
+hipError_t dev_alloc(void** p, size_t bytes, size_t* got) {
+  if (bytes == 0) bytes = 1;
+  const int dev = current_device();
+  if (bytes >= kMinCached) {
+    if (void* q = dev_cache().take(bytes, dev, got)) {
+      *p = q;
+      return hipSuccess;
+    }
+  }
+  *got = bytes;
+  return hipMalloc(p, bytes);
+}
+
+void dev_free(void* p, size_t bytes) {
+  if (!p) return;
+  (void)hipDeviceSynchronize();  // queued work may still use it (hipFree waits too)
+  if (bytes >= kMinCached && dev_cache().put(p, bytes, current_device(), kDevCap)) return;
+  (void)hipFree(p);
+}
+
+hipError_t pinned_alloc(void** p, size_t bytes, size_t* got) {
+  if (bytes == 0) bytes = 1;
+  if (bytes >= kMinCached) {
+    if (void* q = pinned_cache().take(bytes, 0, got)) {
+      *p = q;
+      return hipSuccess;
+    }
+  }
+  *got = bytes;
+  return hipHostMalloc(p, bytes, hipHostMallocDefault);
+}
+
+void pinned_free(void* p, size_t bytes) {
+  if (!p) return;
+  (void)hipDeviceSynchronize();  // an async copy may still read or write it
+  if (bytes >= kMinCached && pinned_cache().put(p, bytes, 0, kPinnedCap)) return;
+  (void)hipHostFree(p);
+}
+
+}  // namespace hbam

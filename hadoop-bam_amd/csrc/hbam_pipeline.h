@@ -11,6 +11,7 @@
 // back counters.  There is no CPU fallback: any HIP failure is an error
 // returned to the caller.
 #pragma once
+#include "hbam_mem.h"
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -34,7 +35,7 @@ struct DevBuf {
     std::swap(n, o.n);
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) dev_free(p, n * sizeof(T));
     p = nullptr;
     n = 0;
   }
@@ -43,16 +44,17 @@ struct DevBuf {
   hipError_t grow(size_t count) {
     if (count <= n && p) return hipSuccess;
     const size_t c = count > 2 * n ? count : 2 * n;
-    T* q = nullptr;
-    hipError_t e = hipMalloc(reinterpret_cast<void**>(&q), c * sizeof(T));
+    void* q = nullptr;
+    size_t got = 0;
+    hipError_t e = dev_alloc(&q, c * sizeof(T), &got);
     if (e != hipSuccess) return e;
     if (p) {
       if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
       if ((e = hipMemcpy(q, p, n * sizeof(T), hipMemcpyDeviceToDevice)) != hipSuccess) return e;
-      (void)hipFree(p);
+      dev_free(p, n * sizeof(T));
     }
-    p = q;
-    n = c;
+    p = static_cast<T*>(q);
+    n = got / sizeof(T);
     return hipSuccess;
   }
   // grow-only (contents not preserved)
@@ -61,8 +63,13 @@ struct DevBuf {
     if (p) (void)hipDeviceSynchronize();  // queued work on any stream may still use it
     release();
     size_t c = count ? count : 1;
-    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), c * sizeof(T));
-    if (e == hipSuccess) n = c;
+    void* q = nullptr;
+    size_t got = 0;
+    hipError_t e = dev_alloc(&q, c * sizeof(T), &got);
+    if (e == hipSuccess) {
+      p = static_cast<T*>(q);
+      n = got / sizeof(T);
+    }
     return e;
   }
 };
