@@ -469,7 +469,7 @@ def main():
         # untimed measurement passes: every launch on one stream between its own
         # HIP events -> per-stage and per-kernel durations (the roofline)
         stats = [step(timing=True) for _ in range(3)]
-        check = step(timing=False, digest=True)  # untimed: the digest for the parity check
+        check = step(timing=args.serial, digest=True)  # untimed: the digest for the parity check
         mine = (0, 0, 0, 0, 0) if check is None else (int(check["records"]), int(check["inflated_bytes"]),
                                                        int(check["compressed_bytes"]), int(check["key_xor"]),
                                                        int(check["voff_sum"]))
