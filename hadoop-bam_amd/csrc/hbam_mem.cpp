@@ -71,10 +71,20 @@ hipError_t dev_alloc(void** p, size_t bytes, size_t* got) {
   return hipMalloc(p, bytes);
 }
 
+// the device a block lives on (the caller's current device may differ)
+int device_of(void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) return -1;
+  return a.device;
+}
+
 void dev_free(void* p, size_t bytes) {
   if (!p) return;
   (void)hipDeviceSynchronize();  // queued work may still use it (hipFree waits too)
-  if (bytes >= kMinCached && dev_cache().put(p, bytes, current_device(), kDevCap)) return;
+  if (bytes >= kMinCached) {
+    const int dev = device_of(p);
+    if (dev >= 0 && dev_cache().put(p, bytes, dev, kDevCap)) return;
+  }
   (void)hipFree(p);
 }
 

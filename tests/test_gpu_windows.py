@@ -259,3 +259,38 @@ def test_continuation_at_an_empty_block_is_eof():
             got = f.decode_all()
             assert_same_records(got, want)
             assert f.splitting_index(5) == s.splitting_index(5)
+
+
+def test_reopened_splits_reuse_cached_blocks(tmp_path):
+    """hbam_mem: the device and page-locked blocks a closed split frees are
+    handed to the next open in the process with their old contents.  Opening
+    different files in turn (short reads, long reads, windowed, batched) must
+    give the oracle's records every time -- nothing may rely on fresh memory."""
+    files = []
+    for n, mode in ((40000, "short"), (300, "long"), (25000, "short")):
+        data, _ = synth.make_bam(n, mode=mode, seed=77 + n)
+        p = tmp_path / f"r{n}.bam"
+        p.write_bytes(data)
+        s = orc.Stream(data)
+        rc, want = s.decode_all()
+        assert rc == 0
+        files.append((str(p), want, s.data))
+    for rnd in range(2):
+        for path, want, u in files:
+            for window, batch in ((0, 0), (200_000, 7000)):
+                with hbam.BamFile(path=path, window_bytes=window) as f:
+                    first = f.header()["first_record_voff"]
+                    if batch:
+                        parts, v = [], first
+                        while v < ALL:
+                            r = f.decode_span(v, ALL, max_records=batch)
+                            if len(r["key"]) == 0:
+                                break
+                            parts.append(r)
+                            v = r["next_voff"]
+                        got = {k: np.concatenate([p_[k] for p_ in parts]) for k in ("key", "voff", "pos", "flag")}
+                        for k in got:
+                            assert np.array_equal(got[k], want[k]), (rnd, path, window, k)
+                    else:
+                        got = f.decode_all()
+                        assert_same_records(got, want, u)
