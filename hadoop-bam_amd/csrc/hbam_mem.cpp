@@ -80,12 +80,17 @@ int device_of(void* p) {
 
 void dev_free(void* p, size_t bytes) {
   if (!p) return;
-  (void)hipDeviceSynchronize();  // queued work may still use it (hipFree waits too)
-  if (bytes >= kMinCached) {
-    const int dev = device_of(p);
-    if (dev >= 0 && dev_cache().put(p, bytes, dev, kDevCap)) return;
+  const int dev = bytes >= kMinCached ? device_of(p) : -1;
+  if (dev < 0) {
+    (void)hipFree(p);
+    return;
   }
-  (void)hipFree(p);
+  // queued work on the block's device may still use it (hipFree waits too)
+  const int cur = current_device();
+  if (cur != dev) (void)hipSetDevice(dev);
+  (void)hipDeviceSynchronize();
+  if (cur != dev && cur >= 0) (void)hipSetDevice(cur);
+  if (!dev_cache().put(p, bytes, dev, kDevCap)) (void)hipFree(p);
 }
 
 hipError_t pinned_alloc(void** p, size_t bytes, size_t* got) {
