@@ -12,7 +12,7 @@
 namespace hbam {
 
 namespace {
-constexpr uint32_t kInflateChunkBlocks = 16384;  // blocks per phase-A/B launch pair
+constexpr uint32_t kInflateChunkBlocks = 32768;  // blocks per phase-A/B launch pair (16 K: -0.7 %, 8 K: -4 % on C2)
 constexpr int kMaxChainIters = 64;
 constexpr int kMaxLinkFix = 4;        // re-walk rounds before the serial link
 constexpr int kMaxFreeStarts = 64;    // header candidates tried by a free-start locate
