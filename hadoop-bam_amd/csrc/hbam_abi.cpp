@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "hbam_deflate_api.h"
+#include "hbam_mem.h"
 #include "hbam_host.h"
 #include "hbam_launch.h"
 
@@ -211,6 +212,8 @@ void hbam_close(hbam_ctx* ctx) { delete ctx; }
 const char* hbam_last_error(hbam_ctx* ctx) { return ctx ? ctx->err.c_str() : g_open_err.c_str(); }
 
 void hbam_free(void* p) { free(p); }
+
+uint64_t hbam_release_cached_memory(void) { return hbam::release_cached(); }
 
 int hbam_bgzf_compress(const hbam_opts* opts, const void* data, uint64_t len, const uint32_t* block_lens,
                        uint64_t n_blocks, int32_t block_size, int32_t level, int32_t flags, uint8_t** out,

@@ -59,25 +59,35 @@ __device__ __forceinline__ uint64_t ldu64(const uint8_t* base, uint64_t off) {
 __global__ void k_bgzf_scan(const uint8_t* __restrict__ buf, uint64_t len, uint64_t base, uint64_t from,
                             uint64_t* __restrict__ cand, uint32_t cap, uint32_t* __restrict__ count) {
   // buf = first byte of the loaded range (16 B aligned, zero padded past
-  // len); 16 positions per thread from one 16 B load + the next word;
-  // candidates are reported in file coordinates (base + offset)
-  const uint64_t nc = (len + 15) / 16;
+  // len); 64 positions per thread from four 16 B loads + the next word.  A
+  // word without a 0x1f byte (nearly all of them) costs three VALU
+  // operations; the rare 0x1f bytes get the full header test.  Candidates
+  // are reported in file coordinates (base + offset).
+  const uint64_t nc = (len + 63) / 64;
   for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nc;
        t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint4 v = *reinterpret_cast<const uint4*>(buf + 16 * t);
-    const uint32_t w4 = *reinterpret_cast<const uint32_t*>(buf + 16 * t + 16);
-    const uint32_t w[5] = {v.x, v.y, v.z, v.w, w4};
+    const uint4* q = reinterpret_cast<const uint4*>(buf + 64 * t);
+    const uint4 v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3];
+    const uint32_t w16 = *reinterpret_cast<const uint32_t*>(buf + 64 * t + 64);
+    const uint32_t w[17] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
+                            v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w, w16};
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const uint32_t magic = __builtin_amdgcn_alignbyte(w[(s >> 2) + 1], w[s >> 2], s & 3);
-      if (magic != 0x04088b1fu) continue;
-      const uint64_t p = 16 * t + s;
-      if (p + 18 > len || base + p < from) continue;
-      const uint32_t xlen = ldu32(buf, p + 10) & 0xffffu;
-      const uint32_t sub = ldu32(buf, p + 12);
-      if (xlen != 6 || sub != 0x00024342u) continue;
-      const uint32_t i = atomicAdd(count, 1u);
-      if (i < cap) cand[i] = base + p;
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t x = w[k] ^ 0x1f1f1f1fu;
+      uint32_t hz = (x - 0x01010101u) & ~x & 0x80808080u;  // a byte of w[k] may be 0x1f (superset)
+      while (hz) {
+        const uint32_t byte = (uint32_t)__builtin_ctz(hz) >> 3;
+        hz &= hz - 1;
+        const uint32_t magic = __builtin_amdgcn_alignbyte(w[k + 1], w[k], byte);
+        if (magic != 0x04088b1fu) continue;
+        const uint64_t p = 64 * t + 4 * k + byte;
+        if (p + 18 > len || base + p < from) continue;
+        const uint32_t xlen = ldu32(buf, p + 10) & 0xffffu;
+        const uint32_t sub = ldu32(buf, p + 12);
+        if (xlen != 6 || sub != 0x00024342u) continue;
+        const uint32_t i = atomicAdd(count, 1u);
+        if (i < cap) cand[i] = base + p;
+      }
     }
   }
 }
@@ -2957,7 +2967,7 @@ hipError_t launch_bgzf_scan(const uint8_t* file, uint64_t buf_base, uint64_t lo,
   // allocated); candidates below lo are dropped
   (void)buf_base;
   const uint64_t a = lo & ~15ull;
-  const uint64_t nc = (hi - a + 15) / 16;
+  const uint64_t nc = (hi - a + 63) / 64;  // 64 B per thread and step
   hipLaunchKernelGGL(k_bgzf_scan, dim3(grid_for(nc, 256, 8192)), dim3(256), 0, s, file + a, hi - a, a, lo, cand,
                      cap, count);
   return hipGetLastError();

@@ -31,6 +31,14 @@ struct Cache {
     }
     return nullptr;
   }
+  // empties the cache into `out` (freed by the caller, outside the lock)
+  size_t drain(std::multimap<size_t, std::pair<void*, int>>* out) {
+    std::lock_guard<std::mutex> lk(mu);
+    out->swap(blocks);
+    const size_t t = total;
+    total = 0;
+    return t;
+  }
   bool put(void* p, size_t bytes, int dev, size_t cap) {
     std::lock_guard<std::mutex> lk(mu);
     if (total + bytes > cap) return false;
@@ -110,6 +118,19 @@ void pinned_free(void* p, size_t bytes) {
   (void)hipDeviceSynchronize();  // an async copy may still read or write it
   if (bytes >= kMinCached && pinned_cache().put(p, bytes, 0, kPinnedCap)) return;
   (void)hipHostFree(p);
+}
+
+size_t release_cached() {
+  std::multimap<size_t, std::pair<void*, int>> d, h;
+  size_t n = dev_cache().drain(&d) + pinned_cache().drain(&h);
+  const int cur = current_device();
+  for (auto& b : d) {
+    (void)hipSetDevice(b.second.second);
+    (void)hipFree(b.second.first);
+  }
+  if (cur >= 0) (void)hipSetDevice(cur);
+  for (auto& b : h) (void)hipHostFree(b.second.first);
+  return n;
 }
 
 }  // namespace hbam

@@ -25,4 +25,7 @@ void dev_free(void* p, size_t bytes);
 hipError_t pinned_alloc(void** p, size_t bytes, size_t* got);
 void pinned_free(void* p, size_t bytes);
 
+// Every cached block back to the HIP runtime; returns the bytes released.
+size_t release_cached();
+
 }  // namespace hbam

@@ -73,6 +73,7 @@ def _sig(name, res, args):
 
 
 _sig("hbam_abi_version", i32, [])
+_sig("hbam_release_cached_memory", u64, [])
 _sig("hbam_open", C.c_int, [C.c_char_p, C.POINTER(Opts), C.POINTER(P)])
 _sig("hbam_open_mem", C.c_int, [P, u64, C.POINTER(Opts), C.POINTER(P)])
 _sig("hbam_open_bgzf", C.c_int, [P, u64, C.POINTER(Opts), C.POINTER(P)])
@@ -179,6 +180,11 @@ def bgzf_compress(data, block_lens=None, block_size=HTSJDK_BLOCK_SIZE, level=5, 
         return C.string_at(out, olen.value)
     finally:
         _L.hbam_free(out)
+
+
+def release_cached_memory():
+    """hbam_release_cached_memory: the process-wide block caches back to HIP (bytes)."""
+    return int(_L.hbam_release_cached_memory())
 
 
 def get_key0(ref_idx, start0):

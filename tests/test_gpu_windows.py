@@ -294,3 +294,10 @@ def test_reopened_splits_reuse_cached_blocks(tmp_path):
                     else:
                         got = f.decode_all()
                         assert_same_records(got, want, u)
+    # the closed splits left their blocks in the process caches; releasing
+    # them empties the caches, and a later open allocates afresh
+    assert hbam.release_cached_memory() > 0
+    assert hbam.release_cached_memory() == 0
+    path, want, u = files[0]
+    with hbam.BamFile(path=path) as f:
+        assert_same_records(f.decode_all(), want, u)
