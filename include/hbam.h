@@ -109,8 +109,8 @@ int32_t hbam_abi_version(void);
 /* Device (HBM) and page-locked host blocks freed by closed contexts stay in
  * a process-wide cache for the next split of the process (an executor or a
  * reused task JVM reads many); this returns them to the HIP runtime.  Call
- * it with no context open (no JNI counterpart: a maintainer may bind it to
- * the task's cleanup).  Returns the bytes released. */
+ * it with no context open (HbamNative.releaseCachedMemory; no reference
+ * counterpart).  Returns the bytes released. */
 uint64_t hbam_release_cached_memory(void);
 
 int hbam_header(hbam_ctx *ctx, hbam_header_info *out);

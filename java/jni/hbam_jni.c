@@ -339,3 +339,5 @@ JNIEXPORT jlong FN(murmurhash3)(JNIEnv *env, jclass c, jbyteArray key, jint seed
   (*env)->ReleaseByteArrayElements(env, key, k, JNI_ABORT);
   return (jlong)h;
 }
+
+JNIEXPORT jlong FN(releaseCachedMemory)(JNIEnv *env, jclass c) { return (jlong)hbam_release_cached_memory(); }

@@ -131,4 +131,11 @@ public final class HbamNative {
 
   /** hbam_murmurhash3: util/MurmurHash3.murmurhash3(byte[], int). */
   public static native long murmurhash3(byte[] key, int seed);
+
+  /**
+   * hbam_release_cached_memory: the HBM and page-locked blocks closed readers
+   * left in the library's process-wide cache go back to the HIP runtime (no
+   * reference counterpart; bind to the executor's shutdown).  Bytes released.
+   */
+  public static native long releaseCachedMemory();
 }
