@@ -2578,6 +2578,13 @@ __global__ __launch_bounds__(64) void k_rec_search(ChainEnv E, const uint64_t* _
   const uint32_t lane = lane_id();
   const BlockInfo b = E.blocks[E.k0 + i];
   const uint64_t bend = b.ustart + b.isize;
+  {  // the walks below are dependent-load chains: pull the block (+ the
+     // lookahead past its end) into L2 first with independent loads
+    uint32_t acc = 0;
+    const uint64_t hi = min(bend + 4096, E.e_inf);
+    for (uint64_t a = (b.ustart & ~127ull) + 128ull * lane; a < hi; a += 128ull * 64) acc += ldu32(E.u, a);
+    if (acc == 0x9e3779b9u && E.k0 == 0xffffffffu) atomicOr(overflow, 0u);  // keeps the loads (never true)
+  }
   uint64_t g = kNone, x = kNone;
   for (uint64_t c0 = cand[i] + 1; c0 < bend && g == kNone; c0 += 64) {
     const uint64_t p = c0 + lane;
