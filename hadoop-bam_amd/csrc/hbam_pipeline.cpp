@@ -12,6 +12,7 @@
 namespace hbam {
 
 namespace {
+constexpr uint32_t kStreamInflateBlocks = 8192;  // run_streamed: blocks per inflate call
 constexpr uint32_t kInflateChunkBlocks = 32768;  // blocks per phase-A/B launch pair (16 K: -0.7 %, 8 K: -4 % on C2)
 constexpr int kMaxChainIters = 64;
 constexpr int kMaxLinkFix = 4;        // re-walk rounds before the serial link
@@ -321,7 +322,7 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
   inflated_.clear();
   total_u_ = 0;
   uint64_t lo = base_;
-  uint32_t nb = 0;
+  uint32_t nb = 0, queued = 0;  // blocks located / handed to inflate
   for (uint64_t k = 0; k < np; ++k) {
     HIPCHK(hipEventSynchronize(copy_ev_[k]));
     const bool last = k + 1 == np;
@@ -336,9 +337,14 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
       HIPCHK(du_.grow(total_u_ + kUPad));
       HIPCHK(hout_.grow(nb + nnew + 1));
       inflated_.resize(nb + nnew, 0);
-      rc = inflate(nb, nb + nnew, true, false);
-      if (rc != kOk) return rc;
       nb += nnew;
+    }
+    // inflate in launches of >= kStreamInflateBlocks blocks: a piece's few
+    // thousand blocks alone would leave most CUs idle in each round's tail
+    if (nb > queued && (nb - queued >= kStreamInflateBlocks || last)) {
+      rc = inflate(queued, nb, true, false);
+      if (rc != kOk) return rc;
+      queued = nb;
     }
     lo = tail;
   }
