@@ -294,11 +294,6 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
   HIPCHK(hipSetDevice(device_));
   piece = std::max<uint64_t>(piece, 1ull << 20);
   const uint64_t np = std::max<uint64_t>(1, (len + piece - 1) / piece);
-  while (copy_ev_.size() < np) {
-    hipEvent_t e;
-    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    copy_ev_.push_back(e);
-  }
   // capacity up front, so that nothing reallocates under queued work (grow()
   // still handles a file that outruns the estimates, at the cost of a wait)
   HIPCHK(dblocks_.grow(len / 16384 + 4096));
@@ -312,25 +307,30 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
   }
   HIPCHK(hipDeviceSynchronize());
 
-  HIPCHK(hipEventRecord(ev_[6], stream_copy_));
-  for (uint64_t k = 0; k < np; ++k) {
+  // Piece k's copy and its locate run in order on stream_copy_, the inflate
+  // of located blocks on the inflate streams.  (With locate on stream_loc_,
+  // which shares a hardware queue with stream_ at GPU_MAX_HW_QUEUES = 4, every
+  // locate waited behind the queued inflates: copy and decode serialized.)
+  auto queue_copy = [&](uint64_t k) -> int {
     const uint64_t o = k * piece, sz = std::min(piece, len - o);
     HIPCHK(hipMemcpyAsync(dfile_ + o, data + o, sz, hipMemcpyHostToDevice, stream_copy_));
-    HIPCHK(hipEventRecord(copy_ev_[k], stream_copy_));
-  }
+    return kOk;
+  };
+  HIPCHK(hipEventRecord(ev_[6], stream_copy_));
+  if (int rc0 = queue_copy(0)) return rc0;
   hblocks_.clear();
   inflated_.clear();
   total_u_ = 0;
   uint64_t lo = base_;
   uint32_t nb = 0, queued = 0;  // blocks located / handed to inflate
   for (uint64_t k = 0; k < np; ++k) {
-    HIPCHK(hipEventSynchronize(copy_ev_[k]));
     const bool last = k + 1 == np;
     const uint64_t hi = base_ + (last ? len : (k + 1) * piece);
     uint32_t nnew = 0;
     uint64_t tail = hi;
-    int rc = locate_range(lo, hi, !last, false, nb, total_u_, stream_loc_, &nnew, &tail);
+    int rc = locate_range(lo, hi, !last, false, nb, total_u_, stream_copy_, &nnew, &tail);
     if (rc != kOk) return rc;
+    if (!last && (rc = queue_copy(k + 1)) != kOk) return rc;  // on the wire while piece k inflates
     if (nnew) {
       const BlockInfo& e = hblocks_[nb + nnew - 1];
       total_u_ = e.ustart + e.isize;
