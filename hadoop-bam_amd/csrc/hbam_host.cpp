@@ -366,6 +366,29 @@ int BamFile::decode_step(Carry from, uint64_t vend, hbam::ChainMode mode, bool d
     int rc = load_window(c.coff, hi, false, host_only);
     if (rc != kOk) return rc;
     hbam::Pipeline& p = *pipe_;
+    // the split goes on past this window: start the next window's new bytes
+    // on their way to HBM while this one decodes (Pipeline::stage)
+    if (src_.host && win_hi_ < src_.size && (!clamp || win_hi_ < (vend >> 16) + 0x20000)) {
+      // the next window starts at the record this one cannot finish (a few
+      // blocks before win_hi_), so it ends up to that tail short of
+      // win_hi_ + span_w: stage that much less, or the bytes past its end
+      // would be copied again by the window after it
+      const uint64_t s_lo = win_hi_;
+      const uint64_t tail = std::min<uint64_t>(span_w / 2, 4 * 65536);
+      uint64_t s_hi = std::min(src_.size, s_lo + span_w - tail);
+      if (clamp) s_hi = std::min(s_hi, std::max((vend >> 16) + 0x20000, s_lo));
+      const bool resident = src_.dev.p && s_lo >= src_.dev_lo && s_hi <= src_.dev_hi;
+      if (s_hi > s_lo && !resident) {
+        rc = p.stage(src_.host, s_lo, s_hi);
+        if (rc != kOk) {
+          err_ = p.error();
+          return rc;
+        }
+        if (s_lo != staged_lo_ || s_hi != staged_hi_) src_.bytes_read += s_hi - s_lo;
+        staged_lo_ = s_lo;
+        staged_hi_ = s_hi;
+      }
+    }
     const auto& B = p.blocks();
     if (B.empty()) {
       if (p.at_eof()) return kOk;  // no complete block left

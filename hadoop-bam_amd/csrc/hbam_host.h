@@ -152,6 +152,7 @@ class BamFile {
   Source src_;
   std::unique_ptr<hbam::Pipeline> pipe_;
   uint64_t win_lo_ = ~0ull, win_hi_ = 0;  // the loaded window
+  uint64_t staged_lo_ = 0, staged_hi_ = 0;  // the range handed to Pipeline::stage last
   bool win_free_ = false;
   uint64_t window_bytes_ = kDefaultWindowBytes;
   int32_t n_ref_ = 0;

@@ -2,6 +2,8 @@
 // read pipeline (see hbam_pipeline.h).
 #include "hbam_pipeline.h"
 
+#include <thread>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -39,6 +41,7 @@ Pipeline::Pipeline(int device) : device_(device) {
 }
 
 Pipeline::~Pipeline() {
+  if (stage_thr_.joinable()) stage_thr_.join();
   (void)hipSetDevice(device_);
   (void)hipDeviceSynchronize();
   for (auto& e : ev_) (void)hipEventDestroy(e);
@@ -81,8 +84,24 @@ int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof
   HIPCHK(own_file_.reserve(len + 16 + kFilePad));
   dfile_ = own_file_.p + (base & 15);
   if (keep) HIPCHK(hipMemcpyAsync(dfile_, old, keep, hipMemcpyDeviceToDevice, stream_));
-  if (len > keep) HIPCHK(hipMemcpyAsync(dfile_ + keep, data + keep, len - keep, hipMemcpyHostToDevice, stream_));
-  if (host_bytes) *host_bytes = len - keep;
+  uint64_t host = 0;
+  if (len > keep) {
+    // [a, b): the part of the new bytes a stage() copy already brought over
+    const uint64_t a = std::max(base + keep, stage_lo_), b = std::min(base + len, stage_hi_);
+    if (stage_hi_ > stage_lo_ && a < b) {
+      if (int rc = stage_wait()) return rc;
+      if (a > base + keep)
+        HIPCHK(hipMemcpyAsync(dfile_ + keep, data + keep, a - base - keep, hipMemcpyHostToDevice, stream_));
+      HIPCHK(hipMemcpyAsync(dfile_ + (a - base), stage_.p + (a - stage_lo_), b - a, hipMemcpyDeviceToDevice, stream_));
+      if (base + len > b)
+        HIPCHK(hipMemcpyAsync(dfile_ + (b - base), data + (b - base), base + len - b, hipMemcpyHostToDevice, stream_));
+      host = len - keep - (b - a);
+    } else {
+      HIPCHK(hipMemcpyAsync(dfile_ + keep, data + keep, len - keep, hipMemcpyHostToDevice, stream_));
+      host = len - keep;
+    }
+  }
+  if (host_bytes) *host_bytes = host;
   HIPCHK(hipMemsetAsync(dfile_ + len, 0, kFilePad, stream_));
   HIPCHK(hipStreamSynchronize(stream_));
   flen_ = len;
@@ -92,6 +111,39 @@ int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof
   hblocks_.clear();
   inflated_.clear();
   total_u_ = 0;
+  return kOk;
+}
+
+int Pipeline::stage_wait() {
+  if (stage_thr_.joinable()) stage_thr_.join();
+  const hipError_t e = stage_err_;
+  stage_err_ = hipSuccess;
+  if (e != hipSuccess) {
+    stage_lo_ = stage_hi_ = 0;
+    return hip_check(e, "staged host->HBM copy");
+  }
+  return kOk;
+}
+
+int Pipeline::stage(const uint8_t* host, uint64_t lo, uint64_t hi) {
+  HIPCHK(hipSetDevice(device_));
+  if (hi <= lo || (lo == stage_lo_ && hi == stage_hi_)) return kOk;  // nothing new to stage
+  if (int rc = stage_wait()) return rc;
+  HIPCHK(stage_.reserve(hi - lo));  // growing it waits for the device
+  // A copy from pageable memory (the mapped file) returns only when it is
+  // done, so a helper thread issues it: the caller goes on queueing this
+  // window's decode while the next window's bytes cross the link.
+  uint8_t* dst = stage_.p;
+  const int dev = device_;
+  hipStream_t cs = stream_copy_;
+  stage_thr_ = std::thread([this, dst, host, lo, hi, dev, cs]() {
+    hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess) e = hipMemcpyAsync(dst, host + lo, hi - lo, hipMemcpyHostToDevice, cs);
+    if (e == hipSuccess) e = hipStreamSynchronize(cs);
+    stage_err_ = e;
+  });
+  stage_lo_ = lo;
+  stage_hi_ = hi;
   return kOk;
 }
 
@@ -292,6 +344,7 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
   if (!dfile_ || dfile_ != own_file_.p || len != flen_ || base_ != 0 || !at_eof_)
     return fail(kErrState, "run_streamed needs the whole file loaded in one window");
   HIPCHK(hipSetDevice(device_));
+  if (int rc = stage_wait()) return rc;  // a staged copy shares stream_copy_
   piece = std::max<uint64_t>(piece, 1ull << 20);
   const uint64_t np = std::max<uint64_t>(1, (len + piece - 1) / piece);
   // capacity up front, so that nothing reallocates under queued work (grow()

@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "hbam_device.h"
@@ -113,6 +114,11 @@ class Pipeline {
   // of the new range, that prefix moves device to device and only the rest
   // crosses PCIe; *host_bytes (optional) = the bytes copied from `data`.
   int load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof, uint64_t* host_bytes = nullptr);
+  // Start copying file bytes [lo, hi) (host pointer `host` = file offset 0)
+  // into a staging buffer on the copy stream; a later load() takes the part
+  // of its window inside [lo, hi) from there (device-to-device) instead of
+  // the host, so a window's H2D overlaps the previous window's decode.
+  int stage(const uint8_t* host, uint64_t lo, uint64_t hi);
   // Use device-resident file bytes [base, base + len) (readable for kFilePad
   // bytes past len).
   int attach_device(const uint8_t* dptr, uint64_t len, uint64_t base, bool at_eof);
@@ -220,6 +226,11 @@ class Pipeline {
   uint8_t* dfile_ = nullptr;
   DevBuf<uint8_t> own_file_;  // window bytes copied from the host (+ kFilePad zeros)
   DevBuf<uint8_t> own_spare_;  // the other buffer of the pair (a window's kept prefix moves across)
+  DevBuf<uint8_t> stage_;      // stage(): file bytes [stage_lo_, stage_hi_) in flight / landed
+  uint64_t stage_lo_ = 0, stage_hi_ = 0;
+  std::thread stage_thr_;      // issues the staged copy (pageable copies block their caller)
+  hipError_t stage_err_ = hipSuccess;
+  int stage_wait();            // the staged copy done (its error, if any)
   uint64_t flen_ = 0, base_ = 0;
   bool at_eof_ = true;
   uint64_t window_end_ = 0;
