@@ -31,8 +31,7 @@ Pipeline::Pipeline(int device) : device_(device) {
   if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&stream_b_, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&stream_t_, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&stream_copy_, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&stream_loc_, hipStreamNonBlocking) != hipSuccess)
+      hipStreamCreateWithFlags(&stream_copy_, hipStreamNonBlocking) != hipSuccess)
     err_ = "hipStreamCreate failed";
   for (auto& e : ev_) (void)hipEventCreate(&e);
   for (auto& e : sync_ev_) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -50,7 +49,7 @@ Pipeline::~Pipeline() {
   for (auto& e : hdone_ev_) (void)hipEventDestroy(e);
   for (auto& e : tev_) (void)hipEventDestroy(e);
   for (auto& e : copy_ev_) (void)hipEventDestroy(e);
-  for (hipStream_t s : {stream_b_, stream_t_, stream_copy_, stream_loc_, stream_})
+  for (hipStream_t s : {stream_b_, stream_t_, stream_copy_, stream_})
     if (s) (void)hipStreamDestroy(s);
 }
 
@@ -361,7 +360,7 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
   HIPCHK(hipDeviceSynchronize());
 
   // Piece k's copy and its locate run in order on stream_copy_, the inflate
-  // of located blocks on the inflate streams.  (With locate on stream_loc_,
+  // of located blocks on the inflate streams.  (With locate on its own stream,
   // which shares a hardware queue with stream_ at GPU_MAX_HW_QUEUES = 4, every
   // locate waited behind the queued inflates: copy and decode serialized.)
   auto queue_copy = [&](uint64_t k) -> int {

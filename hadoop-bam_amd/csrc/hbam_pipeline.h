@@ -219,7 +219,6 @@ class Pipeline {
   int device_ = 0;
   hipStream_t stream_ = nullptr;
   hipStream_t stream_copy_ = nullptr;  // run_streamed: host->HBM pieces
-  hipStream_t stream_loc_ = nullptr;   // run_streamed: per-piece block discovery
   std::vector<hipEvent_t> copy_ev_;
   std::string err_;
 
