@@ -7,21 +7,27 @@ discovery -> inflate (Huffman phase + LZ77 phase) -> record-boundary chain ->
 fused field decode + sort keys + voffs into SoA columns in HBM
 (hbam_decode_span_device, the BAMRecordReader path).
 
-The file: N ranks write one BAM together.  Rank r generates records
-[r*R, (r+1)*R) of an N*R-record model (tools/gen_synth_bam.c, zlib level 5,
-BGZF runs ending at record boundaries, header on rank 0, EOF block on the
-last rank) and writes them at its offset of a shared file.  At N=1 this is
-config C2 (10M x 150 bp paired-end, ~1.4 GB compressed); at N>1 a C3-shaped
-file of N*C2 bytes.  Each rank then plans its split exactly as Hadoop-BAM
-does (FileInputFormat byte range -> BAMSplitGuesser -> empty-split merge,
-hbam/shard.py), copies only its split's bytes to its GPU, and decodes it:
-weak scaling, no data-path collective (metadata all_gathers only).
+Workloads (config.workload):
+  c2  (default at --gpus 1): BASELINE config 2, synthetic 10M x 150 bp
+      paired-end (~1.4 GB compressed).  With N ranks: N x C2 records in one
+      file, one split per rank (weak scaling) -- the side leg of an N>1 run.
+  c3  (default at --gpus N>1): BASELINE config 3, ONE ~60 GB BAM split by
+      BGZF byte ranges across the N ranks exactly as Hadoop-BAM plans it
+      (FileInputFormat ranges -> BAMSplitGuesser -> empty-split merge,
+      hbam/shard.py): strong scaling, total work fixed.  The same run gathers
+      every rank's .splitting-bai entries at g = 4096 on rank 0 (config 5,
+      SURVEY 8e) and checks them and an order-sensitive decode digest against
+      the oracle run over the whole file on the host's cores.
 
-Prints ONE JSON line (rank 0).  Side legs at N=1 (rank 0): CPU baseline
-(the oracle at 1 thread and on every host core), in-session PMC traffic of
+Multi-rank runs write the file together (each rank generates its segments),
+and each rank copies only its split's bytes to its GPU; the only collectives
+are metadata all_gathers and the max-over-ranks timing all_reduce.
+
+Prints ONE JSON line (rank 0).  Side legs at N=1 (rank 0): CPU baseline (the
+oracle at 1 thread and on every usable host core), in-session PMC traffic of
 the dominant kernel (rocprofv3 child runs), the drop-in call end to end
-(hbam_open -> hbam_decode_span batches -> pinned host columns), the C3 / C5
-configs at 60 GB, C4 long reads, write-path legs.
+(hbam_open -> hbam_decode_span batches -> pinned host columns), C3 / C5 at
+60 GB, C4 long reads, write-path legs.
 """
 import argparse
 import glob
@@ -254,67 +260,192 @@ def pinned_host_leg(path, records):
             "records_per_s": round(records / dt, 1), "compressed_GBps_h2d": round(os.path.getsize(path) / dt / 1e9, 3)}
 
 
-def c3_c5_leg(target_gb, cores):
-    """C3 / C5 at their stated size: a >= target_gb BAM (header segment +
-    one C2-sized record segment repeated + EOF block: the repeats keep the
-    build to seconds; every byte is still read, inflated and decoded).
-    C3: decoded with the file streamed host->HBM window by window (4 GiB
-    windows, default hbam_opts), then again resident after a prefetch.
-    C5: .splitting-bai at g=4096 over it (resident).  Both checked against
-    the oracle run over BGZF ranges on every host core."""
+C3_SEG_RECORDS = 5_000_000  # records per segment of the C3 file
+C3_BODIES = 3                # distinct body segments (each repeated an odd number of times)
+
+
+def c3_sequence(k):
+    """Order of the body segments of the C3 file: k (about) copies spread
+    over C3_BODIES distinct bodies, each an odd number of times, in a fixed
+    shuffled order (no period: an error repeated in every copy of a body still
+    moves the order-sensitive digests)."""
+    import random
+    counts = [k // C3_BODIES + (1 if j < k % C3_BODIES else 0) for j in range(C3_BODIES)]
+    counts = [c if c % 2 else c + 1 for c in counts]
+    seq = [j + 1 for j in range(C3_BODIES) for _ in range(counts[j])]
+    random.Random(0x4842).shuffle(seq)
+    return seq
+
+
+def build_c3_file(path, D, target_gb, seg_records=C3_SEG_RECORDS):
+    """The C3 BAM (~target_gb): a header segment then body segments (records
+    [jS, (j+1)S) of a (1 + C3_BODIES) * S record model, S = C3_SEG_RECORDS)
+    in c3_sequence order, then the EOF block.  Rank r generates the distinct
+    segments j with j % world == r and writes every copy of them."""
     import numpy as np
-    import hbam
     from hbam import synth
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import orc
-    r = 10_000_000
     t = time.time()
-    head, hi = synth.make_bam_segment(2 * r, 0, r, with_header=True, eof_block=False, seed=SEED + 3)
-    body, bi = synth.make_bam_segment(2 * r, r, 2 * r, with_header=False, eof_block=False, seed=SEED + 3)
-    k = max(1, -(-(int(target_gb * 1e9) - head.nbytes) // body.nbytes))
-    size = head.nbytes + k * body.nbytes + len(BGZF_EOF)
-    path = os.path.join(scratch_dir(), f"hbam_c3_{os.getpid()}.bam")
-    try:
+    n_model = (1 + C3_BODIES) * seg_records
+    mine = {}
+    for j in range(1 + C3_BODIES):
+        if j % D.world == D.rank:
+            mine[j] = synth.make_bam_segment(n_model, j * seg_records, (j + 1) * seg_records,
+                                             with_header=j == 0, eof_block=False, seed=SEED + 3)
+    sizes = {}
+    for part in D.all_gather({j: (int(a.nbytes), int(i["uncompressed"])) for j, (a, i) in mine.items()}):
+        sizes.update(part)
+    body_mean = sum(sizes[j][0] for j in range(1, 1 + C3_BODIES)) / C3_BODIES
+    k = max(1, int(-(-(target_gb * 1e9 - sizes[0][0]) // body_mean)))
+    seq = c3_sequence(k)
+    place = [(0, 0)]
+    off = sizes[0][0]
+    for j in seq:
+        place.append((j, off))
+        off += sizes[j][0]
+    size = off + len(BGZF_EOF)
+    if D.rank == 0:
         with open(path, "wb") as fh:
             fh.truncate(size)
-        fd = os.open(path, os.O_WRONLY)
-        try:
-            pwrite_all(fd, head, 0)
-            for i in range(k):
-                pwrite_all(fd, body, head.nbytes + i * body.nbytes)
-            pwrite_all(fd, np.frombuffer(BGZF_EOF, np.uint8), head.nbytes + k * body.nbytes)
-        finally:
-            os.close(fd)
-        del head, body
-        n_rec = r * (k + 1)
-        u_tot = hi["uncompressed"] + k * bi["uncompressed"]
-        build_s = time.time() - t
-        log(f"[c3] built {size} B ({n_rec} records) in {build_s:.1f}s")
-        res = {"file": {"compressed_bytes": size, "uncompressed_bytes": u_tot, "records": n_rec,
-                        "layout": f"header segment + 1 segment x {k} + EOF (10M records each)",
-                        "build_seconds": round(build_s, 1)}}
-        with hbam.BamFile(path=path) as f:
-            first = f.header()["first_record_voff"]
+    D.barrier()
+    fd = os.open(path, os.O_WRONLY)
+    try:
+        for j, o in place:
+            if j in mine:
+                pwrite_all(fd, mine[j][0], o)
+        if D.rank == 0:
+            pwrite_all(fd, np.frombuffer(BGZF_EOF, np.uint8), off)
+    finally:
+        os.close(fd)
+    del mine
+    D.barrier()
+    u = sizes[0][1] + sum(sizes[j][1] for j in seq)
+    counts = {j: seq.count(j) for j in range(1, 1 + C3_BODIES)}
+    meta = {"compressed_bytes": size, "uncompressed_bytes": u, "records": seg_records * (1 + len(seq)),
+            "layout": f"header segment + {len(seq)} body segments of {seg_records} records: "
+                      f"{C3_BODIES} distinct bodies x {counts} copies (odd), shuffled order, + EOF",
+            "build_seconds": round(time.time() - t, 1)}
+    log(f"[rank {D.rank}] C3 file {size} B, {meta['records']} records ({meta['build_seconds']}s)")
+    return meta
+
+
+def compose_digests(parts):
+    """[(records, key_digest, voff_digest)] of consecutive spans -> the whole
+    run's (records, key_digest, voff_digest) (hbam.h HBAM_DIGEST_P)."""
+    n, kd, vd = 0, 0, 0
+    for k, a, b in parts:
+        w = pow(0x100000001B3, int(k), 1 << 64)
+        kd = (kd * w + int(a)) & ALL
+        vd = (vd * w + int(b)) & ALL
+        n += int(k)
+    return n, kd, vd
+
+
+def roofline_of(stats, world=1):
+    """The roofline object of the dominant kernel from measurement passes
+    (every inflate launch between its own HIP events on one stream: kernel
+    durations, as rocprofv3 reports them)."""
+    st = stats[-1]
+    n_launch = max(1, st["inflate_launches"])
+    avg = lambda k: sum(s_[k] for s_ in stats) / len(stats)
+    kt = {"hbam::k_inflate_huff": avg("ms_huff"), "hbam::k_inflate_lz77": avg("ms_lz77"),
+          "hbam::k_huff_tables": avg("ms_tables")}
+    dom = max(kt, key=kt.get)
+    dom_ms = kt[dom]
+    if dom != "hbam::k_inflate_lz77":  # phase A launches once per round of each chunk
+        n_launch *= INFLATE_ROUNDS
+    b_alg = st["compressed_bytes"] + st["inflated_bytes"] + SOA_BYTES_PER_RECORD * st["records"]
+    achieved = b_alg / (dom_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "launches_per_pass": n_launch, "avg_launch_ms": round(dom_ms / n_launch, 4),
+            "alg_bytes_per_launch": int(b_alg / n_launch),
+            "alg_bytes_rule": "(C + U + 37 N) of the pass / launches (SURVEY 8d)" +
+                              ("" if world == 1 else ", rank 0's split"),
+            "kernel_ms_per_pass": {k: round(v, 3) for k, v in kt.items()},
+            "whole_pass": {"achieved": round(b_alg / (st["ms_total"] * 1e-3) / 1e9, 2),
+                           "frac": round(b_alg / (st["ms_total"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}}
+
+
+def run_c3(D, target_gb, steps, warmup, host_leg=False):
+    """C3 / C5 (strong scaling): the ranks split ONE ~60 GB BAM by BGZF byte
+    ranges (hbam/shard.py: BAMInputFormat.addProbabilisticSplits on the GPU
+    guesser), prefetch their split's bytes to HBM and time `steps` decodes of
+    it; then, untimed: one measurement pass (stage / kernel times), a digest
+    pass (order-sensitive key / voff digests composed in split order), and the
+    .splitting-bai entries of each split at g = 4096 from the global record
+    ordinals (hbam_splitting_entries), gathered on rank 0.  Rank 0 checks
+    both against the oracle run over the whole file on every usable core.
+    host_leg (N=1): first a decode with the windows copied from the mapped
+    file inside the timed call (PCIe-inclusive)."""
+    import numpy as np
+    import hbam
+    from hbam import shard
+    path = os.path.join(scratch_dir(), f"hbam_c3_{D.tag}.bam")
+    try:
+        meta = build_c3_file(path, D, target_gb)
+        size = meta["compressed_bytes"]
+        res = {"file": meta}
+        f = hbam.BamFile(path=path, device=D.device)
+        first = f.header()["first_record_voff"]
+        split = shard.ShardedBamReader(f, size, first, D.rank, D.world, D.all_gather).split()
+        vs, ve = split if split is not None else (0, 0)
+        lo, hi = vs >> 16, min(size, (ve >> 16) + (256 << 10))
+        if host_leg and split is not None:
             t = time.perf_counter()
-            st = f.decode_span_device(first, ALL, timing=False, digest=True)
+            st = f.decode_span_device(vs, ve, timing=False, digest=False)
             dt = time.perf_counter() - t
-            assert st["records"] == n_rec, (st["records"], n_rec)
             res["c3_streamed_from_host"] = {
-                "seconds": round(dt, 3), "uncompressed_GBps": round(u_tot / dt / 1e9, 3),
-                "records_per_s": round(n_rec / dt, 1), "windows": st["windows"],
+                "seconds": round(dt, 3), "uncompressed_GBps": round(meta["uncompressed_bytes"] / dt / 1e9, 3),
+                "records_per_s": round(st["records"] / dt, 1), "windows": st["windows"],
                 "note": "windows copied from the mapped file (pageable) inside the timed call"}
-            t = time.perf_counter()
-            f.prefetch(0, size)
-            pf = time.perf_counter() - t
-            t = time.perf_counter()
-            st2 = f.decode_span_device(first, ALL, timing=False, digest=True)
-            dt2 = time.perf_counter() - t
-            res["c3_resident"] = {"seconds": round(dt2, 3), "uncompressed_GBps": round(u_tot / dt2 / 1e9, 3),
-                                  "records_per_s": round(n_rec / dt2, 1), "windows": st2["windows"],
-                                  "prefetch_seconds": round(pf, 3)}
-            t = time.perf_counter()
-            sbi = f.splitting_index(4096)
-            dti = time.perf_counter() - t
+        t = time.perf_counter()
+        if split is not None:
+            f.prefetch(lo, hi)  # inputs resident in HBM before the timed region
+        pf = time.perf_counter() - t
+        log(f"[rank {D.rank}] C3 split [{vs:#x}, {ve:#x}) -> bytes [{lo}, {hi}) resident ({pf:.1f}s)")
+
+        def step(timing=False, digest=False):
+            return f.decode_span_device(vs, ve, timing=timing, digest=digest) if split is not None else None
+
+        for _ in range(warmup):
+            step()
+        D.barrier()
+        t = time.perf_counter()
+        for _ in range(steps):
+            step()
+        D.barrier()
+        elapsed = D.max_over_ranks(time.perf_counter() - t)
+        meas = step(timing=True)
+        dig = step(digest=True)
+        mine = (0, 0, 0) if dig is None else (int(dig["records"]), int(dig["key_digest"]), int(dig["voff_digest"]))
+        parts = D.all_gather(mine)
+        n_all, kd, vd = compose_digests(parts)
+        base = sum(p[0] for p in parts[:D.rank])
+        if split is not None:
+            nrec, ent = f.splitting_entries(vs, ve, 4096, base)
+            assert nrec == mine[0], (nrec, mine[0])
+        else:
+            ent = np.zeros(0, np.uint64)
+        gathered = D.all_gather(ent.tobytes())
+        f.close()
+        if D.rank != 0:
+            return None
+        sbi = shard.be64([first]) + b"".join(
+            np.frombuffer(g, np.uint64).astype(">u8").tobytes() for g in gathered) + shard.be64([size << 16])
+        u = meta["uncompressed_bytes"]
+        res.update({
+            "value": u * steps / elapsed / 1e9, "ms_per_step": elapsed / steps * 1e3,
+            "records_per_s": meta["records"] * steps / elapsed, "records": n_all,
+            "split_bytes_rank0": hi - lo, "prefetch_seconds_rank0": round(pf, 3),
+            "stages_ms_rank0": None if meas is None else {
+                k: round(meas[k], 3) for k in ("ms_locate", "ms_inflate", "ms_tables", "ms_huff", "ms_lz77",
+                                               "ms_chain", "ms_decode", "ms_total")},
+            "windows_rank0": None if meas is None else meas["windows"],
+            "roofline": None if meas is None else roofline_of([meas], D.world)})
+        # the oracle over the whole file (rank 0, every usable core)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import orc
+        cores = host_cores()
         data = np.memmap(path, np.uint8, mode="r", shape=(size,))
         t = time.perf_counter()
         dec, _ = orc.scan(data, threads=cores, mode="decode")
@@ -323,20 +454,27 @@ def c3_c5_leg(target_gb, cores):
         ires, want = orc.scan(data, threads=cores, mode="index", granularity=4096)
         dtoi = time.perf_counter() - t
         del data
-        res["c3_parity"] = {"records": st["records"] == dec["records"] == n_rec,
-                            "key_xor": st["key_xor"] == st2["key_xor"] == dec["key_xor"],
-                            "voff_sum": st["voff_sum"] == st2["voff_sum"] == dec["voff_sum"],
-                            "oracle_seconds": round(dto, 1), "oracle_threads": cores,
-                            "oracle_uncompressed_GBps": round(u_tot / dto / 1e9, 3)}
+        res["c3_parity"] = {
+            "records": n_all == dec["records"] == meta["records"],
+            "key_digest": kd == dec["key_digest"], "voff_digest": vd == dec["voff_digest"],
+            "digest": "order-sensitive (HBAM_DIGEST_P), composed over the ranks' splits in file order",
+            "oracle_seconds": round(dto, 1), "oracle_threads": cores,
+            "oracle_uncompressed_GBps": round(u / dto / 1e9, 3)}
         res["c5_splitting_bai_g4096"] = {
-            "entries": len(sbi) // 8, "seconds": round(dti, 3), "uncompressed_GBps": round(u_tot / dti / 1e9, 3),
-            "identical_to_oracle": sbi == want, "oracle_seconds": round(dtoi, 1), "oracle_threads": cores}
+            "entries": len(sbi) // 8, "identical_to_oracle": sbi == want,
+            "assembled_from": f"{D.world} split(s): hbam_splitting_entries per rank, gathered on rank 0",
+            "oracle_seconds": round(dtoi, 1), "oracle_threads": cores}
+        res["matches_oracle"] = bool(res["c3_parity"]["records"] and res["c3_parity"]["key_digest"] and
+                                     res["c3_parity"]["voff_digest"] and
+                                     res["c5_splitting_bai_g4096"]["identical_to_oracle"])
         return res
     finally:
-        try:
-            os.unlink(path)
-        except OSError:
-            pass
+        D.barrier()
+        if D.rank == 0:
+            try:
+                os.unlink(path)
+            except OSError:
+                pass
 
 
 def long_read_leg():
@@ -416,12 +554,166 @@ def write_legs(path, size, info_u):
 
 
 # ---------------------------------------------------------------------------
+class Dist:
+    """One process per GPU (torchrun env); torch.distributed (RCCL on GPUs)
+    only for metadata all_gathers, barriers and the timing all_reduce."""
+
+    def __init__(self, args):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.device = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", "0"))
+        self.backend = args.dist_backend
+        self.dist = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+            torch.cuda.set_device(self.device)
+            dist.init_process_group(self.backend)
+            self.dist = dist
+        self.tag = self.all_gather(f"{os.getpid()}_{int(time.time())}")[0]
+
+    def all_gather(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def barrier(self):
+        # hbam calls return after their streams drain; torch's stream is idle
+        if self.dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            self.dist.barrier()
+
+    def max_over_ranks(self, x):
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64,
+                         device=f"cuda:{self.device}" if self.backend == "nccl" else "cpu")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+def run_c2(D, args, steps, warmup, extras):
+    """C2 (N=1) / N x C2 weak scaling: every rank decodes one C2 of records
+    from its split of one shared file.  extras (N=1): the CPU baseline, PMC
+    traffic and the side legs, on the same file."""
+    import hbam
+    from hbam import shard
+    path = os.path.join(scratch_dir(), f"hbam_bench_{D.tag}.bam")
+    try:
+        size, u_file = build_shared_bam(path, D.rank, D.world, args.records, D.all_gather, D.barrier)
+        f = hbam.BamFile(path=path, device=D.device)
+        first = f.header()["first_record_voff"]
+        split = shard.ShardedBamReader(f, size, first, D.rank, D.world, D.all_gather).split()
+        vs, ve = split if split is not None else (0, 0)
+        lo = vs >> 16
+        hi = min(size, (ve >> 16) + (256 << 10))
+        if split is not None:
+            f.prefetch(lo, hi)  # inputs resident in HBM before the timed region
+        log(f"[rank {D.rank}] split [{vs:#x}, {ve:#x}) -> bytes [{lo}, {hi}) resident")
+
+        def step(timing=True, digest=False):
+            if split is None:
+                return None
+            return f.decode_span_device(vs, ve, timing=timing, digest=digest)
+
+        for _ in range(warmup):
+            step(timing=args.serial)
+        D.barrier()
+        t = time.perf_counter()
+        for _ in range(steps):
+            step(timing=args.serial)  # production launch order (phase A / phase B overlapped), no events
+        D.barrier()
+        elapsed = D.max_over_ranks(time.perf_counter() - t)
+        # untimed measurement passes: every launch on one stream between its own
+        # HIP events -> per-stage and per-kernel durations (the roofline)
+        stats = [step(timing=True) for _ in range(3)]
+        check = step(timing=args.serial, digest=True)  # untimed: the digests for the parity check
+        mine = (0, 0, 0, 0) if check is None else (int(check["records"]), int(check["inflated_bytes"]),
+                                                   int(check["key_digest"]), int(check["voff_digest"]))
+        parts = D.all_gather(mine)
+        n_all, kd, vd = compose_digests([(p[0], p[2], p[3]) for p in parts])
+        u_all = sum(p[1] for p in parts)
+        assert n_all == D.world * args.records, (n_all, D.world * args.records)
+        out = None
+        if D.rank == 0:
+            st = stats[-1] if stats and stats[-1] is not None else check
+            out = {
+                "value": u_all * steps / elapsed / 1e9, "ms_per_step": elapsed / steps * 1e3,
+                "records_per_s": n_all * steps / elapsed,
+                "config": {"workload": ("C2: synthetic 10M x 150bp paired-end coordinate-sorted BAM" if D.world == 1
+                                        else f"N x C2: one BAM of {D.world} x C2 records split by BGZF ranges "
+                                             f"(weak scaling)"),
+                           "records_per_gpu": args.records, "file_bytes": size, "uncompressed_bytes": u_file,
+                           "split_bytes_rank0": hi - lo,
+                           "parallelism": f"FileVirtualSplit per rank x{D.world} (BAMSplitGuesser)"},
+                "parity": {"records": n_all, "key_digest": f"{kd:#018x}", "voff_digest": f"{vd:#018x}"},
+                "link_fallbacks": int(sum(s_["link_fallbacks"] for s_ in stats)),
+                "link_rewalks": int(sum(s_["link_rewalks"] for s_ in stats)),
+                "stages_ms": {k: round(st[k], 3) for k in ("ms_locate", "ms_inflate", "ms_tables", "ms_huff",
+                                                            "ms_lz77", "ms_chain", "ms_decode", "ms_total")},
+                "roofline": roofline_of(stats, D.world),
+                "cpu_baseline": None,
+            }
+        f.close()
+        if D.rank == 0 and extras:
+            if not args.no_cpu_baseline:
+                try:
+                    cb, full = cpu_baseline(path, size, args.cpu_seconds)
+                    out["cpu_baseline"] = cb
+                    out["parity"]["matches_oracle"] = bool(full["records"] == n_all and full["key_digest"] == kd
+                                                           and full["voff_digest"] == vd)
+                except Exception as e:  # reported, never substituted for the GPU number
+                    out["cpu_baseline"] = {"error": repr(e)}
+            if not args.no_pmc:
+                try:
+                    tr = pmc_traffic(path, vs, ve, out["roofline"]["kernel"])
+                    if tr and "bytes_per_launch" in tr:
+                        out["roofline"]["traffic"] = tr["bytes_per_launch"]
+                        out["roofline"]["traffic_detail"] = dict(tr, source="rocprofv3 --pmc child runs, this session")
+                    elif tr:
+                        out["roofline"]["traffic_error"] = tr["error"]
+                except Exception as e:
+                    out["roofline"]["traffic_error"] = repr(e)
+            if not args.no_extra:
+                extra = {}
+                for name, fn in (("c2_from_pinned_host", lambda: pinned_host_leg(path, n_all)),
+                                 ("dropin_end_to_end", lambda: dropin_leg(path, first, n_all)),
+                                 ("write_path", lambda: write_legs(path, size, u_file)),
+                                 ("c4_long_reads", long_read_leg)):
+                    t = time.time()
+                    try:
+                        extra[name] = fn()
+                    except Exception as e:
+                        extra[name] = {"error": repr(e)}
+                    log(f"[extra] {name} {time.time() - t:.1f}s")
+                out["extra"] = extra
+        return out
+    finally:
+        D.barrier()
+        if D.rank == 0:
+            try:
+                os.unlink(path)
+            except OSError:
+                pass
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--records", type=int, default=10_000_000, help="records per rank (C2: 10M)")
+    ap.add_argument("--workload", choices=("c2", "c3"), default=None,
+                    help="c2: C2 per rank (weak); c3: one ~60 GB BAM split over the ranks (strong). "
+                         "Default: c2 at one GPU, c3 at N > 1")
+    ap.add_argument("--records", type=int, default=10_000_000, help="C2 records per rank (10M)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the in-session rocprofv3 PMC passes")
@@ -430,7 +722,7 @@ def main():
                     help="every step in the measurement launch order (one stream, events per launch): the "
                          "command profiles/collect.sh traces, so rocprofv3's per-kernel averages are the "
                          "durations the roofline uses")
-    ap.add_argument("--c3-gb", type=float, default=60.0, help="size of the C3/C5 file (0: skip that leg)")
+    ap.add_argument("--c3-gb", type=float, default=60.0, help="size of the C3/C5 file (0: skip the C3 side leg)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo + --one-device: rehearse the N-rank sequence on a one-GPU box")
     ap.add_argument("--one-device", action="store_true", help="every rank on device 0 (rehearsal only)")
@@ -442,182 +734,68 @@ def main():
         pmc_child(args.pmc_child, *args.pmc_span)
         return
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    device = 0 if args.one_device else local_rank
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(device)
-        dist.init_process_group(args.dist_backend)
-
-    def all_gather(obj):
-        if dist is None:
-            return [obj]
-        out = [None] * world
-        dist.all_gather_object(out, obj)
-        return out
-
-    def barrier():
-        # hbam calls return after their streams drain; torch's stream is idle
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
-
-    import hbam
-    from hbam import shard
-
-    tag = all_gather(f"{os.getpid()}_{int(time.time())}")[0]
-    path = os.path.join(scratch_dir(), f"hbam_bench_{tag}.bam")
-    try:
-        size, u_file = build_shared_bam(path, rank, world, args.records, all_gather, barrier)
-        f = hbam.BamFile(path=path, device=device)
-        first = f.header()["first_record_voff"]
-        split = shard.ShardedBamReader(f, size, first, rank, world, all_gather).split()
-        vs, ve = split if split is not None else (0, 0)
-        lo = vs >> 16
-        hi = min(size, (ve >> 16) + (256 << 10))
-        if split is not None:
-            f.prefetch(lo, hi)  # inputs resident in HBM before the timed region
-        log(f"[rank {rank}] split [{vs:#x}, {ve:#x}) -> bytes [{lo}, {hi}) resident")
-
-        def step(timing=True, digest=False):
-            if split is None:
-                return None
-            return f.decode_span_device(vs, ve, timing=timing, digest=digest)
-
-        for _ in range(args.warmup):
-            step(timing=args.serial)
-        barrier()
-        t = time.perf_counter()
-        for _ in range(args.steps):
-            step(timing=args.serial)  # production launch order (phase A / phase B overlapped), no events
-        barrier()
-        elapsed = time.perf_counter() - t
-        # untimed measurement passes: every launch on one stream between its own
-        # HIP events -> per-stage and per-kernel durations (the roofline)
-        stats = [step(timing=True) for _ in range(3)]
-        check = step(timing=args.serial, digest=True)  # untimed: the digest for the parity check
-        mine = (0, 0, 0, 0, 0) if check is None else (int(check["records"]), int(check["inflated_bytes"]),
-                                                       int(check["compressed_bytes"]), int(check["key_xor"]),
-                                                       int(check["voff_sum"]))
-        if dist is not None:
-            import torch
-            tt = torch.tensor([elapsed], dtype=torch.float64,
-                              device=f"cuda:{device}" if args.dist_backend == "nccl" else "cpu")
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            elapsed = float(tt.item())
-        parts = all_gather(mine)
-        n_all = sum(p[0] for p in parts)
-        u_all = sum(p[1] for p in parts)
-        kx = 0
-        for p in parts:
-            kx ^= p[3]
-        vsum = sum(p[4] for p in parts) & ALL
-        assert n_all == world * args.records, (n_all, world * args.records)
-
-        st = stats[-1] if stats and stats[-1] is not None else check
-        ms_step = elapsed / args.steps * 1e3
-        value = u_all * args.steps / elapsed / 1e9
-        out = None
-        if rank == 0:
-            # dominant kernel: by its HIP-event time in the measurement passes
-            # (every inflate launch bracketed by its own events on one stream:
-            # kernel durations, as rocprofv3 reports them)
-            n_launch = max(1, st["inflate_launches"])
-            avg = lambda k: sum(s_[k] for s_ in stats) / len(stats)
-            kt = {"hbam::k_inflate_huff": avg("ms_huff"), "hbam::k_inflate_lz77": avg("ms_lz77"),
-                  "hbam::k_huff_tables": avg("ms_tables")}
-            dom = max(kt, key=kt.get)
-            dom_ms = kt[dom]
-            if dom != "hbam::k_inflate_lz77":  # phase A launches once per round of each chunk
-                n_launch *= INFLATE_ROUNDS
-            b_alg = st["compressed_bytes"] + st["inflated_bytes"] + SOA_BYTES_PER_RECORD * st["records"]
-            achieved = b_alg / (dom_ms * 1e-3) / 1e9
-            out = {
-                "metric": METRIC,
-                "value": round(value, 3),
-                "unit": "GB/s",
-                "n_gpus": world,
-                "steps": args.steps,
-                "warmup": args.warmup,
-                "ms_per_step": round(ms_step, 3),
-                "higher_is_better": True,
-                "scaling": "weak",
-                "vs_baseline": None,
-                "dtype": "u8",
-                "launch_order": "serial (measurement)" if args.serial else "overlapped (production)",
-                "data": "synthetic (tools/gen_synth_bam.c: Illumina-like qualities, zlib level 5 BGZF), "
-                        "generated on the box",
-                "config": {"workload": ("C2: synthetic 10M x 150bp paired-end coordinate-sorted BAM" if world == 1
-                                        else f"C3-shaped: one BAM of {world} x C2 records split by BGZF ranges"),
-                           "records_per_gpu": args.records, "file_bytes": size, "uncompressed_bytes": u_file,
-                           "split_bytes_rank0": hi - lo,
-                           "parallelism": f"FileVirtualSplit per rank x{world} (BAMSplitGuesser)"},
-                "records_per_s": round(n_all * args.steps / elapsed, 1),
-                "parity": {"records": n_all, "key_xor": f"{kx:#018x}", "voff_sum": f"{vsum:#018x}"},
-                "link_fallbacks": int(sum(s_["link_fallbacks"] for s_ in stats)),
-                "link_rewalks": int(sum(s_["link_rewalks"] for s_ in stats)),
-                "stages_ms": {k: round(st[k], 3) for k in ("ms_locate", "ms_inflate", "ms_tables", "ms_huff", "ms_lz77",
-                                                            "ms_chain", "ms_decode", "ms_total")},
-                "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                             "launches_per_pass": n_launch, "avg_launch_ms": round(dom_ms / n_launch, 4),
-                             "alg_bytes_per_launch": int(b_alg / n_launch),
-                             "alg_bytes_rule": "(C + U + 37 N) of the pass / launches (SURVEY 8d)",
-                             "kernel_ms_per_pass": {k: round(v, 3) for k, v in kt.items()},
-                             "whole_pass": {"achieved": round(b_alg / (st["ms_total"] * 1e-3) / 1e9, 2),
-                                            "frac": round(b_alg / (st["ms_total"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                                                          5)}},
-                "cpu_baseline": None,
-            }
-        f.close()
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    D = Dist(args)
+    workload = args.workload or ("c2" if D.world == 1 else "c3")
+    line = None
+    if workload == "c2":
+        r = run_c2(D, args, args.steps, args.warmup, extras=D.world == 1)
+        if D.rank == 0:
+            line = dict(r, scaling="weak", workload_key="c2")
+        if D.world == 1 and not args.no_extra and args.c3_gb > 0:
+            t = time.time()
             try:
-                cb, full = cpu_baseline(path, size, args.cpu_seconds)
-                out["cpu_baseline"] = cb
-                out["parity"]["matches_oracle"] = bool(full["records"] == n_all and full["key_xor"] == kx
-                                                       and full["voff_sum"] == vsum)
-            except Exception as e:  # reported, never substituted for the GPU number
-                out["cpu_baseline"] = {"error": repr(e)}
-        if rank == 0 and world == 1 and not args.no_pmc:
-            try:
-                tr = pmc_traffic(path, vs, ve, out["roofline"]["kernel"])
-                if tr and "bytes_per_launch" in tr:
-                    out["roofline"]["traffic"] = tr["bytes_per_launch"]
-                    out["roofline"]["traffic_detail"] = dict(tr, source="rocprofv3 --pmc child runs, this session")
-                elif tr:
-                    out["roofline"]["traffic_error"] = tr["error"]
+                c3 = run_c3(D, args.c3_gb, steps=3, warmup=1, host_leg=True)
             except Exception as e:
-                out["roofline"]["traffic_error"] = repr(e)
-        if rank == 0 and world == 1 and not args.no_extra:
-            extra = {}
-            for name, fn in (("c2_from_pinned_host", lambda: pinned_host_leg(path, n_all)),
-                             ("dropin_end_to_end", lambda: dropin_leg(path, first, n_all)),
-                             ("write_path", lambda: write_legs(path, size, u_file)),
-                             ("c4_long_reads", long_read_leg),
-                             ("c3_c5_60GB", lambda: c3_c5_leg(args.c3_gb, host_cores()) if args.c3_gb > 0 else None)):
-                t = time.time()
-                try:
-                    extra[name] = fn()
-                except Exception as e:
-                    extra[name] = {"error": repr(e)}
-                log(f"[extra] {name} {time.time() - t:.1f}s")
-            out["extra"] = extra
-        if rank == 0:
-            print(json.dumps(out), flush=True)
-    finally:
-        barrier()
-        if rank == 0:
-            try:
-                os.unlink(path)
-            except OSError:
-                pass
-    if dist is not None:
-        dist.destroy_process_group()
+                c3 = {"error": repr(e)}
+            log(f"[extra] c3_c5_60GB {time.time() - t:.1f}s")
+            if D.rank == 0:
+                line.setdefault("extra", {})["c3_c5_60GB"] = c3
+    else:
+        r = run_c3(D, args.c3_gb, args.steps, args.warmup, host_leg=False)
+        if D.rank == 0:
+            line = {"value": r["value"], "ms_per_step": r["ms_per_step"], "records_per_s": r["records_per_s"],
+                    "scaling": "strong", "workload_key": "c3",
+                    "config": {"workload": f"C3: one {r['file']['compressed_bytes'] / 1e9:.1f} GB synthetic BAM "
+                                           f"(150 bp paired-end model) split by BGZF byte ranges across "
+                                           f"{D.world} GPU(s)",
+                               "file_bytes": r["file"]["compressed_bytes"],
+                               "uncompressed_bytes": r["file"]["uncompressed_bytes"],
+                               "records": r["file"]["records"], "layout": r["file"]["layout"],
+                               "split_bytes_rank0": r["split_bytes_rank0"],
+                               "parallelism": f"FileVirtualSplit per rank x{D.world} (BAMSplitGuesser)"},
+                    "parity": {"records": r["records"], "matches_oracle": r["matches_oracle"],
+                               "c3": r["c3_parity"], "c5_splitting_bai_g4096": r["c5_splitting_bai_g4096"]},
+                    "stages_ms": r["stages_ms_rank0"], "windows_rank0": r["windows_rank0"],
+                    "roofline": r["roofline"], "cpu_baseline": None}
+        if D.world > 1 and not args.no_extra:
+            try:  # the weak-scaling side leg: N x C2, one C2 per rank
+                w = run_c2(D, args, steps=max(3, args.steps // 2), warmup=1, extras=False)
+            except Exception as e:
+                w = {"error": repr(e)}
+            if D.rank == 0:
+                line["extra"] = {"weak_nxc2": w}
+    if D.rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(line.pop("value"), 3),
+            "unit": "GB/s",
+            "n_gpus": D.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(line.pop("ms_per_step"), 3),
+            "higher_is_better": True,
+            "scaling": line.pop("scaling"),
+            "vs_baseline": None,
+            "dtype": "u8",
+            "launch_order": "serial (measurement)" if args.serial else "overlapped (production)",
+            "data": "synthetic (tools/gen_synth_bam.c: Illumina-like qualities, zlib level 5 BGZF), "
+                    "generated on the box",
+        }
+        line.pop("workload_key")
+        line["records_per_s"] = round(line["records_per_s"], 1)
+        out.update(line)
+        print(json.dumps(out), flush=True)
+    D.close()
 
 
 if __name__ == "__main__":

@@ -50,7 +50,9 @@ struct hbam_gpu {
 };
 
 namespace {
-std::string g_open_err;
+// the last error of a call with no ctx (open, compress, codec): per thread,
+// as JNI callers from many executor threads read it right after their call
+thread_local std::string g_open_err;
 
 OpenOptions options_of(const hbam_opts* opts, bool header) {
   hbam_opts o{};
@@ -129,8 +131,17 @@ int decode_device(BamFile& f, uint64_t vstart, uint64_t vend, int32_t flags, hba
     st->windows += 1;
     st->records += s.n;
     st->n_blocks += p.blocks().size();
-    st->compressed_bytes += p.window_end() - p.base();
-    st->inflated_bytes += p.total_u();
+    // bytes of this window up to the block the next window starts at (it
+    // starts at the record this one could not finish): each counted once
+    const bool last_window = step.ended || step.status != HBAM_OK;
+    const int64_t next_u = last_window ? -1 : p.pos_of_voff(step.next.coff << 16);
+    if (next_u < 0) {
+      st->compressed_bytes += p.window_end() - c.coff;
+      st->inflated_bytes += p.total_u();
+    } else {
+      st->compressed_bytes += step.next.coff - c.coff;
+      st->inflated_bytes += (uint64_t)next_u;
+    }
     if (p.timing) {
       st->ms_locate += p.times.locate;
       st->ms_inflate += p.times.inflate;
@@ -145,16 +156,21 @@ int decode_device(BamFile& f, uint64_t vstart, uint64_t vend, int32_t flags, hba
       (void)hipMemcpy(&st->last_voff, s.rec_voff + s.n - 1, 8, hipMemcpyDeviceToHost);
       first = false;
       if (digest) {
-        uint64_t kx = 0, vs = 0;
+        uint64_t dg[4];
         hbam::SpanDev d = s;
         if (!decode) d.col.key = nullptr;
-        rc = p.span_digest(d, &kx, &vs);
+        rc = p.span_digest(d, dg);
         if (rc != HBAM_OK) {
           *err = p.error();
           break;
         }
-        st->key_xor ^= kx;
-        st->voff_sum += vs;
+        st->key_xor ^= dg[0];
+        st->voff_sum += dg[1];
+        uint64_t w = 1, b = HBAM_DIGEST_P;  // P^n of this window's records
+        for (uint64_t e = s.n; e; e >>= 1, b *= b)
+          if (e & 1) w *= b;
+        st->key_digest = st->key_digest * w + dg[2];
+        st->voff_digest = st->voff_digest * w + dg[3];
       }
     }
     if (last) *last = s;
@@ -307,6 +323,7 @@ int hbam_ref(hbam_ctx* ctx, int32_t i, const char** name, int32_t* length) {
 
 int hbam_file_stats(hbam_ctx* ctx, uint64_t* n_blocks, uint64_t* uncompressed_size) {
   if (!ctx || !ctx->f) return HBAM_E_STATE;
+  ctx->cursor.reset();  // all_blocks() moves the window
   const std::vector<hbam::BlockInfo>* B = nullptr;
   int rc = ctx->f->all_blocks(&B);
   if (rc != HBAM_OK) {
@@ -350,13 +367,17 @@ int hbam_decode_span(hbam_ctx* ctx, uint64_t vstart, uint64_t vend, uint64_t max
 }
 
 int hbam_reader_position(hbam_ctx* ctx, uint64_t i, uint64_t* pos) {
+  *pos = 0;
   if (!ctx || !ctx->f) return HBAM_E_STATE;
+  if (ctx->last_is_writables || !ctx->cursor.valid()) {
+    ctx->err = "hbam_reader_position needs the last call on the ctx to be hbam_decode_span";
+    return HBAM_E_STATE;
+  }
   if (i >= ctx->batch.n) {
     ctx->err = "record index outside the last batch";
     return HBAM_E_ARG;
   }
-  *pos = ctx->cursor.reader_position(*ctx->f, i);
-  return HBAM_OK;
+  return ctx->cursor.reader_position(i, pos, &ctx->err);
 }
 
 int hbam_decode_span_device(hbam_ctx* ctx, uint64_t vstart, uint64_t vend, int32_t flags, hbam_gpu_stats* st) {
@@ -410,7 +431,7 @@ int hbam_encode_writables(hbam_ctx* ctx, uint8_t* out, uint64_t cap, uint64_t* o
     return HBAM_E_ARG;
   }
   if (bytes == 0) return HBAM_OK;
-  hbam::DevBuf<uint8_t> dst;
+  hbam::DevBuf<uint8_t> dst(&p.streams());
   if (dst.reserve((bytes + 15) & ~15ull) != hipSuccess) {
     ctx->err = "hipMalloc failed";
     return HBAM_E_DEVICE;
@@ -476,6 +497,25 @@ int hbam_build_splitting_index(hbam_ctx* ctx, int32_t granularity, uint8_t** buf
   return HBAM_OK;
 }
 
+int hbam_splitting_entries(hbam_ctx* ctx, uint64_t vstart, uint64_t vend, int32_t granularity, uint64_t ordinal0,
+                           uint64_t** entries, uint64_t* n_entries, uint64_t* n_records) {
+  *entries = nullptr;
+  *n_entries = *n_records = 0;
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  ctx->cursor.reset();
+  std::vector<uint64_t> ent;
+  int rc = SplittingBAMIndexer::entries(*ctx->f, vstart, vend, granularity, ordinal0, &ent, n_records);
+  if (rc != HBAM_OK) {
+    ctx->err = ctx->f->error();
+    return rc;
+  }
+  *entries = static_cast<uint64_t*>(malloc(ent.empty() ? 8 : ent.size() * 8));
+  if (!*entries) return HBAM_E_NOMEM;
+  if (!ent.empty()) memcpy(*entries, ent.data(), ent.size() * 8);
+  *n_entries = ent.size();
+  return HBAM_OK;
+}
+
 int hbam_splitting_index_for_records(const hbam_opts* opts, const uint64_t* voffs, uint64_t n, int32_t granularity,
                                      uint64_t file_size, uint8_t** buf, uint64_t* len) {
   *buf = nullptr;
@@ -497,7 +537,7 @@ int hbam_splitting_index_for_records(const hbam_opts* opts, const uint64_t* voff
     g_open_err = p.error();
     return HBAM_E_DEVICE;
   }
-  hbam::DevBuf<uint64_t> dv;
+  hbam::DevBuf<uint64_t> dv(&p.streams());
   std::vector<uint64_t> ent;
   hbam::SpanDev span;
   if (n) {
@@ -657,6 +697,8 @@ int hbam_gpu_load(hbam_gpu* g, const void* data, uint64_t len) {
   OpenOptions o;
   o.device = g->device;
   o.window_bytes = g->window;
+  g->enc.release();  // owned by the old file's pipeline streams
+  g->enc.owner = nullptr;
   g->f.reset();
   g->span = hbam::SpanDev();
   std::string err;
@@ -795,6 +837,7 @@ int hbam_gpu_encode_writables(hbam_gpu* g, int32_t iters, float* ms_per_iter, ui
   if (!g->f) return HBAM_E_STATE;
   hbam::Pipeline& p = g->f->pipe();
   uint64_t nb = 0;
+  g->enc.owner = &p.streams();
   int rc = p.encoded_bytes(g->span, &nb);
   if (rc != HBAM_OK) {
     g->err = p.error();

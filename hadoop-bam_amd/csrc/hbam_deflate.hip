@@ -217,10 +217,10 @@ BgzfCompressor::~BgzfCompressor() {
 }
 
 template <typename T>
-static hipError_t grow_buf(T** p, size_t* have, size_t need) {
+static hipError_t grow_buf(T** p, size_t* have, size_t need, hipStream_t s) {
   if (*p && *have >= need) return hipSuccess;
   if (*p) {
-    (void)hipDeviceSynchronize();
+    (void)hipStreamSynchronize(s);  // the compressor's work runs on s only
     (void)hipFree(*p);
   }
   *p = nullptr;
@@ -269,15 +269,15 @@ int BgzfCompressor::compress(const uint8_t* d_in, const std::vector<uint64_t>& u
   const uint32_t lanes = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(nb, 1), max_lanes);
   uint64_t worst = eof ? 28 : 0;
   for (uint32_t l : lens) worst += (uint64_t)l + 26 + 64;
-  DCHK(grow_buf(&arenas_, &arenas_n_, (size_t)lanes * sizeof(dfl::Arena)));
-  DCHK(grow_buf(&slots_, &slots_n_, (size_t)lanes * kSlot));
-  DCHK(grow_buf(&csize_, &csize_n_, std::max<uint64_t>(nb, 1) * 4));
-  DCHK(grow_buf(&ovf_, &ovf_n_, std::max<uint64_t>(nb, 1)));
-  DCHK(grow_buf(&crc_, &crc_n_, std::max<uint64_t>(nb, 1) * 4));
-  DCHK(grow_buf(&offs_, &offs_n_, (nb + 1) * 8));
-  DCHK(grow_buf(&ustart_, &ustart_n_, std::max<uint64_t>(nb, 1) * 8));
-  DCHK(grow_buf(&lens_, &lens_n_, std::max<uint64_t>(nb, 1) * 4));
-  DCHK(grow_buf(&out_, &out_n_, worst + 16));
+  DCHK(grow_buf(&arenas_, &arenas_n_, (size_t)lanes * sizeof(dfl::Arena), s));
+  DCHK(grow_buf(&slots_, &slots_n_, (size_t)lanes * kSlot, s));
+  DCHK(grow_buf(&csize_, &csize_n_, std::max<uint64_t>(nb, 1) * 4, s));
+  DCHK(grow_buf(&ovf_, &ovf_n_, std::max<uint64_t>(nb, 1), s));
+  DCHK(grow_buf(&crc_, &crc_n_, std::max<uint64_t>(nb, 1) * 4, s));
+  DCHK(grow_buf(&offs_, &offs_n_, (nb + 1) * 8, s));
+  DCHK(grow_buf(&ustart_, &ustart_n_, std::max<uint64_t>(nb, 1) * 8, s));
+  DCHK(grow_buf(&lens_, &lens_n_, std::max<uint64_t>(nb, 1) * 4, s));
+  DCHK(grow_buf(&out_, &out_n_, worst + 16, s));
   struct Ev {  // destroyed on every return path
     hipEvent_t e = nullptr;
     ~Ev() {

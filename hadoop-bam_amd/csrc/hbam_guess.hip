@@ -499,7 +499,7 @@ int prepare_window(BamFile& f, uint64_t lo, uint64_t hi, hbam::DevBuf<uint8_t>* 
     for (uint32_t j = 0; j < nblk; ++j)
       if (valid[j] && blk[j].isize > 0) dev_idx.push_back(j);
   }
-  DevBuf<uint32_t> dlist;
+  DevBuf<uint32_t> dlist(&p.streams());
   hipStream_t s = p.stream();
   auto chk = [&](hipError_t e) {
     if (e != hipSuccess) *err = std::string("HIP: ") + hipGetErrorString(e);
@@ -529,8 +529,8 @@ int run_points(BamFile& f, const std::vector<GuessPoint>& pts, size_t a, size_t 
     hb[j] = pts[a + j].beg;
     he[j] = pts[a + j].end;
   }
-  DevBuf<uint64_t> dbeg, dend, dout;
-  DevBuf<int32_t> dst;
+  DevBuf<uint64_t> dbeg(&p.streams()), dend(&p.streams()), dout(&p.streams());
+  DevBuf<int32_t> dst(&p.streams());
   hipStream_t s = p.stream();
   auto chk = [&](hipError_t e) {
     if (e != hipSuccess) *err = std::string("HIP: ") + hipGetErrorString(e);
@@ -580,7 +580,7 @@ int guess_batch(BamFile& f, const std::vector<uint64_t>& begs, const std::vector
     const uint64_t lim = std::min<uint64_t>(begs[i] + std::min<uint64_t>(ends[i] - begs[i], kMaxBytesRead), f.file_size());
     pts.push_back({begs[i], ends[i], lim, i});
   }
-  DevBuf<uint8_t> dvalid;
+  DevBuf<uint8_t> dvalid(&f.pipe().streams());
   return for_each_window(f, pts, [&](uint64_t lo, uint64_t hi, size_t a, size_t b) {
     int rc = prepare_window(f, lo, hi, &dvalid, err);
     if (rc != kOk) return rc;
@@ -612,7 +612,7 @@ int guess_bgzf_batch(BamFile& f, const std::vector<uint64_t>& begs, const std::v
         std::min<uint64_t>(begs[i] + std::min<uint64_t>(ends[i] - begs[i], kBgzfGuessWindow), f.file_size());
     pts.push_back({begs[i], ends[i], lim, i});
   }
-  DevBuf<uint8_t> dvalid;
+  DevBuf<uint8_t> dvalid(&f.pipe().streams());
   return for_each_window(f, pts, [&](uint64_t lo, uint64_t hi, size_t a, size_t b) {
     int rc = prepare_window(f, lo, hi, &dvalid, err);
     if (rc != kOk) return rc;

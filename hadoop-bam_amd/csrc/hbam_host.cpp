@@ -146,6 +146,7 @@ int BamFile::init(const OpenOptions& o, std::string* err) {
     *err = pipe_->error();
     return kErrDevice;
   }
+  src_.dev.owner = &pipe_->streams();  // kernels read the resident copy on the pipeline's streams
   pipe_->set_stringency(o.stringency);
   set_window_bytes(o.window_bytes ? o.window_bytes : kDefaultWindowBytes);
   int rc;
@@ -590,6 +591,43 @@ int SplittingBAMIndexer::index(BamFile& f, int32_t g, std::vector<uint8_t>* out)
   return kOk;
 }
 
+int SplittingBAMIndexer::entries(BamFile& f, uint64_t vstart, uint64_t vend, int32_t g, uint64_t ordinal0,
+                                 std::vector<uint64_t>* out, uint64_t* n_records) {
+  out->clear();
+  *n_records = 0;
+  if (g <= 0) {
+    f.error() = "Granularity must be a positive integer";
+    return kErrArg;
+  }
+  // the indexer's chain (readAlignment / fullySkip, :340-368) over the split,
+  // window by window; entries at global ordinals k*g - 1 (:273-277)
+  Carry c{vstart >> 16, vstart & 0xffff};
+  bool cont = false;
+  uint64_t ordinal = ordinal0;
+  std::vector<uint64_t> ent;
+  for (;;) {
+    Step st;
+    int rc = f.decode_step(c, vend, hbam::kIndexer, false, cont, &st);
+    if (rc != kOk) return rc;
+    if (st.status != kOk) {
+      f.error() = st.error;
+      return st.status;
+    }
+    rc = f.pipe().splitting_entries(st.span, (uint32_t)g, ordinal, &ent);
+    if (rc != kOk) {
+      f.error() = f.pipe().error();
+      return rc;
+    }
+    out->insert(out->end(), ent.begin(), ent.end());
+    ordinal += st.span.n;
+    if (st.ended) break;
+    c = st.next;
+    cont = true;
+  }
+  *n_records = ordinal - ordinal0;
+  return kOk;
+}
+
 void SplittingBAMIndexer::processAlignment(uint64_t voff) {
   if (count_ == 0 || (count_ + 1) % (uint64_t)granularity_ == 0) writeVirtualOffset(voff);
   count_++;
@@ -899,7 +937,10 @@ int fetch_span(hbam::Pipeline& p, const SpanDev& s, uint64_t k, uint64_t m, Host
   const uint8_t* src = s.data ? s.data : p.d_u();
   if (hi > lo)
     ok = ok && hipMemcpyAsync(h->data.data() + d0, src + lo, hi - lo, hipMemcpyDeviceToHost, st) == hipSuccess;
-  if (!ok || hipStreamSynchronize(st) != hipSuccess) {
+  // always drained, also after a failed enqueue: the pinned columns are freed
+  // (or cached for another context) without a device-wide wait
+  const bool drained = hipStreamSynchronize(st) == hipSuccess;
+  if (!ok || !drained) {
     *err = "hipMemcpy D2H failed";
     return kErrDevice;
   }
@@ -936,7 +977,7 @@ int SpanCursor::next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t 
   h->data_len = 0;
   h->window_pos.clear();
   batch_one_window_ = false;
-  batch_end_pos_.clear();
+  batch_end_.clear();
   const bool cont = valid_ && vend == vend_ && vstart == next_voff_;
   if (!cont) {  // a seek to the split start (or anywhere in it)
     valid_ = true;
@@ -995,17 +1036,17 @@ int SpanCursor::next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t 
     *next_voff = vend;
   }
   next_voff_ = *next_voff;
-  if (batch_one_window_) {  // last byte of each record (+ the read-ahead one) for reader_position
+  if (batch_one_window_) {  // block end of each record's last byte (+ the read-ahead one) for reader_position
     const uint64_t base = h->window_pos.empty() ? 0 : h->window_pos[0];
-    batch_end_pos_.resize(h->n + 1);
-    for (uint64_t i = 0; i < h->n; ++i) batch_end_pos_[i] = base + h->rest_off[i] + h->rest_len[i] - 1;
-    batch_end_pos_[h->n] = ~0ull;
+    batch_end_.resize(h->n + 1);
+    for (uint64_t i = 0; i < h->n; ++i) batch_end_[i] = f.block_end_of(base + h->rest_off[i] + h->rest_len[i] - 1);
+    batch_end_[h->n] = ~0ull;
     if (k_ < step_.span.n) {
       uint64_t ro = 0;
       uint32_t rl = 0;
       if (hipMemcpy(&ro, step_.span.col.rest_off + k_, 8, hipMemcpyDeviceToHost) == hipSuccess &&
           hipMemcpy(&rl, step_.span.col.rest_len + k_, 4, hipMemcpyDeviceToHost) == hipSuccess)
-        batch_end_pos_[h->n] = ro + rl - 1;
+        batch_end_[h->n] = f.block_end_of(ro + rl - 1);
     }
   }
   return status;
@@ -1021,15 +1062,26 @@ bool SpanCursor::last_batch_span(SpanDev* out) const {
   return true;
 }
 
-uint64_t SpanCursor::reader_position(BamFile& f, uint64_t i) const {
+int SpanCursor::reader_position(uint64_t i, uint64_t* pos, std::string* err) const {
   // BAMRecordReader.getProgress (:209-219) reads in.position(): htsjdk's
   // iterator has already read the record after the one just returned (when
   // the split holds one), so the stream stands at the end of the block
   // holding that record's last byte.
-  if (batch_end_pos_.empty()) return 0;
-  uint64_t pos = i + 1 < batch_end_pos_.size() ? batch_end_pos_[i + 1] : ~0ull;
-  if (pos == ~0ull) pos = batch_end_pos_[std::min<uint64_t>(i, batch_end_pos_.size() - 2)];
-  return f.block_end_of(pos);
+  if (!valid_ || batch_end_.size() < 2 || i + 1 >= batch_end_.size()) {
+    *err = "no position for this record: the last batch spans several windows";
+    return kErrState;
+  }
+  *pos = batch_end_[i + 1] != ~0ull ? batch_end_[i + 1] : batch_end_[i];
+  return kOk;
+}
+
+int SpanCursor::initial_position(uint64_t* pos, std::string* err) const {
+  if (!valid_ || batch_end_.size() < 2) {
+    *err = "no batch";
+    return kErrState;
+  }
+  *pos = batch_end_[0];
+  return kOk;
 }
 
 int BAMRecordReader::initialize(BamFile& f, const FileVirtualSplit& split) {
@@ -1089,8 +1141,11 @@ float BAMRecordReader::getProgress() const {
   const uint64_t fileEnd = virtualEnd_ >> 16;
   if (b_.n == 0) return 0.0f;
   // before the first nextKeyValue the iterator has read record 0
-  const uint64_t filePos = started_ ? cur_span_.reader_position(*f_, cur_) : f_->block_end_of(
-      b_.window_pos.empty() ? 0 : b_.window_pos[0] + b_.rest_off[0] + b_.rest_len[0] - 1);
+  // before the first nextKeyValue the iterator has read record 0
+  uint64_t filePos = 0;
+  std::string e;
+  const int rc = started_ ? cur_span_.reader_position(cur_, &filePos, &e) : cur_span_.initial_position(&filePos, &e);
+  if (rc != kOk) return 0.0f;
   return (float)((double)((int64_t)filePos - (int64_t)fileStart_) / (double)(fileEnd - fileStart_ + 1));
 }
 

@@ -107,6 +107,7 @@ class BamFile {
   static int open_device_copy(const uint8_t* data, uint64_t len, const OpenOptions& o, std::unique_ptr<BamFile>* out,
                               std::string* err);
 
+  ~BamFile() { src_.dev.release(); }  // before pipe_, whose streams own it
   hbam::Pipeline& pipe() { return *pipe_; }
   uint64_t file_size() const { return src_.size; }
   uint64_t bytes_read() const { return src_.bytes_read; }
@@ -208,6 +209,11 @@ class SplittingBAMIndexer {
   // index(in, out, inputSize, granularity) :248-290 -- GPU record chain under
   // the indexer's read rules, window by window, entries by global ordinal.
   static int index(BamFile& f, int32_t granularity, std::vector<uint8_t>* out);
+  // the part of index() one split contributes (multi-GPU):
+  // entries of the records of [vstart, vend), the first having global ordinal
+  // ordinal0; *n_records = records of the split
+  static int entries(BamFile& f, uint64_t vstart, uint64_t vend, int32_t granularity, uint64_t ordinal0,
+                     std::vector<uint64_t>* out, uint64_t* n_records);
   // write-time API :175-243 (BAMRecordWriter.java:145-149 drives it): the
   // entries of a run of record voffs, computed on the GPU (k_sbi_emit)
   explicit SplittingBAMIndexer(int32_t granularity = DEFAULT_GRANULARITY) : granularity_(granularity) {}
@@ -309,9 +315,16 @@ class SpanCursor {
                  uint64_t* next_voff, std::string* err);
   // device view of the records of the last batch when they lie in one window
   bool last_batch_span(SpanDev* out) const;
-  // BAMRecordReader.getProgress's in.position() after record i of the last batch
-  uint64_t reader_position(BamFile& f, uint64_t i) const;
-  void reset() { valid_ = false; }
+  // BAMRecordReader.getProgress's in.position() after record i of the last
+  // batch; kErrState when the last batch cannot answer (see hbam.h)
+  int reader_position(uint64_t i, uint64_t* pos, std::string* err) const;
+  // ... before the first record is returned (htsjdk has read record 0)
+  int initial_position(uint64_t* pos, std::string* err) const;
+  bool valid() const { return valid_; }
+  void reset() {
+    valid_ = false;
+    batch_end_.clear();
+  }
 
  private:
   bool valid_ = false;
@@ -320,7 +333,9 @@ class SpanCursor {
   uint64_t k_ = 0;                    // next record of step_ to hand out
   uint64_t batch_k0_ = 0, batch_n_ = 0;  // the last batch within step_ (single window)
   bool batch_one_window_ = false;
-  std::vector<uint64_t> batch_end_pos_;  // window position of each batch record's last byte (+1 read-ahead)
+  // file offset of the end of the block holding each batch record's last
+  // byte (+ the read-ahead record's), computed while the batch is built
+  std::vector<uint64_t> batch_end_;
 };
 
 // BAMRecordReader (BAMRecordReader.java:63-233) over one FileVirtualSplit.

@@ -2849,22 +2849,59 @@ __global__ void k_next_pos(const uint8_t* __restrict__ u, const uint64_t* __rest
   *out = q + 4 + (uint64_t)(mode == kReader ? bs : (bs > 0 ? bs : 0));
 }
 
-// xor of the keys and sum of the voffs (order-independent digests)
+// Digests of a span (bench / test parity checks, not on the timed path):
+// out[0] xor of the keys, out[1] sum of the voffs (order-independent), and
+// the order-sensitive out[2] / out[3] = sum_i dmix(x_i) * P^(n-1-i) mod 2^64
+// over keys / voffs (oracle/hbam_oracle.h ORC_DIGEST_P; composable across
+// windows and ranks: D(A ++ B) = D(A) * P^|B| + D(B)).  Each thread takes a
+// contiguous run of records (Horner), weighted by P^(records after the run).
+__device__ __forceinline__ uint64_t dig_mix(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+__device__ __forceinline__ uint64_t dig_pow(uint64_t b, uint64_t e) {
+  uint64_t r = 1;
+  for (; e; e >>= 1, b *= b)
+    if (e & 1) r *= b;
+  return r;
+}
+constexpr uint64_t kDigestP = 0x100000001b3ull;
+
 __global__ __launch_bounds__(256) void k_digest(const int64_t* __restrict__ keys, const uint64_t* __restrict__ voffs,
                                                 uint64_t n, unsigned long long* __restrict__ out) {
-  uint64_t kx = 0, vs = 0;
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    if (keys) kx ^= (uint64_t)keys[i];
-    vs += voffs[i];
+  const uint64_t nt = (uint64_t)gridDim.x * blockDim.x, t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t per = (n + nt - 1) / nt;
+  const uint64_t i0 = t * per < n ? t * per : n, i1 = i0 + per < n ? i0 + per : n;
+  uint64_t kx = 0, vs = 0, kd = 0, vd = 0;
+  for (uint64_t i = i0; i < i1; ++i) {
+    const uint64_t v = voffs[i];
+    vs += v;
+    vd = vd * kDigestP + dig_mix(v);
+    if (keys) {
+      const uint64_t k = (uint64_t)keys[i];
+      kx ^= k;
+      kd = kd * kDigestP + dig_mix(k);
+    }
   }
+  const uint64_t w = dig_pow(kDigestP, n - i1);
+  kd *= w;
+  vd *= w;
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) {
     kx ^= (uint64_t)__shfl_xor((unsigned long long)kx, d, 64);
     vs += (uint64_t)__shfl_xor((unsigned long long)vs, d, 64);
+    kd += (uint64_t)__shfl_xor((unsigned long long)kd, d, 64);
+    vd += (uint64_t)__shfl_xor((unsigned long long)vd, d, 64);
   }
   if (lane_id() == 0) {
     atomicXor(&out[0], (unsigned long long)kx);
     atomicAdd(&out[1], (unsigned long long)vs);
+    atomicAdd(&out[2], (unsigned long long)kd);
+    atomicAdd(&out[3], (unsigned long long)vd);
   }
 }
 

@@ -93,11 +93,7 @@ void dev_free(void* p, size_t bytes) {
     (void)hipFree(p);
     return;
   }
-  // queued work on the block's device may still use it (hipFree waits too)
-  const int cur = current_device();
-  if (cur != dev) (void)hipSetDevice(dev);
-  (void)hipDeviceSynchronize();
-  if (cur != dev && cur >= 0) (void)hipSetDevice(cur);
+  // the owner has drained its streams (DevBuf::release): no device-wide wait
   if (!dev_cache().put(p, bytes, dev, kDevCap)) (void)hipFree(p);
 }
 
@@ -115,7 +111,8 @@ hipError_t pinned_alloc(void** p, size_t bytes, size_t* got) {
 
 void pinned_free(void* p, size_t bytes) {
   if (!p) return;
-  (void)hipDeviceSynchronize();  // an async copy may still read or write it
+  // every copy into a batch buffer is waited for by its owner (fetch_span,
+  // the batch prefetch): no device-wide wait here
   if (bytes >= kMinCached && pinned_cache().put(p, bytes, 0, kPinnedCap)) return;
   (void)hipHostFree(p);
 }

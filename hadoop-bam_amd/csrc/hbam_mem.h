@@ -7,8 +7,13 @@
 // than decoding a C2 split (hipHostMalloc of a 1M-record batch, ~0.3 s).  A
 // freed block goes back to a per-process cache instead and the next split of
 // the same process (a Spark executor or a reused task JVM reads many) takes
-// it.  A released block may still be read by queued work, so the device is
-// synchronized first, as hipFree / hipHostFree would.
+// it.
+//
+// Concurrency: many contexts (one per reader thread of an executor) share a
+// GPU.  A released block may still be read by work its owner queued, so the
+// owner waits for ITS streams (StreamSet) before a block is released or
+// handed on -- never for the whole device, which would stall every other
+// reader on the GPU.  The caches themselves are mutex-guarded.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -16,12 +21,28 @@
 
 namespace hbam {
 
+// The streams whose queued work may touch an owner's blocks.
+struct StreamSet {
+  hipStream_t s[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  int n = 0;
+  hipError_t sync() const {
+    for (int i = 0; i < n; ++i)
+      if (s[i]) {
+        const hipError_t e = hipStreamSynchronize(s[i]);
+        if (e != hipSuccess) return e;
+      }
+    return hipSuccess;
+  }
+};
+
 // A block of at least `bytes` on the current device (a cached one of at most
 // twice the size, else hipMalloc); *got = its size.
 hipError_t dev_alloc(void** p, size_t bytes, size_t* got);
+// The caller has waited for every stream that used the block.
 void dev_free(void* p, size_t bytes);
 
-// Page-locked host memory (hipHostMalloc), cached the same way.
+// Page-locked host memory (hipHostMalloc), cached the same way; the caller
+// has waited for every copy into or out of the block before freeing it.
 hipError_t pinned_alloc(void** p, size_t bytes, size_t* got);
 void pinned_free(void* p, size_t bytes);
 

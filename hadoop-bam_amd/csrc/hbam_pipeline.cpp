@@ -33,6 +33,15 @@ Pipeline::Pipeline(int device) : device_(device) {
       hipStreamCreateWithFlags(&stream_t_, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&stream_copy_, hipStreamNonBlocking) != hipSuccess)
     err_ = "hipStreamCreate failed";
+  streams_.s[0] = stream_;
+  streams_.s[1] = stream_b_;
+  streams_.s[2] = stream_t_;
+  streams_.s[3] = stream_copy_;
+  streams_.n = 4;
+  own(own_file_, own_spare_, stage_, dblocks_, ref_len_, du_, tokens_[0], tokens_[1], hout_, tables_[0], tables_[1],
+      tinfo_[0], tinfo_[1], g_, x_, x2_, entry_, base_arr_, summary_, dead_, cand_, sorted_, isz_, ust_, cnt_, flags_,
+      errv_, need_, rec_pos_, rec_voff_, rcand_, force_, wcnt_, counters_, list_, scan_tmp_, cols_, long_rec_,
+      long_n_, wbuf_, woffs_, wbad_, scalars_);
   for (auto& e : ev_) (void)hipEventCreate(&e);
   for (auto& e : sync_ev_) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : tab_ev_) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -42,7 +51,9 @@ Pipeline::Pipeline(int device) : device_(device) {
 Pipeline::~Pipeline() {
   if (stage_thr_.joinable()) stage_thr_.join();
   (void)hipSetDevice(device_);
-  (void)hipDeviceSynchronize();
+  // this pipeline's own streams only: other contexts on the GPU run on
+  (void)streams_.sync();
+  streams_.n = 0;  // drained: the member buffers release without waiting (the streams go below)
   for (auto& e : ev_) (void)hipEventDestroy(e);
   for (auto& e : sync_ev_) (void)hipEventDestroy(e);
   for (auto& e : tab_ev_) (void)hipEventDestroy(e);
@@ -184,7 +195,7 @@ int Pipeline::reload(const uint8_t* data, uint64_t len, bool pinned, float* ms) 
 
 int Pipeline::d2d_bandwidth(uint64_t bytes, int iters, float* gbps) {
   *gbps = 0;
-  DevBuf<uint8_t> a, b;
+  DevBuf<uint8_t> a(&streams_), b(&streams_);
   HIPCHK(a.reserve(bytes));
   HIPCHK(b.reserve(bytes));
   HIPCHK(hipMemsetAsync(a.p, 1, bytes, stream_));
@@ -357,7 +368,7 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
     HIPCHK(tables_[i].reserve((uint64_t)kInflateChunkBlocks * kHuffTableImage));
     HIPCHK(tinfo_[i].reserve(kInflateChunkBlocks));
   }
-  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(streams_.sync());
 
   // Piece k's copy and its locate run in order on stream_copy_, the inflate
   // of located blocks on the inflate streams.  (With locate on its own stream,
@@ -826,7 +837,7 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
   }
   if (dec) HIPCHK(launch_long_hash(du_.p, rec_pos_.p, c, stream_));
   // the next record's start: the chain successor of the last record
-  HIPCHK(scalars_.reserve(4));
+  HIPCHK(scalars_.reserve(8));
   HIPCHK(launch_next_pos(du_.p, rec_pos_.p, total, p0, mode, scalars_.p, stream_));
   HIPCHK(hipMemcpyAsync(&out->next_pos, scalars_.p, 8, hipMemcpyDeviceToHost, stream_));
   if (timing) HIPCHK(hipEventRecord(ev_[2], stream_));
@@ -954,7 +965,7 @@ int Pipeline::splitting_entries(const SpanDev& span, uint32_t g, uint64_t o0, st
   // global ordinals o0 .. o0+n-1; entries at ordinals k*g - 1
   const uint64_t m = (o0 + span.n) / g - o0 / g;
   if (m == 0) return kOk;
-  DevBuf<uint64_t> ent;
+  DevBuf<uint64_t> ent(&streams_);
   HIPCHK(ent.reserve(m));
   HIPCHK(launch_sbi_emit(span.rec_voff, span.n, g, o0, ent.p, stream_));
   out->resize(m);
@@ -963,17 +974,14 @@ int Pipeline::splitting_entries(const SpanDev& span, uint32_t g, uint64_t o0, st
   return kOk;
 }
 
-int Pipeline::span_digest(const SpanDev& span, uint64_t* key_xor, uint64_t* voff_sum) {
-  *key_xor = *voff_sum = 0;
+int Pipeline::span_digest(const SpanDev& span, uint64_t out[4]) {
+  out[0] = out[1] = out[2] = out[3] = 0;
   if (span.n == 0) return kOk;
-  HIPCHK(scalars_.reserve(4));
-  HIPCHK(hipMemsetAsync(scalars_.p, 0, 32, stream_));
-  HIPCHK(launch_digest(span.col.key, span.rec_voff, span.n, scalars_.p + 1, stream_));
-  uint64_t d[2];
-  HIPCHK(hipMemcpyAsync(d, scalars_.p + 1, 16, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(scalars_.reserve(8));
+  HIPCHK(hipMemsetAsync(scalars_.p + 2, 0, 32, stream_));
+  HIPCHK(launch_digest(span.col.key, span.rec_voff, span.n, scalars_.p + 2, stream_));
+  HIPCHK(hipMemcpyAsync(out, scalars_.p + 2, 32, hipMemcpyDeviceToHost, stream_));
   HIPCHK(hipStreamSynchronize(stream_));
-  *key_xor = d[0];
-  *voff_sum = d[1];
   return kOk;
 }
 

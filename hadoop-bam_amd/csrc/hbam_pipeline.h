@@ -23,25 +23,33 @@
 
 namespace hbam {
 
+// A device buffer.  `owner` = the streams that may have queued work on it
+// (its Pipeline's): releasing or regrowing it waits for those streams only.
+// A buffer without an owner waits for the whole device.
 template <typename T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;  // elements
+  const StreamSet* owner = nullptr;
   DevBuf() = default;
+  explicit DevBuf(const StreamSet* o) : owner(o) {}
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
-  void swap(DevBuf& o) {
+  void swap(DevBuf& o) {  // the contents; both keep their owner
     std::swap(p, o.p);
     std::swap(n, o.n);
   }
+  hipError_t quiesce() const { return owner ? owner->sync() : hipDeviceSynchronize(); }
   void release() {
-    if (p) dev_free(p, n * sizeof(T));
+    if (p) {
+      (void)quiesce();
+      dev_free(p, n * sizeof(T));
+    }
     p = nullptr;
     n = 0;
   }
-  // grow, keeping the contents (waits for the whole device first: the old
-  // buffer may be in use on any stream)
+  // grow, keeping the contents
   hipError_t grow(size_t count) {
     if (count <= n && p) return hipSuccess;
     const size_t c = count > 2 * n ? count : 2 * n;
@@ -50,7 +58,7 @@ struct DevBuf {
     hipError_t e = dev_alloc(&q, c * sizeof(T), &got);
     if (e != hipSuccess) return e;
     if (p) {
-      if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+      if ((e = quiesce()) != hipSuccess) return e;
       if ((e = hipMemcpy(q, p, n * sizeof(T), hipMemcpyDeviceToDevice)) != hipSuccess) return e;
       dev_free(p, n * sizeof(T));
     }
@@ -61,7 +69,6 @@ struct DevBuf {
   // grow-only (contents not preserved)
   hipError_t reserve(size_t count) {
     if (count <= n && p) return hipSuccess;
-    if (p) (void)hipDeviceSynchronize();  // queued work on any stream may still use it
     release();
     size_t c = count ? count : 1;
     void* q = nullptr;
@@ -106,6 +113,9 @@ class Pipeline {
 
   int device() const { return device_; }
   hipStream_t stream() const { return stream_; }
+  // every stream this pipeline queues work on (owner of its buffers and of
+  // buffers its callers hand it: BamFile's resident copy, ABI temporaries)
+  const StreamSet& streams() const { return streams_; }
   const std::string& error() const { return err_; }
 
   // Copy file bytes [base, base + len) into the window buffer.  at_eof: the
@@ -183,8 +193,9 @@ class Pipeline {
   // .splitting-bai entries of a span whose first record has global ordinal
   // `ordinal0` (SplittingBAMIndexer.java:273-277: ordinals k*g - 1)
   int splitting_entries(const SpanDev& span, uint32_t granularity, uint64_t ordinal0, std::vector<uint64_t>* out);
-  // order-independent digests of a decoded span's keys / voffs (bench checks)
-  int span_digest(const SpanDev& span, uint64_t* key_xor, uint64_t* voff_sum);
+  // digests of a decoded span (bench / test checks): key xor, voff sum and
+  // the order-sensitive key / voff digests (k_digest)
+  int span_digest(const SpanDev& span, uint64_t out[4]);
 
   // host helpers on the block table
   int64_t pos_of_voff(uint64_t voff) const;
@@ -216,7 +227,13 @@ class Pipeline {
   int alloc_columns(uint64_t n, uint64_t stream_bytes, Columns* c);
   int hip_check(hipError_t e, const char* what);
 
+  template <typename... B>
+  void own(B&... b) {
+    ((b.owner = &streams_), ...);
+  }
+
   int device_ = 0;
+  StreamSet streams_;
   hipStream_t stream_ = nullptr;
   hipStream_t stream_copy_ = nullptr;  // run_streamed: host->HBM pieces
   std::vector<hipEvent_t> copy_ev_;

@@ -62,7 +62,8 @@ class GpuStats(C.Structure):
                 ("ms_locate", C.c_float), ("ms_inflate", C.c_float), ("ms_huff", C.c_float),
                 ("ms_lz77", C.c_float), ("ms_chain", C.c_float), ("ms_decode", C.c_float),
                 ("ms_total", C.c_float), ("status", i32), ("link_fallbacks", i32),
-                ("inflate_launches", i32), ("link_rewalks", i32), ("windows", i32), ("ms_tables", C.c_float)]
+                ("inflate_launches", i32), ("link_rewalks", i32), ("windows", i32), ("ms_tables", C.c_float),
+                ("reserved", i32), ("key_digest", u64), ("voff_digest", u64)]
 
 
 def _sig(name, res, args):
@@ -90,6 +91,7 @@ _sig("hbam_bytes_read", C.c_int, [P, C.POINTER(u64)])
 _sig("hbam_prefetch", C.c_int, [P, u64, u64])
 _sig("hbam_splitting_index_for_records", C.c_int, [C.POINTER(Opts), P, u64, i32, u64, C.POINTER(P), C.POINTER(u64)])
 _sig("hbam_build_splitting_index", C.c_int, [P, i32, C.POINTER(P), C.POINTER(u64)])
+_sig("hbam_splitting_entries", C.c_int, [P, u64, u64, i32, u64, C.POINTER(P), C.POINTER(u64), C.POINTER(u64)])
 _sig("hbam_guess_record_starts", C.c_int, [P, P, P, u64, P])
 _sig("hbam_guess_bgzf_block_starts", C.c_int, [P, P, P, u64, P])
 _sig("hbam_get_splits", C.c_int, [P, P, P, u64, P, u64, P, P, C.POINTER(u64)])
@@ -460,6 +462,22 @@ class BamFile:
         b = C.string_at(p, n.value)
         _L.hbam_free(p)
         return b
+
+    def splitting_entries(self, vstart, vend, granularity, ordinal0):
+        """This split's part of SplittingBAMIndexer.index (hbam_splitting_entries):
+        (records of the split, [voffs of the records at global ordinals k*g - 1])."""
+        p = P()
+        ne = u64()
+        nr = u64()
+        rc = _L.hbam_splitting_entries(self._h, vstart, vend, granularity, ordinal0, C.byref(p), C.byref(ne),
+                                       C.byref(nr))
+        if rc != OK:
+            raise self._err(rc)
+        try:
+            ent = np.frombuffer(C.string_at(p, 8 * ne.value), np.uint64).copy() if ne.value else np.zeros(0, np.uint64)
+        finally:
+            _L.hbam_free(p)
+        return nr.value, ent
 
     def guess_record_starts(self, begs, ends):
         n = len(begs)

@@ -45,7 +45,7 @@ extern "C" {
 #define HBAM_E_STATE 6
 #define HBAM_E_NOMEM 7
 
-#define HBAM_ABI_VERSION 2
+#define HBAM_ABI_VERSION 3
 
 /* htsjdk ValidationStringency, as util/SAMHeaderReader.java:45-46 reads it */
 #define HBAM_STRICT 0  /* htsjdk's default: SAMRecord.isValid errors -> SAMFormatException */
@@ -237,9 +237,9 @@ int64_t hbam_murmurhash3(const void *key, uint64_t len, int32_t seed);
 
 /* ---- device-resident decode (benchmark / multi-GPU shard driver) ---- */
 typedef struct hbam_gpu_stats {
-  uint64_t n_blocks;          /* BGZF blocks decoded (summed over windows) */
-  uint64_t compressed_bytes;  /* C of the decoded windows */
-  uint64_t inflated_bytes;    /* U of the decoded windows */
+  uint64_t n_blocks;          /* BGZF blocks located (summed over windows) */
+  uint64_t compressed_bytes;  /* C of the span: file bytes from its first block to where it ended, each byte once */
+  uint64_t inflated_bytes;    /* U of those blocks (windows overlap by a record's blocks: counted once) */
   uint64_t records;           /* N */
   uint64_t first_voff, last_voff;
   uint64_t key_xor, voff_sum; /* order-independent digests of the keys / voffs */
@@ -250,12 +250,30 @@ typedef struct hbam_gpu_stats {
   int32_t link_rewalks;       /* parallel-link re-walk rounds of this run */
   int32_t windows;            /* HBM windows the span was decoded in */
   float ms_tables;            /* k_huff_tables (ms_huff: k_inflate_huff, ms_lz77: k_inflate_lz77) */
+  int32_t reserved;
+  /* order-sensitive digests (flags bit2): sum over the span's records i of
+   * fmix64(x_i) * P^(n-1-i) mod 2^64, x = key / voff, P = HBAM_DIGEST_P;
+   * the digests of consecutive spans A, B compose as D(A) * P^|B| + D(B) */
+  uint64_t key_digest, voff_digest;
 } hbam_gpu_stats;
+#define HBAM_DIGEST_P 0x100000001b3ull
 
 /* hbam_decode_span with the records left in HBM (no host copies): counts,
  * digests (flags bit2) and per-stage timings (flags bit0) only; flags bit1
  * skips the field decode (chain + voffs only). */
 int hbam_decode_span_device(hbam_ctx *ctx, uint64_t vstart, uint64_t vend, int32_t flags, hbam_gpu_stats *st);
+
+/* The sharded SplittingBAMIndexer.index (SplittingBAMIndexer.java:262-287,
+ * SURVEY 8e step 3): the records of FileVirtualSplit [vstart, vend) read
+ * under the indexer's rules (readAlignment/fullySkip, :340-368), their count
+ * in *n_records and, given the global ordinal of the split's first record,
+ * the virtual offsets of those whose ordinal + 1 is a multiple of
+ * granularity in *entries (*n_entries of them; hbam_free).  The ranks of a
+ * multi-GPU read concatenate their entries in split order between the first
+ * record's voff and file_size << 16: byte-identical to index() over the
+ * whole file. */
+int hbam_splitting_entries(hbam_ctx *ctx, uint64_t vstart, uint64_t vend, int32_t granularity, uint64_t ordinal0,
+                           uint64_t **entries, uint64_t *n_entries, uint64_t *n_records);
 
 typedef struct hbam_gpu hbam_gpu;
 

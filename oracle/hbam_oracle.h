@@ -152,9 +152,20 @@ uint64_t orc_bgzf_compress(const uint8_t *data, uint64_t len, const uint32_t *bl
 typedef struct {
   uint64_t records, key_xor, voff_sum, blocks, u_bytes;
   int32_t status, rewalks;
+  /* order-sensitive digests over the records in file order (bench parity at
+   * 60 GB, where xor / sum would cancel over repeated segments):
+   * D = sum_i dmix(x_i) * ORC_DIGEST_P^(n-1-i) mod 2^64, x = key (mode 0)
+   * or voff (both modes); dmix = MurmurHash3 fmix64.  Composable:
+   * D(A ++ B) = D(A) * P^|B| + D(B). */
+  uint64_t key_digest, voff_digest;
 } orc_scan_result;
+#define ORC_DIGEST_P 0x100000001b3ull
 int orc_scan(const uint8_t *file, uint64_t len, int threads, int mode, int stringency, int32_t g,
              uint64_t max_blocks, uint8_t **sbi, uint64_t *sbi_len, orc_scan_result *res);
+/* mode 0 of orc_scan, also writing every record's key and voff in file order
+ * into keys / voffs (room for cap records; ORC_E_NOMEM if more) */
+int orc_scan_records(const uint8_t *file, uint64_t len, int threads, int stringency, uint64_t cap, int64_t *keys,
+                     uint64_t *voffs, orc_scan_result *res);
 
 /* zlib crc32, for tests */
 uint32_t orc_crc32(const uint8_t *p, uint64_t n);

@@ -60,6 +60,7 @@ def lib():
         L.orc_writable_decode.argtypes = [P, u64, P, u64, P]
         L.orc_set_stringency.argtypes = [P, C.c_int]
         L.orc_scan.argtypes = [P, u64, C.c_int, C.c_int, C.c_int, i32, u64, C.POINTER(P), C.POINTER(u64), P]
+        L.orc_scan_records.argtypes = [P, u64, C.c_int, C.c_int, u64, P, P, P]
         L.orc_record_invalid.argtypes = [P, i32, i32, P, C.c_int]
         L.orc_record_invalid.restype = C.c_int
         _LIB = L
@@ -288,7 +289,41 @@ def record_invalid(rec: bytes, n_ref, ref_len=None, strict=True):
 
 class _ScanResult(C.Structure):
     _fields_ = [("records", C.c_uint64), ("key_xor", C.c_uint64), ("voff_sum", C.c_uint64),
-                ("blocks", C.c_uint64), ("u_bytes", C.c_uint64), ("status", C.c_int32), ("rewalks", C.c_int32)]
+                ("blocks", C.c_uint64), ("u_bytes", C.c_uint64), ("status", C.c_int32), ("rewalks", C.c_int32),
+                ("key_digest", C.c_uint64), ("voff_digest", C.c_uint64)]
+
+
+DIGEST_P = 0x100000001B3  # ORC_DIGEST_P (hbam_oracle.h)
+M64 = (1 << 64) - 1
+
+
+def dmix(k):
+    """MurmurHash3 fmix64 (the digest's per-record mix)."""
+    k &= M64
+    k ^= k >> 33
+    k = (k * 0xFF51AFD7ED558CCD) & M64
+    k ^= k >> 33
+    k = (k * 0xC4CEB9FE1A85EC53) & M64
+    k ^= k >> 33
+    return k
+
+
+def digest(values):
+    """Order-sensitive digest of a sequence of u64 (orc_scan_result.key_digest):
+    sum_i dmix(x_i) * P^(n-1-i) mod 2^64, by Horner (small inputs / tests)."""
+    d = 0
+    for v in values:
+        d = (d * DIGEST_P + dmix(int(v))) & M64
+    return d
+
+
+def digest_concat(parts):
+    """Compose [(n, digest)] of consecutive record runs: D(A ++ B) = D(A) * P^|B| + D(B)."""
+    d, n = 0, 0
+    for k, dk in parts:
+        d = (d * pow(DIGEST_P, int(k), 1 << 64) + int(dk)) & M64
+        n += int(k)
+    return n, d
 
 
 def scan(data, threads=1, mode="decode", stringency=STRICT, granularity=4096, max_blocks=0):
@@ -314,3 +349,18 @@ def scan(data, threads=1, mode="decode", stringency=STRICT, granularity=4096, ma
     d = {f: getattr(r, f) for f, _ in _ScanResult._fields_}
     d["rc"] = rc
     return d, sbi
+
+
+def scan_records(data, cap, threads=1, stringency=STRICT):
+    """orc_scan_records: the restated reader over a whole file on `threads`
+    host threads, returning (result dict, keys int64[n], voffs uint64[n])."""
+    L = lib()
+    ptr, n = data.ctypes.data, data.nbytes
+    keys = np.empty(max(cap, 1), np.int64)
+    voffs = np.empty(max(cap, 1), np.uint64)
+    r = _ScanResult()
+    rc = L.orc_scan_records(ptr, n, threads, stringency, cap, keys.ctypes.data, voffs.ctypes.data, C.byref(r))
+    d = {f: getattr(r, f) for f, _ in _ScanResult._fields_}
+    d["rc"] = rc
+    k = int(r.records)
+    return d, keys[:k], voffs[:k]

@@ -33,6 +33,22 @@ static inline uint32_t s_rd32(const uint8_t *p) {
 }
 static inline int32_t s_rdi32(const uint8_t *p) { return (int32_t)s_rd32(p); }
 
+/* the order-sensitive digest of orc_scan_result (bench.py's 60 GB parity) */
+static inline uint64_t s_dmix(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+static uint64_t s_pow(uint64_t b, uint64_t e) {
+  uint64_t r = 1;
+  for (; e; e >>= 1, b *= b)
+    if (e & 1) r *= b;
+  return r;
+}
+
 typedef struct {
   uint64_t coff, ustart;
   uint32_t csize, isize;
@@ -128,7 +144,10 @@ typedef struct {
   int stopped;              /* the chain ended inside the range (EOF / error) */
   int status;
   uint64_t n, key_xor, voff_sum;
-  uint64_t *voffs, vcap;    /* index mode: every record voff */
+  uint64_t kdig, vdig;      /* order-sensitive digests of this range (Horner) */
+  uint64_t *voffs, vcap;    /* index mode (and keep): every record voff */
+  int64_t *keys;            /* decode mode with keep: every record key (capacity vcap) */
+  int keep;                 /* decode mode: keep every voff and key */
 } stask;
 
 static int is_dead_pos(const stask *t, uint64_t q) {
@@ -177,6 +196,7 @@ static int s_plausible_at(sreader *r, const stask *t, uint64_t q, int *st) {
 static void s_walk(stask *t, sreader *r) {
   uint64_t q = t->entry;
   t->n = t->key_xor = t->voff_sum = 0;
+  t->kdig = t->vdig = 0;
   t->stopped = 0;
   t->status = ORC_OK;
   int first = 1;  /* reader: the split start follows a seek (no dead check) */
@@ -213,8 +233,23 @@ static void s_walk(stask *t, sreader *r) {
         break;
       }
       const uint16_t flag = (uint16_t)(x[18] | (x[19] << 8));
-      t->key_xor ^= (uint64_t)orc_get_key(ref, s_rdi32(x + 8), flag, x + 36, (uint32_t)(bs - 32));
+      const uint64_t key = (uint64_t)orc_get_key(ref, s_rdi32(x + 8), flag, x + 36, (uint32_t)(bs - 32));
+      t->key_xor ^= key;
       t->voff_sum += v;
+      t->kdig = t->kdig * ORC_DIGEST_P + s_dmix(key);
+      t->vdig = t->vdig * ORC_DIGEST_P + s_dmix(v);
+      if (t->keep) {
+        if (t->n == t->vcap) {
+          t->vcap = t->vcap ? 2 * t->vcap : 1 << 16;
+          uint64_t *nv = (uint64_t *)realloc(t->voffs, t->vcap * 8);
+          int64_t *nk = (int64_t *)realloc(t->keys, t->vcap * 8);
+          if (nv) t->voffs = nv;
+          if (nk) t->keys = nk;
+          if (!nv || !nk) { t->status = ORC_E_NOMEM; t->stopped = 1; break; }
+        }
+        t->voffs[t->n] = v;
+        t->keys[t->n] = (int64_t)key;
+      }
       t->n++;
       q += 4 + (uint64_t)bs;
     } else {
@@ -226,6 +261,7 @@ static void s_walk(stask *t, sreader *r) {
       }
       t->voffs[t->n++] = v;
       t->voff_sum += v;
+      t->vdig = t->vdig * ORC_DIGEST_P + s_dmix(v);
       q += 4;
       if (bs > 0) {
         if ((uint64_t)bs > avail - 4 || is_dead_pos(t, q)) { t->status = ORC_E_IO; t->stopped = 1; break; } /* Skip failed */
@@ -271,8 +307,9 @@ static void *s_worker(void *arg) {
   return NULL;
 }
 
-int orc_scan(const uint8_t *file, uint64_t len, int threads, int mode, int stringency, int32_t g,
-             uint64_t max_blocks, uint8_t **sbi, uint64_t *sbi_len, orc_scan_result *res) {
+static int scan_impl(const uint8_t *file, uint64_t len, int threads, int mode, int stringency, int32_t g,
+                     uint64_t max_blocks, uint8_t **sbi, uint64_t *sbi_len, orc_scan_result *res, int64_t *keys_out,
+                     uint64_t *voffs_out, uint64_t out_cap) {
   memset(res, 0, sizeof *res);
   if (sbi) { *sbi = NULL; *sbi_len = 0; }
   if (mode == 1 && g <= 0) return ORC_E_ARG;
@@ -355,6 +392,7 @@ int orc_scan(const uint8_t *file, uint64_t len, int threads, int mode, int strin
     t->entry = t->lo_pos;
     t->guessed = i > 0;
     t->seek_start = i == 0;
+    t->keep = mode == 0 && keys_out != NULL;
     kb = ke;
   }
   spool P = {T, ntask, 0, PTHREAD_MUTEX_INITIALIZER};
@@ -389,15 +427,27 @@ int orc_scan(const uint8_t *file, uint64_t len, int threads, int mode, int strin
         } else { /* the previous chain jumped over this whole range */
           t->n = 0;
           t->key_xor = t->voff_sum = 0;
+          t->kdig = t->vdig = 0;
           t->exit = t->entry;
           t->stopped = 0;
           t->status = ORC_OK;
         }
       }
     }
+    if (t->keep) {
+      if (res->records + t->n > out_cap) {
+        rc = ORC_E_NOMEM;
+        break;
+      }
+      memcpy(voffs_out + res->records, t->voffs, t->n * 8);
+      memcpy(keys_out + res->records, t->keys, t->n * 8);
+    }
     res->records += t->n;
     res->key_xor ^= t->key_xor;
     res->voff_sum += t->voff_sum;
+    const uint64_t w = s_pow(ORC_DIGEST_P, t->n);
+    res->key_digest = res->key_digest * w + t->kdig;
+    res->voff_digest = res->voff_digest * w + t->vdig;
     if (mode == 1 && sbi) {
       for (uint64_t j = 0; j < t->n; j++) {
         if ((ordinal + j + 1) % (uint64_t)g == 0) {
@@ -428,10 +478,23 @@ int orc_scan(const uint8_t *file, uint64_t len, int threads, int mode, int strin
     *sbi_len = n * 8;
   }
   free(ent);
-  for (int i = 0; i < ntask; i++) free(T[i].voffs);
+  for (int i = 0; i < ntask; i++) {
+    free(T[i].voffs);
+    free(T[i].keys);
+  }
   free(T);
   free(dead);
   free(ref_len);
   free(b);
   return rc;
+}
+
+int orc_scan(const uint8_t *file, uint64_t len, int threads, int mode, int stringency, int32_t g,
+             uint64_t max_blocks, uint8_t **sbi, uint64_t *sbi_len, orc_scan_result *res) {
+  return scan_impl(file, len, threads, mode, stringency, g, max_blocks, sbi, sbi_len, res, NULL, NULL, 0);
+}
+
+int orc_scan_records(const uint8_t *file, uint64_t len, int threads, int stringency, uint64_t cap, int64_t *keys,
+                     uint64_t *voffs, orc_scan_result *res) {
+  return scan_impl(file, len, threads, 0, stringency, 0, 0, NULL, NULL, res, keys, voffs, cap);
 }

@@ -124,3 +124,31 @@ def test_oracle_vs_python_synthetic(kw):
     assert [v for v, _ in pr] == [int(x) for x in r["voff"]]
     for g in (1, 7, 4096):
         assert s.splitting_index(g) == py_oracle.splitting_index(d, g)
+
+
+def test_scan_digests_are_order_sensitive_and_compose():
+    """orc_scan's key / voff digests (the 60 GB bench parity): equal to the
+    Horner digest of the single-threaded oracle's columns at any thread count,
+    composable over consecutive runs, and changed by swapping two records --
+    which the xor / sum digests cannot see."""
+    from hbam import synth
+    data, _ = synth.make_bam(6000, as_numpy=True, block_payload=8192)
+    rc, want = orc.Stream(data.tobytes()).decode_all()
+    assert rc == 0
+    keys = want["key"].astype(np.uint64)
+    kd, vd = orc.digest(keys), orc.digest(want["voff"])
+    for threads in (1, 3, 8):
+        r, _ = orc.scan(data, threads=threads)
+        assert (r["records"], r["key_digest"], r["voff_digest"]) == (len(keys), kd, vd)
+    ri, _ = orc.scan(data, threads=4, mode="index")
+    assert ri["voff_digest"] == vd
+    a = len(keys) // 3
+    assert orc.digest_concat([(a, orc.digest(keys[:a])), (len(keys) - a, orc.digest(keys[a:]))]) == (len(keys), kd)
+    sw = keys.copy()
+    i = int(np.nonzero(sw[:-1] != sw[1:])[0][0])
+    sw[[i, i + 1]] = sw[[i + 1, i]]
+    assert orc.digest(sw) != kd
+    d, k, v = orc.scan_records(data, len(keys), threads=5)
+    assert d["rc"] == 0
+    np.testing.assert_array_equal(k, want["key"])
+    np.testing.assert_array_equal(v, want["voff"])
