@@ -32,8 +32,9 @@ struct hbam_ctx {
   std::unique_ptr<BamFile> f;
   std::unique_ptr<hbam::Pipeline> codec;  // hbam_open_codec: a pipeline with no file
   std::string err;
-  SpanCursor cursor;
-  HostBatch batch;
+  SpanCursor cursor;    // (destroyed before f: it drains its copies on f's pipeline stream)
+  HostBatch wbatch;     // the columns of the last hbam_decode_writables
+  hadoop_bam::BatchView batch;  // the last batch handed out (cursor slots or wbatch)
   hbam::SpanDev wspan;  // device result of the last hbam_decode_writables
   bool last_is_writables = false;
 };
@@ -80,24 +81,24 @@ int finish_open(int rc, std::unique_ptr<BamFile>&& f, const std::string& err, hb
 
 bool valid_stringency(const hbam_opts* o) { return !o || (o->stringency >= 0 && o->stringency <= 2); }
 
-void fill_batch(const HostBatch& h, hbam_batch* out) {
+void fill_batch(const hadoop_bam::BatchView& h, hbam_batch* out) {
   out->n = h.n;
-  out->ref_id = h.ref_id.data();
-  out->pos = h.pos.data();
-  out->l_seq = h.l_seq.data();
-  out->next_ref_id = h.next_ref_id.data();
-  out->next_pos = h.next_pos.data();
-  out->tlen = h.tlen.data();
-  out->l_read_name = h.l_read_name.data();
-  out->mapq = h.mapq.data();
-  out->bin = h.bin.data();
-  out->n_cigar = h.n_cigar.data();
-  out->flag = h.flag.data();
-  out->key = h.key.data();
-  out->voff = h.voff.data();
-  out->rest_off = h.rest_off.data();
-  out->rest_len = h.rest_len.data();
-  out->data = h.data.data();
+  out->ref_id = h.ref_id;
+  out->pos = h.pos;
+  out->l_seq = h.l_seq;
+  out->next_ref_id = h.next_ref_id;
+  out->next_pos = h.next_pos;
+  out->tlen = h.tlen;
+  out->l_read_name = h.l_read_name;
+  out->mapq = h.mapq;
+  out->bin = h.bin;
+  out->n_cigar = h.n_cigar;
+  out->flag = h.flag;
+  out->key = h.key;
+  out->voff = h.voff;
+  out->rest_off = h.rest_off;
+  out->rest_len = h.rest_len;
+  out->data = h.data;
   out->data_len = h.data_len;
 }
 
@@ -421,8 +422,8 @@ int hbam_encode_writables(hbam_ctx* ctx, uint8_t* out, uint64_t cap, uint64_t* o
   }
   *len = bytes;
   if (offs) {  // encodings have the records' own lengths: record i starts where its bytes did
-    const HostBatch& h = ctx->batch;
-    for (uint64_t i = 0; i < h.n; ++i) offs[i] = h.rest_off[i] - 36 - (h.rest_off[0] - 36);
+    const hadoop_bam::BatchView& h = ctx->batch;
+    for (uint64_t i = 0; i < h.n; ++i) offs[i] = h.rest_off[i] - h.rest_off[0];
     offs[h.n] = bytes;
   }
   if (!out) return HBAM_OK;
@@ -464,13 +465,15 @@ int hbam_decode_writables(hbam_ctx* ctx, const void* buf, uint64_t len, const ui
     span = hbam::SpanDev();
     return rc;
   }
-  HostBatch& h = ctx->batch;
+  HostBatch& h = ctx->wbatch;
   h.n = 0;
   h.data_len = 0;
   h.window_pos.clear();
+  ctx->batch = hadoop_bam::BatchView();
   rc = hadoop_bam::fetch_span(p, span, 0, span.n, &h, &ctx->err);
   if (rc != HBAM_OK) return rc;
-  fill_batch(h, out);
+  ctx->batch = hadoop_bam::BatchView::of(h);
+  fill_batch(ctx->batch, out);
   out->status = span.status;
   if (span.status != HBAM_OK) {
     ctx->err = span.error;

@@ -84,4 +84,49 @@ struct Columns {
 };
 constexpr uint32_t kLongHash = 2048;
 
+// n records' columns in one buffer (the drop-in batch path: a decoded
+// window's records exported out of the pipeline on the device, and the
+// page-locked host batches): 16 B-aligned pieces, widest columns first.
+// rec_pos (device slots only) has n + 1 entries, the last = the slot's byte
+// count.
+struct ColLayout {
+  enum : int {
+    kKey, kRestOff, kVoff, kRecPos, kRefId, kPos, kLSeq, kNextRefId, kNextPos, kTlen, kRestLen, kBin, kNCigar,
+    kFlag, kLReadName, kMapq, kCount
+  };
+  uint64_t off[kCount];
+  uint64_t bytes;
+  static constexpr uint32_t size_of(int c) { return c <= kRecPos ? 8 : c <= kRestLen ? 4 : c <= kFlag ? 2 : 1; }
+  ColLayout(uint64_t n, bool rec_pos) {
+    uint64_t p = 0;
+    for (int c = 0; c < kCount; ++c) {
+      off[c] = p;
+      const uint64_t k = c == kRecPos ? (rec_pos ? n + 1 : 0) : n;
+      p += (k * size_of(c) + 15) & ~15ull;
+    }
+    bytes = p;
+  }
+  // the Columns (no long-key list) of a buffer laid out this way
+  Columns at(uint8_t* b, uint64_t** rec_pos) const {
+    Columns c{};
+    c.key = reinterpret_cast<int64_t*>(b + off[kKey]);
+    c.rest_off = reinterpret_cast<uint64_t*>(b + off[kRestOff]);
+    c.voff = reinterpret_cast<uint64_t*>(b + off[kVoff]);
+    if (rec_pos) *rec_pos = reinterpret_cast<uint64_t*>(b + off[kRecPos]);
+    c.ref_id = reinterpret_cast<int32_t*>(b + off[kRefId]);
+    c.pos = reinterpret_cast<int32_t*>(b + off[kPos]);
+    c.l_seq = reinterpret_cast<int32_t*>(b + off[kLSeq]);
+    c.next_ref_id = reinterpret_cast<int32_t*>(b + off[kNextRefId]);
+    c.next_pos = reinterpret_cast<int32_t*>(b + off[kNextPos]);
+    c.tlen = reinterpret_cast<int32_t*>(b + off[kTlen]);
+    c.rest_len = reinterpret_cast<uint32_t*>(b + off[kRestLen]);
+    c.bin = reinterpret_cast<uint16_t*>(b + off[kBin]);
+    c.n_cigar = reinterpret_cast<uint16_t*>(b + off[kNCigar]);
+    c.flag = reinterpret_cast<uint16_t*>(b + off[kFlag]);
+    c.l_read_name = b + off[kLReadName];
+    c.mapq = b + off[kMapq];
+    return c;
+  }
+};
+
 }  // namespace hbam

@@ -149,6 +149,7 @@ int BamFile::init(const OpenOptions& o, std::string* err) {
   src_.dev.owner = &pipe_->streams();  // kernels read the resident copy on the pipeline's streams
   pipe_->set_stringency(o.stringency);
   set_window_bytes(o.window_bytes ? o.window_bytes : kDefaultWindowBytes);
+  window_explicit_ = o.window_bytes != 0;
   int rc;
   if (o.parse_header) {
     rc = parse_header();
@@ -351,10 +352,10 @@ int BamFile::parse_header() {
 }
 
 int BamFile::decode_step(Carry from, uint64_t vend, hbam::ChainMode mode, bool decode, bool continuation,
-                         Step* out) {
+                         Step* out, uint64_t window) {
   *out = Step();
   Carry c = from;
-  uint64_t span_w = window_bytes_;
+  uint64_t span_w = window ? std::max<uint64_t>(window, 1ull << 16) : window_bytes_;
   bool host_only = false, clamp = vend != ~0ull;
   for (int guard = 0; guard < 96; ++guard) {
     out->next = c;
@@ -897,6 +898,29 @@ int HostBatch::reserve(uint64_t nn, uint64_t bytes) {
   return ok ? kOk : kErrNoMem;
 }
 
+BatchView BatchView::of(const HostBatch& h) {
+  BatchView v;
+  v.n = h.n;
+  v.ref_id = h.ref_id.data();
+  v.pos = h.pos.data();
+  v.l_seq = h.l_seq.data();
+  v.next_ref_id = h.next_ref_id.data();
+  v.next_pos = h.next_pos.data();
+  v.tlen = h.tlen.data();
+  v.l_read_name = h.l_read_name.data();
+  v.mapq = h.mapq.data();
+  v.bin = h.bin.data();
+  v.n_cigar = h.n_cigar.data();
+  v.flag = h.flag.data();
+  v.key = h.key.data();
+  v.voff = h.voff.data();
+  v.rest_off = h.rest_off.data();
+  v.rest_len = h.rest_len.data();
+  v.data = h.data.data();
+  v.data_len = h.data_len;
+  return v;
+}
+
 int fetch_span(hbam::Pipeline& p, const SpanDev& s, uint64_t k, uint64_t m, HostBatch* h, std::string* err) {
   if (m == 0) return kOk;
   const hipStream_t st = p.stream();
@@ -951,144 +975,11 @@ int fetch_span(hbam::Pipeline& p, const SpanDev& s, uint64_t k, uint64_t m, Host
   return kOk;
 }
 
-static hbam::Columns offset_columns(const hbam::Columns& c, uint64_t k) {
-  hbam::Columns o = c;
-  o.ref_id += k;
-  o.pos += k;
-  o.l_seq += k;
-  o.next_ref_id += k;
-  o.next_pos += k;
-  o.tlen += k;
-  o.l_read_name += k;
-  o.mapq += k;
-  o.bin += k;
-  o.n_cigar += k;
-  o.flag += k;
-  o.key += k;
-  o.voff += k;
-  o.rest_off += k;
-  o.rest_len += k;
-  return o;
-}
-
-int SpanCursor::next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t max_records, HostBatch* h,
-                           uint64_t* next_voff, std::string* err) {
-  h->n = 0;
-  h->data_len = 0;
-  h->window_pos.clear();
-  batch_one_window_ = false;
-  batch_end_.clear();
-  const bool cont = valid_ && vend == vend_ && vstart == next_voff_;
-  if (!cont) {  // a seek to the split start (or anywhere in it)
-    valid_ = true;
-    vend_ = vend;
-    k_ = 0;
-    const int rc = f.decode_step(Carry{vstart >> 16, vstart & 0xffff}, vend, hbam::kReader, true, false, &step_);
-    if (rc != kOk) {
-      valid_ = false;
-      *err = f.error();
-      return rc;
-    }
-  }
-  int status = kOk;
-  for (;;) {
-    const uint64_t avail = step_.span.n - k_;
-    if (avail == 0) {
-      if (step_.ended) {
-        status = step_.status;
-        if (status != kOk) *err = step_.error;
-        break;
-      }
-      if (h->n && max_records) break;  // bounded batches stay inside one window
-      const int rc = f.decode_step(step_.next, vend, hbam::kReader, true, true, &step_);
-      k_ = 0;
-      if (rc != kOk) {
-        valid_ = false;
-        *err = f.error();
-        return rc;
-      }
-      continue;
-    }
-    const uint64_t m = max_records ? std::min(max_records - h->n, avail) : avail;
-    const bool first_segment = h->n == 0;
-    int rc = fetch_span(f.pipe(), step_.span, k_, m, h, err);
-    if (rc != kOk) return rc;
-    if (first_segment) {
-      batch_k0_ = k_;
-      batch_n_ = m;
-      batch_one_window_ = true;
-    } else {
-      batch_one_window_ = false;
-    }
-    k_ += m;
-    if (max_records && h->n >= max_records) break;
-  }
-  if (k_ < step_.span.n) {
-    uint64_t v = 0;
-    if (hipMemcpy(&v, step_.span.rec_voff + k_, 8, hipMemcpyDeviceToHost) != hipSuccess) {
-      *err = "hipMemcpy D2H failed";
-      return kErrDevice;
-    }
-    *next_voff = v;
-  } else if (!step_.ended || status != kOk) {
-    *next_voff = step_.next.voff();
-  } else {
-    *next_voff = vend;
-  }
-  next_voff_ = *next_voff;
-  if (batch_one_window_) {  // block end of each record's last byte (+ the read-ahead one) for reader_position
-    const uint64_t base = h->window_pos.empty() ? 0 : h->window_pos[0];
-    batch_end_.resize(h->n + 1);
-    for (uint64_t i = 0; i < h->n; ++i) batch_end_[i] = f.block_end_of(base + h->rest_off[i] + h->rest_len[i] - 1);
-    batch_end_[h->n] = ~0ull;
-    if (k_ < step_.span.n) {
-      uint64_t ro = 0;
-      uint32_t rl = 0;
-      if (hipMemcpy(&ro, step_.span.col.rest_off + k_, 8, hipMemcpyDeviceToHost) == hipSuccess &&
-          hipMemcpy(&rl, step_.span.col.rest_len + k_, 4, hipMemcpyDeviceToHost) == hipSuccess)
-        batch_end_[h->n] = f.block_end_of(ro + rl - 1);
-    }
-  }
-  return status;
-}
-
-bool SpanCursor::last_batch_span(SpanDev* out) const {
-  if (!valid_ || !batch_one_window_) return false;
-  *out = step_.span;
-  out->n = batch_n_;
-  out->rec_pos = step_.span.rec_pos + batch_k0_;
-  out->rec_voff = step_.span.rec_voff + batch_k0_;
-  out->col = offset_columns(step_.span.col, batch_k0_);
-  return true;
-}
-
-int SpanCursor::reader_position(uint64_t i, uint64_t* pos, std::string* err) const {
-  // BAMRecordReader.getProgress (:209-219) reads in.position(): htsjdk's
-  // iterator has already read the record after the one just returned (when
-  // the split holds one), so the stream stands at the end of the block
-  // holding that record's last byte.
-  if (!valid_ || batch_end_.size() < 2 || i + 1 >= batch_end_.size()) {
-    *err = "no position for this record: the last batch spans several windows";
-    return kErrState;
-  }
-  *pos = batch_end_[i + 1] != ~0ull ? batch_end_[i + 1] : batch_end_[i];
-  return kOk;
-}
-
-int SpanCursor::initial_position(uint64_t* pos, std::string* err) const {
-  if (!valid_ || batch_end_.size() < 2) {
-    *err = "no batch";
-    return kErrState;
-  }
-  *pos = batch_end_[0];
-  return kOk;
-}
-
 int BAMRecordReader::initialize(BamFile& f, const FileVirtualSplit& split) {
   // :131-133 re-entrant initialize
   f_ = &f;
   cur_span_.reset();
-  b_.n = 0;
+  b_ = BatchView();
   cur_ = 0;
   started_ = reached_end_ = have_batch_ = false;
   status_ = kOk;
@@ -1131,7 +1022,7 @@ bool BAMRecordReader::nextKeyValue() {
   view_.n_cigar = b_.n_cigar[cur_];
   view_.flag = b_.flag[cur_];
   view_.voff = b_.voff[cur_];
-  view_.rest = b_.data.data() + b_.rest_off[cur_];
+  view_.rest = b_.data + b_.rest_off[cur_];
   view_.rest_len = b_.rest_len[cur_];
   return true;
 }
@@ -1140,7 +1031,6 @@ float BAMRecordReader::getProgress() const {
   if (reached_end_) return 1.0f;
   const uint64_t fileEnd = virtualEnd_ >> 16;
   if (b_.n == 0) return 0.0f;
-  // before the first nextKeyValue the iterator has read record 0
   // before the first nextKeyValue the iterator has read record 0
   uint64_t filePos = 0;
   std::string e;

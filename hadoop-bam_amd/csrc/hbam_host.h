@@ -22,6 +22,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <set>
@@ -35,6 +36,7 @@ namespace hadoop_bam {
 using hbam::SpanDev;
 
 constexpr uint64_t kDefaultWindowBytes = 4ull << 30;  // hadoopbam.gpu.window-bytes default
+constexpr uint64_t kDropinWindowBytes = 256ull << 20;  // hbam_decode_span windows when the property is unset
 
 // Page-locked host array (batch columns handed to a JNI caller as direct
 // ByteBuffers; D2H copies into it run at the PCIe rate).
@@ -135,8 +137,15 @@ class BamFile {
   // Decode the part of FileVirtualSplit [.., vend) that starts at `from`
   // and lies in one window.  continuation: `from` is the carry of the
   // previous step (not a reader seek).
+  // window: compressed bytes per window (0 = window_bytes())
   int decode_step(Carry from, uint64_t vend, hbam::ChainMode mode, bool decode, bool continuation,
-                  Step* out);
+                  Step* out, uint64_t window = 0);
+  // window of the drop-in batch path (hbam_decode_span): hadoopbam.gpu.window-bytes
+  // when set, else kDropinWindowBytes -- several windows per split, so that
+  // one window's batches cross PCIe while the next decodes
+  uint64_t dropin_window_bytes() const {
+    return window_explicit_ ? window_bytes_ : std::min(window_bytes_, kDropinWindowBytes);
+  }
 
   // Every BGZF block of the file (window by window; cached).  ustart is the
   // offset in the whole inflated stream.
@@ -156,6 +165,7 @@ class BamFile {
   uint64_t staged_lo_ = 0, staged_hi_ = 0;  // the range handed to Pipeline::stage last
   bool win_free_ = false;
   uint64_t window_bytes_ = kDefaultWindowBytes;
+  bool window_explicit_ = false;
   int32_t n_ref_ = 0;
   std::string text_;
   std::vector<std::string> ref_names_;
@@ -284,7 +294,8 @@ class BAMInputFormat {
 };
 
 // Host copy of a run of decoded records: the LazyBAMRecordFactory argument
-// list + key + voff + the variable-length block of each record.
+// list + key + voff + the variable-length block of each record (owning;
+// hbam_decode_writables and whole-split batches).
 struct HostBatch {
   PinnedVec<int32_t> ref_id, pos, l_seq, next_ref_id, next_pos, tlen;
   PinnedVec<uint8_t> l_read_name, mapq;
@@ -298,44 +309,110 @@ struct HostBatch {
   int reserve(uint64_t n, uint64_t bytes);
 };
 
+// The host columns of one batch as handed to the caller (the hbam_batch
+// field set): pointers into a HostBatch or into a page-locked batch slot.
+struct BatchView {
+  uint64_t n = 0;
+  const int32_t *ref_id = nullptr, *pos = nullptr, *l_seq = nullptr, *next_ref_id = nullptr, *next_pos = nullptr,
+                *tlen = nullptr;
+  const uint8_t *l_read_name = nullptr, *mapq = nullptr;
+  const uint16_t *bin = nullptr, *n_cigar = nullptr, *flag = nullptr;
+  const int64_t* key = nullptr;
+  const uint64_t *voff = nullptr, *rest_off = nullptr;
+  const uint32_t* rest_len = nullptr;
+  const uint8_t* data = nullptr;  // rest_off is relative to data
+  uint64_t data_len = 0;
+  static BatchView of(const HostBatch& h);
+};
+
 // Records [k, k + m) of a device span appended to h at record h->n (columns
 // and their bytes; D2H on the pipeline stream into page-locked memory).
 int fetch_span(hbam::Pipeline& p, const SpanDev& s, uint64_t k, uint64_t m, HostBatch* h, std::string* err);
 
-// A split being read in bounded batches (BAMRecordReader's iterator): the
-// current window's decoded span stays on the device and batches are copied
-// out of it; the next window is decoded when the batch reaches its end.
+// A split being read in bounded batches (BAMRecordReader's iterator,
+// hbam_decode_span).  The split is decoded window by window
+// (BamFile::dropin_window_bytes) and each decoded window's records are
+// exported from the pipeline into one of two device slots, so that:
+//   * while the caller holds batch j, batch j+1 is already crossing PCIe
+//     (SDMA copies of its column slices and bytes; two page-locked host
+//     slots in turn);
+//   * when a window's first batch is handed out, the next window is decoded
+//     (its compressed bytes go host->HBM while this window's batches go
+//     HBM->host: the link is full duplex with the copy engines).
+// A batch holds records of one window.  max_records = 0 returns the rest of
+// the split in one owning HostBatch (several windows appended).
 class SpanCursor {
  public:
+  SpanCursor() = default;
+  SpanCursor(const SpanCursor&) = delete;
+  SpanCursor& operator=(const SpanCursor&) = delete;
+  ~SpanCursor();
   // Up to max_records records (0 = the rest of the split) starting at vstart;
   // *next_voff = where the next call continues (>= vend when the split is
   // exhausted).  A vstart equal to the previous call's *next_voff continues
-  // the same split without re-decoding.
-  int next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t max_records, HostBatch* h,
+  // the same split without re-decoding.  *out stays valid until the next call.
+  int next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t max_records, BatchView* out,
                  uint64_t* next_voff, std::string* err);
   // device view of the records of the last batch when they lie in one window
   bool last_batch_span(SpanDev* out) const;
   // BAMRecordReader.getProgress's in.position() after record i of the last
-  // batch; kErrState when the last batch cannot answer (see hbam.h)
+  // batch (htsjdk's iterator has read the record after it)
   int reader_position(uint64_t i, uint64_t* pos, std::string* err) const;
   // ... before the first record is returned (htsjdk has read record 0)
   int initial_position(uint64_t* pos, std::string* err) const;
   bool valid() const { return valid_; }
-  void reset() {
-    valid_ = false;
-    batch_end_.clear();
-  }
+  // forget the split (waits for this cursor's copies in flight)
+  void reset();
 
  private:
+  struct Window {  // one decoded window's records, exported out of the pipeline
+    hbam::DevBuf<uint8_t> cols, bytes;
+    hbam::Columns col{};
+    uint64_t* rec_pos = nullptr;  // n + 1 entries: slot byte offsets, [n] = nbytes
+    uint64_t n = 0, nbytes = 0, base_pos = 0, id = 0;
+    std::shared_ptr<const std::vector<hbam::BlockInfo>> blocks;  // block table (positions)
+    Carry next;
+    bool ended = true;
+    int status = 0;
+    std::string error;
+    hipEvent_t ready = nullptr;  // export done
+  };
+  struct Slot {  // a page-locked batch: ColLayout(m) columns, then the bytes
+    uint8_t* mem = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+    bool busy = false;            // copies queued
+    uint64_t win = 0, k = 0, m = 0, start = 0, end = 0, ahead_end = 0, next_voff = 0;
+  };
+  int ensure_streams(hbam::Pipeline& p, std::string* err);
+  int decode_window(BamFile& f, Carry from, bool cont, Window* w, std::string* err);
+  int issue(const Window& w, uint64_t k, uint64_t m, Slot* s, std::string* err);
+  int drain();
+  int next_batch_all(BamFile& f, uint64_t vstart, uint64_t vend, BatchView* out, uint64_t* next_voff,
+                     std::string* err);
+  uint64_t block_end(const std::vector<hbam::BlockInfo>& B, uint64_t pos) const;
+
   bool valid_ = false;
   uint64_t vend_ = 0, next_voff_ = 0;
-  Step step_;
-  uint64_t k_ = 0;                    // next record of step_ to hand out
-  uint64_t batch_k0_ = 0, batch_n_ = 0;  // the last batch within step_ (single window)
-  bool batch_one_window_ = false;
-  // file offset of the end of the block holding each batch record's last
-  // byte (+ the read-ahead record's), computed while the batch is built
-  std::vector<uint64_t> batch_end_;
+  hipStream_t d2h_ = nullptr, meta_ = nullptr;
+  int device_ = -1;
+  hbam::StreamSet own_;            // the pipeline stream + d2h_ + meta_ (owner of the slots' device buffers)
+  Window win_[2];
+  uint64_t front_ = 0, nwin_ = 0;  // window ids: front_ = the one being handed out; nwin_ decoded so far
+  uint64_t k_ = 0;                 // next record of the front window
+  Slot slot_[2];
+  int cur_ = -1;                   // slot of the last batch handed out
+  uint64_t* small_ = nullptr;      // page-locked scratch for the boundary reads
+  // the last batch: where its records came from (positions / encode)
+  uint64_t last_win_ = 0, last_k_ = 0, last_m_ = 0, last_start_ = 0, last_ahead_end_ = 0, last_base_pos_ = 0;
+  bool last_bounded_ = false;
+  BatchView last_view_;
+  std::shared_ptr<const std::vector<hbam::BlockInfo>> last_blocks_;
+  // max_records = 0: the whole rest of the split, appended window by window
+  HostBatch all_;
+  std::vector<std::pair<uint64_t, std::shared_ptr<const std::vector<hbam::BlockInfo>>>> all_seg_;  // first record, blocks
+  Step all_step_;
+  bool all_one_window_ = false;
 };
 
 // BAMRecordReader (BAMRecordReader.java:63-233) over one FileVirtualSplit.
@@ -374,7 +451,7 @@ class BAMRecordReader {
   bool fill();
   BamFile* f_ = nullptr;
   SpanCursor cur_span_;
-  HostBatch b_;
+  BatchView b_;
   uint64_t cur_ = 0, next_voff_ = 0;
   bool started_ = false, reached_end_ = false, have_batch_ = false;
   int status_ = 0;

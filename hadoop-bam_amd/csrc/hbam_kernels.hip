@@ -2906,6 +2906,44 @@ __global__ __launch_bounds__(256) void k_digest(const int64_t* __restrict__ keys
 }
 
 // ---------------------------------------------------------------------------
+// Drop-in batch path (hbam_decode_span): a decoded window's records leave the
+// pipeline's buffers for an export slot (so the next window decodes while
+// this one's batches cross PCIe; the batches go to the host by SDMA copies
+// of column slices).  HBM-bound copy, one thread per record: every column's
+// stores coalesce across the wave.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void copy_record_fields(const Columns& s, uint64_t i, const Columns& d, uint64_t j,
+                                                   uint64_t rest_base) {
+  d.key[j] = s.key[i];
+  d.rest_off[j] = s.rest_off[i] - rest_base;
+  d.voff[j] = s.voff[i];
+  d.ref_id[j] = s.ref_id[i];
+  d.pos[j] = s.pos[i];
+  d.l_seq[j] = s.l_seq[i];
+  d.next_ref_id[j] = s.next_ref_id[i];
+  d.next_pos[j] = s.next_pos[i];
+  d.tlen[j] = s.tlen[i];
+  d.rest_len[j] = s.rest_len[i];
+  d.bin[j] = s.bin[i];
+  d.n_cigar[j] = s.n_cigar[i];
+  d.flag[j] = s.flag[i];
+  d.l_read_name[j] = s.l_read_name[i];
+  d.mapq[j] = s.mapq[i];
+}
+
+// slot <- records [0, n) of a span; positions rebased so that window position
+// `base` (the first record's start) is slot byte 0; dpos[n] = the slot's bytes
+__global__ __launch_bounds__(256) void k_export_records(Columns s, const uint64_t* __restrict__ spos, Columns d,
+                                                        uint64_t* __restrict__ dpos, uint64_t n, uint64_t base,
+                                                        uint64_t nbytes) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    copy_record_fields(s, i, d, i, base);
+    dpos[i] = spos[i] - base;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) dpos[n] = nbytes;
+}
+
+// ---------------------------------------------------------------------------
 // SAMRecordWritable codec (SAMRecordWritable.java:55-68)
 // ---------------------------------------------------------------------------
 // write(): [htsjdk] BAMRecordCodec.encode of an unmodified BAMRecord emits
@@ -3232,6 +3270,12 @@ hipError_t launch_sbi_emit(const uint64_t* voff, uint64_t n, uint32_t g, uint64_
 hipError_t launch_next_pos(const uint8_t* u, const uint64_t* rec_pos, uint64_t n, uint64_t p0, int mode,
                            uint64_t* out, hipStream_t s) {
   hipLaunchKernelGGL(k_next_pos, dim3(1), dim3(64), 0, s, u, rec_pos, n, p0, mode, out);
+  return hipGetLastError();
+}
+hipError_t launch_export_records(const Columns& src, const uint64_t* src_pos, const Columns& dst, uint64_t* dst_pos,
+                                 uint64_t n, uint64_t base, uint64_t nbytes, hipStream_t s) {
+  hipLaunchKernelGGL(k_export_records, dim3(grid_for(std::max<uint64_t>(n, 1), 256, 8192)), dim3(256), 0, s, src,
+                     src_pos, dst, dst_pos, n, base, nbytes);
   return hipGetLastError();
 }
 hipError_t launch_digest(const int64_t* keys, const uint64_t* voffs, uint64_t n, uint64_t* out, hipStream_t s) {

@@ -101,7 +101,12 @@ hipError_t launch_sbi_emit(const uint64_t* voff, uint64_t n, uint32_t g, uint64_
 // *out = the chain successor of the last of n records (p0 when n == 0)
 hipError_t launch_next_pos(const uint8_t* u, const uint64_t* rec_pos, uint64_t n, uint64_t p0, int mode,
                            uint64_t* out, hipStream_t s);
-// out[0] ^= xor of keys (if keys), out[1] += sum of voffs
+// drop-in batches: records [0, n) of a decoded span -> an export slot
+// (ColLayout with rec_pos; positions rebased by base, dst_pos[n] = nbytes)
+hipError_t launch_export_records(const Columns& src, const uint64_t* src_pos, const Columns& dst, uint64_t* dst_pos,
+                                 uint64_t n, uint64_t base, uint64_t nbytes, hipStream_t s);
+// out[0] ^= xor of keys (if keys), out[1] += sum of voffs, out[2..3] += the
+// order-sensitive key / voff digests (see k_digest)
 hipError_t launch_digest(const int64_t* keys, const uint64_t* voffs, uint64_t n, uint64_t* out, hipStream_t s);
 // keys deferred by decode_record (rest > kLongHash bytes): one wave per record
 hipError_t launch_long_hash(const uint8_t* u, const uint64_t* rec_pos, const Columns& col, hipStream_t s);

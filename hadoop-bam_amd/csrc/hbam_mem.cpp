@@ -1,8 +1,14 @@
 // hbam_mem.cpp -- the block caches of hbam_mem.h.
 #include "hbam_mem.h"
 
+#include <sys/mman.h>
+
+#include <algorithm>
 #include <map>
 #include <mutex>
+#include <set>
+#include <thread>
+#include <vector>
 
 namespace hbam {
 namespace {
@@ -97,6 +103,41 @@ void dev_free(void* p, size_t bytes) {
   if (!dev_cache().put(p, bytes, dev, kDevCap)) (void)hipFree(p);
 }
 
+namespace {
+// Large page-locked blocks are not hipHostMalloc'ed: that zero-fills every
+// page on one thread (~96 ms per GiB on the MI355X box, scripts/pin_probe.py).
+// They are mapped (2 MiB aligned, huge pages advised), first-touched on
+// several threads, then registered (hipHostRegister: ~3 ms per GiB).
+constexpr size_t kRegisterMin = 16ull << 20;
+constexpr size_t kHuge = 2ull << 20;
+
+std::mutex& reg_mu() {
+  static std::mutex* m = new std::mutex();
+  return *m;
+}
+std::set<void*>& registered() {  // blocks from the map + register path
+  static std::set<void*>* s = new std::set<void*>();
+  return *s;
+}
+
+void* map_and_touch(size_t bytes) {
+  void* q = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (q == MAP_FAILED) return nullptr;
+  (void)madvise(q, bytes, MADV_HUGEPAGE);
+  const size_t nt = std::min<size_t>(8, std::max<size_t>(1, bytes / (32ull << 20)));
+  const size_t per = (bytes / nt + kHuge - 1) & ~(kHuge - 1);
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < nt; ++t)
+    th.emplace_back([q, bytes, per, t]() {
+      volatile uint8_t* b = static_cast<uint8_t*>(q);
+      for (size_t o = t * per; o < std::min(bytes, (t + 1) * per); o += 4096) b[o] = 0;
+    });
+  for (auto& x : th) x.join();
+  return q;
+}
+
+}  // namespace
+
 hipError_t pinned_alloc(void** p, size_t bytes, size_t* got) {
   if (bytes == 0) bytes = 1;
   if (bytes >= kMinCached) {
@@ -105,16 +146,47 @@ hipError_t pinned_alloc(void** p, size_t bytes, size_t* got) {
       return hipSuccess;
     }
   }
+  if (bytes >= kRegisterMin) {
+    const size_t len = (bytes + kHuge - 1) & ~(kHuge - 1);
+    void* q = map_and_touch(len);
+    if (q) {
+      const hipError_t e = hipHostRegister(q, len, hipHostRegisterDefault);
+      if (e == hipSuccess) {
+        std::lock_guard<std::mutex> lk(reg_mu());
+        registered().insert(q);
+        *p = q;
+        *got = len;
+        return hipSuccess;
+      }
+      munmap(q, len);
+    }
+  }
   *got = bytes;
   return hipHostMalloc(p, bytes, hipHostMallocDefault);
 }
+
+namespace {
+void pinned_release(void* p, size_t bytes) {
+  bool reg = false;
+  {
+    std::lock_guard<std::mutex> lk(reg_mu());
+    reg = registered().erase(p) != 0;
+  }
+  if (reg) {
+    (void)hipHostUnregister(p);
+    munmap(p, bytes);
+  } else {
+    (void)hipHostFree(p);
+  }
+}
+}  // namespace
 
 void pinned_free(void* p, size_t bytes) {
   if (!p) return;
   // every copy into a batch buffer is waited for by its owner (fetch_span,
   // the batch prefetch): no device-wide wait here
   if (bytes >= kMinCached && pinned_cache().put(p, bytes, 0, kPinnedCap)) return;
-  (void)hipHostFree(p);
+  pinned_release(p, bytes);
 }
 
 size_t release_cached() {
@@ -126,7 +198,7 @@ size_t release_cached() {
     (void)hipFree(b.second.first);
   }
   if (cur >= 0) (void)hipSetDevice(cur);
-  for (auto& b : h) (void)hipHostFree(b.second.first);
+  for (auto& b : h) pinned_release(b.second.first, b.first);
   return n;
 }
 

@@ -16,15 +16,16 @@ data.tofile(path)
 del data
 ALL = (1 << 64) - 1
 try:
-    for batch in (1 << 16, 1 << 18, 1 << 20):
+    for window, batch in ((0, 1 << 16), (0, 1 << 18), (0, 1 << 20), (64 << 20, 1 << 20), (128 << 20, 1 << 20),
+                          (512 << 20, 1 << 20), (0, 1 << 20)):
         t0 = time.perf_counter()
-        with hbam.BamFile(path=path) as f:
+        with hbam.BamFile(path=path, window_bytes=window) as f:
             first = f.header()["first_record_voff"]
             t1 = time.perf_counter()
             r = f.scan_batches(first, ALL, batch)
             t2 = time.perf_counter()
             u = f.file_stats()[1]
-        print(f"batch {batch}: open+header {t1 - t0:.3f}s scan {t2 - t1:.3f}s total {u / (t2 - t0) / 1e9:.1f} GB/s "
+        print(f"window {window >> 20} MiB batch {batch}: open+header {t1 - t0:.3f}s scan {t2 - t1:.3f}s total {u / (t2 - t0) / 1e9:.1f} GB/s "
               f"({r[1]} batches)", flush=True)
     for rep in range(2):
         t0 = time.perf_counter()

@@ -201,26 +201,37 @@ def _block_end(s, pos):
     raise AssertionError(pos)
 
 
-def test_reader_position_follows_htsjdk_read_ahead():
+@pytest.mark.parametrize("window", [0, 1 << 16])
+def test_reader_position_follows_htsjdk_read_ahead(window):
     """getProgress's in.position(): the end of the block holding the last byte
     of the record after the current one (BAMFileIndexIterator reads one
-    ahead), or of the current one at the end of the split."""
+    ahead), or of the current one at the end of the split -- also when that
+    next record lies in the next window (64 KiB windows: batches end at
+    window ends)."""
     data, _ = synth.make_bam(4000, block_payload=16384)
     s = orc.Stream(data)
     rc, want = s.decode_all()
     ends = [int(want["offset"][i]) + 36 + int(want["rest_len"][i]) - 1 for i in range(len(want["key"]))]
     vo = want["voff"]
     vs, ve = int(vo[100]), int(vo[3000])
-    with hbam.BamFile(data) as f:
-        done = 0
+    with hbam.BamFile(data, window_bytes=window) as f:
+        done, batches = 0, 0
         for batch in f.iter_batches(vs, ve, 500):
             n = len(batch["key"])
-            for i in range(0, n, 37):
+            for i in list(range(0, n, 37)) + [n - 1]:
                 k = 100 + done + i
                 ahead = k + 1 if k + 1 < 3000 else k
                 assert f.reader_position(i) == _block_end(s, ends[ahead]), (done, i)
             done += n
+            batches += 1
         assert done == 2900
+        if window:
+            assert batches > 2900 // 500 + 1  # window ends cut batches short
+        # a call of another kind moves the cursor: no position until the next batch
+        f.file_stats()
+        with pytest.raises(hbam.HbamError) as e:
+            f.reader_position(0)
+        assert e.value.code == hbam.E_STATE
 
 
 @pytest.mark.parametrize("g", [1, 2, 10, 4096])
