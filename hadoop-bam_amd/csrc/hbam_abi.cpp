@@ -374,6 +374,7 @@ int hbam_reader_position(hbam_ctx* ctx, uint64_t i, uint64_t* pos) {
     ctx->err = "hbam_reader_position needs the last call on the ctx to be hbam_decode_span";
     return HBAM_E_STATE;
   }
+  if (i == UINT64_MAX) return ctx->cursor.initial_position(pos, &ctx->err);  // before record 0 is handed out
   if (i >= ctx->batch.n) {
     ctx->err = "record index outside the last batch";
     return HBAM_E_ARG;

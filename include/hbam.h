@@ -137,7 +137,9 @@ int hbam_prefetch(hbam_ctx *ctx, uint64_t lo, uint64_t hi);
 int hbam_decode_span(hbam_ctx *ctx, uint64_t vstart, uint64_t vend, uint64_t max_records, hbam_batch *out);
 /* BAMRecordReader.getProgress's in.position() (BAMRecordReader.java:209-219):
  * the compressed stream position after nextKeyValue returned record i of the
- * last batch (htsjdk's iterator has read one record ahead). */
+ * last batch (htsjdk's iterator has read one record ahead).  i == UINT64_MAX:
+ * the position once the iterator exists and before record 0 of the batch is
+ * handed out (the iterator has read record 0 only). */
 int hbam_reader_position(hbam_ctx *ctx, uint64_t i, uint64_t *pos);
 
 /* SplittingBAMIndexer.index(in, out, inputSize, granularity)

@@ -331,6 +331,8 @@ JNIEXPORT jbyteArray FN(bgzfCompress)(JNIEnv *env, jclass c, jint device, jobjec
 
 JNIEXPORT jlong FN(getKey)(JNIEnv *env, jclass c, jint ref, jint start) { return (jlong)hbam_get_key(ref, start); }
 
+JNIEXPORT jlong FN(getKey0)(JNIEnv *env, jclass c, jint ref, jint start0) { return (jlong)hbam_get_key0(ref, start0); }
+
 JNIEXPORT jlong FN(murmurhash3)(JNIEnv *env, jclass c, jbyteArray key, jint seed) {
   const jsize n = (*env)->GetArrayLength(env, key);
   jbyte *k = (*env)->GetByteArrayElements(env, key, NULL);

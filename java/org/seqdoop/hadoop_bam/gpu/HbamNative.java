@@ -8,6 +8,8 @@
 //
 //   BAMRecordReader.initialize / nextKeyValue / getProgress
 //       (BAMRecordReader.java:123-184, 223-232, 209-219)  -> open, decodeSpan, readerPosition
+//       (the delegating classes: ../GpuBAMRecordReader.java, ../GpuBAMInputFormat.java,
+//        ../GpuSplittingBAMIndexer.java)
 //   SplittingBAMIndexer.index (SplittingBAMIndexer.java:248-290) -> splittingIndex
 //   SplittingBAMIndexer.processAlignment + finish (:186-202, 240-243)
 //       (write time, BAMRecordWriter.java:131-149)       -> splittingIndexForRecords
@@ -81,7 +83,10 @@ public final class HbamNative {
   public static native ByteBuffer[] decodeSpan(long ctx, long vStart, long vEnd, long maxRecords, long[] cursor)
       throws IOException;
 
-  /** hbam_reader_position: BAMRecordReader.getProgress's in.position() after record i of the last batch. */
+  /**
+   * hbam_reader_position: BAMRecordReader.getProgress's in.position() after
+   * record i of the last batch; i = -1: before record 0 is handed out.
+   */
   public static native long readerPosition(long ctx, long i) throws IOException;
 
   /** hbam_build_splitting_index: the .splitting-bai bytes (SplittingBAMIndexer.index). */
@@ -128,6 +133,9 @@ public final class HbamNative {
 
   /** hbam_get_key: BAMRecordReader.getKey(int, int) (BAMRecordReader.java:114-116). */
   public static native long getKey(int refIdx, int alignmentStart);
+
+  /** hbam_get_key0: BAMRecordReader.getKey0(int, int) (BAMRecordReader.java:119-121). */
+  public static native long getKey0(int refIdx, int alignmentStart0);
 
   /** hbam_murmurhash3: util/MurmurHash3.murmurhash3(byte[], int). */
   public static native long murmurhash3(byte[] key, int seed);

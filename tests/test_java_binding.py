@@ -1,0 +1,87 @@
+"""CPU: the committed Java drop-in sources agree with the C ABI they bind.
+
+No JDK exists in this image, so the Java classes and the JNI glue are checked
+textually: every native method of HbamNative has its JNI function, every
+hbam_* call of the glue is declared in include/hbam.h, and every HbamNative
+method the delegating classes (GpuBAMRecordReader, GpuBAMInputFormat,
+GpuSplittingBAMIndexer) call exists with that arity."""
+import os
+import re
+
+import hbam
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+JAVA = os.path.join(ROOT, "java", "org", "seqdoop", "hadoop_bam")
+JNI = os.path.join(ROOT, "java", "jni", "hbam_jni.c")
+
+
+def _strip_comments(s):
+    s = re.sub(r"/\*.*?\*/", "", s, flags=re.S)
+    return re.sub(r"//[^\n]*", "", s)
+
+
+def _natives():
+    src = _strip_comments(open(os.path.join(JAVA, "gpu", "HbamNative.java")).read())
+    out = {}
+    for m in re.finditer(r"public static native [\w\[\]]+ (\w+)\(([^)]*)\)", src):
+        args = [a for a in m.group(2).split(",") if a.strip()]
+        out[m.group(1)] = len(args)
+    return out
+
+
+def test_every_native_method_has_its_jni_function():
+    natives = _natives()
+    assert {"open", "decodeSpan", "readerPosition", "splittingIndex", "splittingIndexForRecords", "getSplits",
+            "getKey", "getKey0", "murmurhash3"} <= set(natives)
+    jni = _strip_comments(open(JNI).read())
+    fns = {}
+    for m in re.finditer(r"JNIEXPORT [\w\s\*]+ FN\((\w+)\)\(([^)]*)\)", jni):
+        fns[m.group(1)] = len(m.group(2).split(",")) - 2  # minus JNIEnv*, jclass
+    assert set(natives) == set(fns), (set(natives) ^ set(fns))
+    for name, n in natives.items():
+        assert fns[name] == n, (name, n, fns[name])
+
+
+def test_jni_calls_only_declared_entry_points():
+    declared = set(hbam.exported_symbols_from_header())
+    jni = _strip_comments(open(JNI).read())
+    called = set(re.findall(r"\b(hbam_\w+)\s*\(", jni))
+    assert called and called <= declared, called - declared
+
+
+def test_delegating_classes_call_existing_natives():
+    natives = _natives()
+    seen = set()
+    for cls in ("GpuBAMRecordReader.java", "GpuBAMInputFormat.java", "GpuSplittingBAMIndexer.java"):
+        src = _strip_comments(open(os.path.join(JAVA, cls)).read())
+        assert "package org.seqdoop.hadoop_bam;" in src
+        for m in re.finditer(r"HbamNative\.(\w+)\(", src):
+            name = m.group(1)
+            assert name in natives, (cls, name)
+            # arity: count top-level commas of the call's argument list
+            i, depth, args, cur = m.end(), 1, 0, ""
+            while depth:
+                ch = src[i]
+                depth += ch in "(["
+                depth -= ch in ")]"
+                if depth == 1 and ch == ",":
+                    args += 1
+                cur += ch
+                i += 1
+            nargs = 0 if not cur[:-1].strip() else args + 1
+            assert nargs == natives[name], (cls, name, nargs, natives[name])
+            seen.add(name)
+    # the reader path, the indexer and the planner all go through the boundary
+    assert {"open", "close", "decodeSpan", "readerPosition", "getSplits", "splittingIndex",
+            "splittingIndexForRecords"} <= seen
+
+
+def test_reader_mirrors_the_reference_reader_surface():
+    src = _strip_comments(open(os.path.join(JAVA, "GpuBAMRecordReader.java")).read())
+    assert "extends RecordReader<LongWritable, SAMRecordWritable>" in src
+    for meth in ("public void initialize(InputSplit", "public boolean nextKeyValue()", "public float getProgress()",
+                 "public LongWritable getCurrentKey()", "public SAMRecordWritable getCurrentValue()",
+                 "public void close()"):
+        assert meth in src, meth
+    # the record is built with the codec's argument order (LazyBAMRecordFactory.java:37-50)
+    assert "factory.createBAMRecord(" in src
