@@ -171,7 +171,7 @@ int BamFile::prefetch(uint64_t lo, uint64_t hi) {
   // on the device, which the kernels' aligned loads assume
   uint8_t* at;
   if (hipSetDevice(pipe_->device()) != hipSuccess || src_.dev.reserve(hi - lo + 16 + hbam::kFilePad) != hipSuccess ||
-      hipMemcpy(at = src_.dev.p + (lo & 15), src_.host + lo, hi - lo, hipMemcpyHostToDevice) != hipSuccess ||
+      pipe_->copy_from_host(at = src_.dev.p + (lo & 15), src_.host + lo, hi - lo) != kOk ||
       hipMemset(at + (hi - lo), 0, hbam::kFilePad) != hipSuccess) {
     err_ = "prefetch: HIP copy failed";
     return kErrDevice;
@@ -766,7 +766,8 @@ int LinearBAMIndex::read(const uint8_t* d, uint64_t len, std::string* err) {
 // starts in gets a guessed start (BAMSplitGuesser, on the GPU) that also
 // ends the split before it.  Where the Java code would throw a
 // NullPointerException (no contig with linear entries, a guessed first
-// split) this returns kErrIO.
+// split) this returns kErrState (unchecked in Java: getSplits does not catch
+// it); a guesser I/O error is the IOException getSplits catches (:249-253).
 int BAMInputFormat::addBAISplits(BamFile& f, const std::vector<FileSplit>& splits, const LinearBAMIndex& idx,
                                  std::vector<FileVirtualSplit>* out) {
   const int32_t dict = f.n_ref();
@@ -777,8 +778,8 @@ int BAMInputFormat::addBAISplits(BamFile& f, const std::vector<FileSplit>& split
   const std::vector<uint64_t>* linIdx = nullptr;
   size_t ctgBins = 0;
   auto npe = [&](const char* what) {
-    f.error() = std::string("BAI split calculator: ") + what;
-    return kErrIO;
+    f.error() = std::string("NullPointerException in the BAI split calculator: ") + what;
+    return kErrState;
   };
   do {  // :353-357 the first contig with linear entries
     ++ctgIdx;
@@ -878,11 +879,13 @@ int BAMInputFormat::getSplits(BamFile& f, const std::vector<FileSplit>& splits, 
   if (bai) {
     LinearBAMIndex idx;
     std::string err;
-    if (idx.read(bai, bai_len, &err) != kOk) {  // htsjdk's parse error is not an IOException: it propagates
+    if (idx.read(bai, bai_len, &err) != kOk) {  // htsjdk's parse error is unchecked (SAMException): it propagates
       f.error() = err;
-      return kErrIO;
+      return kErrFormat;
     }
-    return addBAISplits(f, splits, idx, out);
+    const int rc = addBAISplits(f, splits, idx, out);
+    if (rc != kErrIO) return rc;
+    out->clear();  // addBAISplits' IOException: probabilistic splits (:249-253)
   }
   return addProbabilisticSplits(f, splits, out);
 }

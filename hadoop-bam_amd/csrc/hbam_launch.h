@@ -33,6 +33,7 @@ struct ChainArgs {
   uint32_t* wcnt;       // records listed per block
   uint16_t* list;       // kListCap u16 offsets (from ustart) per block
   uint32_t* counters;   // [0] hard link violations, [1] blocks to re-walk, [2] list overflow
+  uint8_t* has_long;    // check stage: the block has records left to k_rec_check_long; [nb]: any block
 };
 constexpr uint32_t kListCap = 2048;              // >= 65536 / 36 + 2: every reader-mode record start
 constexpr uint64_t kForceEmpty = ~0ull - 1;      // force[]: the block holds no record start
@@ -46,7 +47,8 @@ enum ChainStage : int {
   kStageLinkCheck = 6,   // max-scan link check with re-walk requests
   kStageRewalk = 7,      // re-walk the requested blocks (entries validated)
   kStageRewalkAll = 8,   // re-walk every block off the serial link's entry[]
-  kStageCheck = 9,       // per-record check of the lists -> cnt / err / need
+  kStageCheck = 9,       // per-record check of the lists -> cnt / err / need (has_long[nb]: long cigars left)
+  kStageCheckLong = 10,  // the long-cigar records kStageCheck left, a wave each
 };
 
 // candidates in [lo, hi); file + buf_base is the (aligned) device buffer start
@@ -105,6 +107,8 @@ hipError_t launch_next_pos(const uint8_t* u, const uint64_t* rec_pos, uint64_t n
 // (ColLayout with rec_pos; positions rebased by base, dst_pos[n] = nbytes)
 hipError_t launch_export_records(const Columns& src, const uint64_t* src_pos, const Columns& dst, uint64_t* dst_pos,
                                  uint64_t n, uint64_t base, uint64_t nbytes, hipStream_t s);
+// n bytes device -> page-locked host by a kernel (no copy engine)
+hipError_t launch_readback(void* dst, const void* src, uint64_t n, hipStream_t s);
 // out[0] ^= xor of keys (if keys), out[1] += sum of voffs, out[2..3] += the
 // order-sensitive key / voff digests (see k_digest)
 hipError_t launch_digest(const int64_t* keys, const uint64_t* voffs, uint64_t n, uint64_t* out, hipStream_t s);

@@ -40,7 +40,7 @@ Pipeline::Pipeline(int device) : device_(device) {
   streams_.n = 4;
   own(own_file_, own_spare_, stage_, dblocks_, ref_len_, du_, tokens_[0], tokens_[1], hout_, tables_[0], tables_[1],
       tinfo_[0], tinfo_[1], g_, x_, x2_, entry_, base_arr_, summary_, dead_, cand_, sorted_, isz_, ust_, cnt_, flags_,
-      errv_, need_, rec_pos_, rec_voff_, rcand_, force_, wcnt_, counters_, list_, scan_tmp_, cols_, long_rec_,
+      errv_, need_, rec_pos_, rec_voff_, rcand_, force_, wcnt_, counters_, list_, hlong_, scan_tmp_, cols_, long_rec_,
       long_n_, wbuf_, woffs_, wbad_, scalars_);
   for (auto& e : ev_) (void)hipEventCreate(&e);
   for (auto& e : sync_ev_) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -54,6 +54,7 @@ Pipeline::~Pipeline() {
   // this pipeline's own streams only: other contexts on the GPU run on
   (void)streams_.sync();
   streams_.n = 0;  // drained: the member buffers release without waiting (the streams go below)
+  if (rb_buf_) pinned_free(rb_buf_, rb_cap_);
   for (auto& e : ev_) (void)hipEventDestroy(e);
   for (auto& e : sync_ev_) (void)hipEventDestroy(e);
   for (auto& e : tab_ev_) (void)hipEventDestroy(e);
@@ -100,20 +101,18 @@ int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof
     const uint64_t a = std::max(base + keep, stage_lo_), b = std::min(base + len, stage_hi_);
     if (stage_hi_ > stage_lo_ && a < b) {
       if (int rc = stage_wait()) return rc;
-      if (a > base + keep)
-        HIPCHK(hipMemcpyAsync(dfile_ + keep, data + keep, a - base - keep, hipMemcpyHostToDevice, stream_));
+      if (a > base + keep) HIPCHK(feed_load_.copy(dfile_ + keep, data + keep, a - base - keep, stream_));
       HIPCHK(hipMemcpyAsync(dfile_ + (a - base), stage_.p + (a - stage_lo_), b - a, hipMemcpyDeviceToDevice, stream_));
-      if (base + len > b)
-        HIPCHK(hipMemcpyAsync(dfile_ + (b - base), data + (b - base), base + len - b, hipMemcpyHostToDevice, stream_));
+      if (base + len > b) HIPCHK(feed_load_.copy(dfile_ + (b - base), data + (b - base), base + len - b, stream_));
       host = len - keep - (b - a);
     } else {
-      HIPCHK(hipMemcpyAsync(dfile_ + keep, data + keep, len - keep, hipMemcpyHostToDevice, stream_));
+      HIPCHK(feed_load_.copy(dfile_ + keep, data + keep, len - keep, stream_));
       host = len - keep;
     }
   }
   if (host_bytes) *host_bytes = host;
   HIPCHK(hipMemsetAsync(dfile_ + len, 0, kFilePad, stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(rb_sync(stream_));
   flen_ = len;
   base_ = base;
   at_eof_ = at_eof;
@@ -121,6 +120,52 @@ int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof
   hblocks_.clear();
   inflated_.clear();
   total_u_ = 0;
+  return kOk;
+}
+
+hipError_t Pipeline::rb(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  // a few bytes (counters, flags, one position) take the copy directly: a
+  // small D2H does not wait behind other streams' copies, and a kernel launch
+  // per value costs more; bigger reads (the block table) go through k_readback
+  if (bytes <= 64) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s);
+  hipError_t e;
+  if (rb_stream_ && rb_stream_ != s && (e = rb_sync(rb_stream_)) != hipSuccess) return e;
+  size_t off = (rb_used_ + 15) & ~size_t(15);
+  if (off + bytes > rb_cap_) {
+    if (!rb_items_.empty() && (e = rb_sync(s)) != hipSuccess) return e;  // the old buffer drains first
+    if (rb_buf_) pinned_free(rb_buf_, rb_cap_);
+    rb_buf_ = nullptr;
+    rb_cap_ = 0;
+    void* q = nullptr;
+    size_t got = 0;
+    if ((e = pinned_alloc(&q, std::max<size_t>(bytes + 4096, 1 << 20), &got)) != hipSuccess) return e;
+    rb_buf_ = static_cast<uint8_t*>(q);
+    rb_cap_ = got;
+    off = 0;
+  }
+  if ((e = launch_readback(rb_buf_ + off, src, bytes, s)) != hipSuccess) return e;
+  rb_items_.push_back(RbItem{dst, off, bytes});
+  rb_used_ = off + bytes;
+  rb_stream_ = s;
+  return hipSuccess;
+}
+
+hipError_t Pipeline::rb_sync(hipStream_t s) {
+  hipError_t e = hipStreamSynchronize(s);
+  if (e == hipSuccess && rb_stream_ && rb_stream_ != s) e = hipStreamSynchronize(rb_stream_);
+  if (e != hipSuccess) return e;
+  for (const RbItem& it : rb_items_) memcpy(it.dst, rb_buf_ + it.off, it.bytes);
+  rb_items_.clear();
+  rb_used_ = 0;
+  rb_stream_ = nullptr;
+  return hipSuccess;
+}
+
+int Pipeline::copy_from_host(uint8_t* dst, const uint8_t* src, uint64_t len) {
+  HIPCHK(hipSetDevice(device_));
+  HIPCHK(feed_load_.copy(dst, src, len, stream_));
+  HIPCHK(rb_sync(stream_));
   return kOk;
 }
 
@@ -148,7 +193,7 @@ int Pipeline::stage(const uint8_t* host, uint64_t lo, uint64_t hi) {
   hipStream_t cs = stream_copy_;
   stage_thr_ = std::thread([this, dst, host, lo, hi, dev, cs]() {
     hipError_t e = hipSetDevice(dev);
-    if (e == hipSuccess) e = hipMemcpyAsync(dst, host + lo, hi - lo, hipMemcpyHostToDevice, cs);
+    if (e == hipSuccess) e = feed_stage_.copy(dst, host + lo, hi - lo, cs);
     if (e == hipSuccess) e = hipStreamSynchronize(cs);
     stage_err_ = e;
   });
@@ -214,7 +259,7 @@ int Pipeline::set_ref_lengths(const std::vector<int32_t>& lens) {
   HIPCHK(ref_len_.reserve(lens.size() + 1));
   if (!lens.empty())
     HIPCHK(hipMemcpyAsync(ref_len_.p, lens.data(), lens.size() * 4, hipMemcpyHostToDevice, stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(rb_sync(stream_));
   n_ref_len_ = (uint32_t)lens.size();
   return kOk;
 }
@@ -236,8 +281,8 @@ int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_sta
   // flags_[0] = candidate count, [1] = chain break, [2] = first big ISIZE, [3] = cut tail
   HIPCHK(launch_bgzf_scan(fbase, base_, lo, hi, cand_.p, cap, flags_.p, s));
   uint32_t count = 0;
-  HIPCHK(hipMemcpyAsync(&count, flags_.p, 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(rb(&count, flags_.p, 4, s));
+  HIPCHK(rb_sync(s));
   bool serial = count > cap || (count == 0 && len > 0);
   if (free_start && count == 0) return kOk;  // no header in the window: no blocks
   uint32_t n = serial ? 0 : count;
@@ -251,16 +296,16 @@ int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_sta
     HIPCHK(sort_u64(scan_tmp_.p, &tmp_bytes, cand_.p, sorted_.p, n, s));
     if (free_start) {
       starts.resize(std::min<uint32_t>(n, kMaxFreeStarts));
-      HIPCHK(hipMemcpyAsync(starts.data(), sorted_.p, starts.size() * 8, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(rb(starts.data(), sorted_.p, starts.size() * 8, s));
+      HIPCHK(rb_sync(s));
       lo = starts[0];
     }
     HIPCHK(launch_bgzf_verify(fbase, lo, hi, sorted_.p, n, dblocks_.p + nprev, flags_.p + 1, partial ? 1u : 0u, s));
     uint32_t fl[3];
     uint64_t last = 0;
-    HIPCHK(hipMemcpyAsync(fl, flags_.p + 1, 12, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(&last, sorted_.p + n - 1, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(rb(fl, flags_.p + 1, 12, s));
+    HIPCHK(rb(&last, sorted_.p + n - 1, 8, s));
+    HIPCHK(rb_sync(s));
     if (fl[0]) serial = true;
     else if (fl[1] != 0xffffffffu) return fail(kErrFormat, "BGZF block with ISIZE > 65536 (unsupported on device)");
     else if (fl[2]) {  // the last candidate's block is cut by hi: next range
@@ -276,8 +321,8 @@ int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_sta
     for (size_t j = 0; j < starts.size() && !found; ++j) {
       HIPCHK(hipMemsetAsync(flags_.p, 0, 16, s));
       HIPCHK(launch_bgzf_walk(fbase, starts[j], hi, dblocks_.p + nprev, walk_cap, flags_.p, partial ? 1u : 0u, s));
-      HIPCHK(hipMemcpyAsync(out, flags_.p, 16, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(rb(out, flags_.p, 16, s));
+      HIPCHK(rb_sync(s));
       n = out[0];
       const uint64_t at = (uint64_t)out[2] | ((uint64_t)out[3] << 32);
       if (out[1] != kOk) {
@@ -302,9 +347,8 @@ int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_sta
   HIPCHK(launch_block_ustart(dblocks_.p + nprev, n, isz_.p, ust_.p, scan_tmp_.p, &sb, ubase, s));
   hblocks_.resize(nprev + n);
   if (n)
-    HIPCHK(hipMemcpyAsync(hblocks_.data() + nprev, dblocks_.p + nprev, n * sizeof(BlockInfo), hipMemcpyDeviceToHost,
-                          s));
-  HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(rb(hblocks_.data() + nprev, dblocks_.p + nprev, n * sizeof(BlockInfo), s));
+  HIPCHK(rb_sync(s));
   *nnew = n;
   return kOk;
 }
@@ -324,7 +368,7 @@ int Pipeline::finish_blocks() {
   if (!dead.empty())
     HIPCHK(hipMemcpyAsync(dead_.p, dead.data(), dead.size() * 8, hipMemcpyHostToDevice, stream_));
   ndead_ = (uint32_t)dead.size();
-  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(rb_sync(stream_));
   return kOk;
 }
 
@@ -419,11 +463,12 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
   uint32_t first = none;
   HIPCHK(hipMemcpyAsync(flags_.p + 3, &none, 4, hipMemcpyHostToDevice, stream_));
   HIPCHK(launch_first_error_hout(hout_.p, 0, nb, flags_.p + 3, stream_));
-  HIPCHK(hipMemcpyAsync(&first, flags_.p + 3, 4, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(rb(&first, flags_.p + 3, 4, stream_));
+  HIPCHK(rb_sync(stream_));
   if (first != none) {
     HuffOut ho;
-    HIPCHK(hipMemcpy(&ho, hout_.p + first, sizeof ho, hipMemcpyDeviceToHost));
+    HIPCHK(rb(&ho, hout_.p + first, sizeof ho, stream_));
+    HIPCHK(rb_sync(stream_));
     std::fill(inflated_.begin(), inflated_.end(), 0);
     const char* what = ho.status == kErrFormat ? "Did not inflate expected amount" : "invalid DEFLATE data";
     return fail(ho.status, std::string(what) + " in BGZF block at offset " + std::to_string(hblocks_[first].coff));
@@ -559,9 +604,9 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
   HIPCHK(hipMemcpyAsync(flags_.p + 3, &none, 4, hipMemcpyHostToDevice, stream_));
   HIPCHK(launch_first_error_hout(hout_.p, b0, b1 - b0, flags_.p + 3, stream_));
   uint32_t first = none;
-  HIPCHK(hipMemcpyAsync(&first, flags_.p + 3, 4, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(rb(&first, flags_.p + 3, 4, stream_));
   if (timing) HIPCHK(hipEventRecord(ev_[3], stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(rb_sync(stream_));
   if (timing) {
     (void)hipEventElapsedTime(&times.inflate, ev_[2], ev_[3]);
     times.tables = tab_ms;
@@ -570,7 +615,8 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
   }
   if (first != none) {
     HuffOut ho;
-    HIPCHK(hipMemcpy(&ho, hout_.p + b0 + first, sizeof ho, hipMemcpyDeviceToHost));
+    HIPCHK(rb(&ho, hout_.p + b0 + first, sizeof ho, stream_));
+    HIPCHK(rb_sync(stream_));
     for (uint32_t k = b0; k < b1; ++k) inflated_[k] = 0;
     const BlockInfo& bad = hblocks_[b0 + first];
     const char* what = ho.status == kErrFormat ? "Did not inflate expected amount" : "invalid DEFLATE data";
@@ -640,8 +686,8 @@ int Pipeline::read_stream(uint64_t pos, uint64_t len, std::vector<uint8_t>* out)
   int rc = inflate(b0, b1);
   if (rc != kOk) return rc;
   out->resize(len);
-  HIPCHK(hipMemcpyAsync(out->data(), du_.p + pos, len, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(rb(out->data(), du_.p + pos, len, stream_));
+  HIPCHK(rb_sync(stream_));
   return kOk;
 }
 
@@ -704,6 +750,7 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
     HIPCHK(force_.reserve(nb));
     HIPCHK(wcnt_.reserve(nb));
     HIPCHK(list_.reserve((uint64_t)nb * kListCap));
+    HIPCHK(hlong_.reserve(nb + 1));
     HIPCHK(base_arr_.reserve(nb + 1));
     HIPCHK(counters_.reserve(4));
     size_t lsb = 0;
@@ -721,6 +768,7 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
     a.force = force_.p;
     a.wcnt = wcnt_.p;
     a.list = list_.p;
+    a.has_long = hlong_.p;
     a.counters = counters_.p;
     a.base = base_arr_.p;
     a.scan_tmp = scan_tmp_.p;
@@ -734,8 +782,8 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
       HIPCHK(hipMemsetAsync(counters_.p, 0, 8, stream_));
       HIPCHK(launch_chain(a, mode, kStageLinkCheck, stream_));
       uint32_t ctr[2] = {0, 0};
-      HIPCHK(hipMemcpyAsync(ctr, counters_.p, 8, hipMemcpyDeviceToHost, stream_));
-      HIPCHK(hipStreamSynchronize(stream_));
+      HIPCHK(rb(ctr, counters_.p, 8, stream_));
+      HIPCHK(rb_sync(stream_));
       if (ctr[0]) { serial = true; break; }
       if (ctr[1] == 0) break;
       if (fix == kMaxLinkFix) { serial = true; break; }
@@ -748,22 +796,26 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
       ++link_fallbacks_;
       HIPCHK(launch_chain(a, mode, kStageSerialLink, stream_));
       HIPCHK(launch_chain(a, mode, kStageRewalkAll, stream_));
-      HIPCHK(hipMemcpyAsync(sm, summary_.p, 16, hipMemcpyDeviceToHost, stream_));
+      HIPCHK(rb(sm, summary_.p, 16, stream_));
     } else {  // final chain position = max of every walk exit; no stop
       uint64_t t[2] = {0, 0};
-      HIPCHK(hipMemcpyAsync(&t[0], base_arr_.p + nb - 1, 8, hipMemcpyDeviceToHost, stream_));
-      HIPCHK(hipMemcpyAsync(&t[1], x2_.p + nb - 1, 8, hipMemcpyDeviceToHost, stream_));
-      HIPCHK(hipStreamSynchronize(stream_));
+      HIPCHK(rb(&t[0], base_arr_.p + nb - 1, 8, stream_));
+      HIPCHK(rb(&t[1], x2_.p + nb - 1, 8, stream_));
+      HIPCHK(rb_sync(stream_));
       sm[0] = nb == 1 ? t[1] : std::max(t[0], t[1]);
       sm[1] = 0;
     }
     uint32_t ovf = 0;
-    HIPCHK(hipMemcpyAsync(&ovf, counters_.p + 2, 4, hipMemcpyDeviceToHost, stream_));
-    HIPCHK(hipStreamSynchronize(stream_));
+    HIPCHK(rb(&ovf, counters_.p + 2, 4, stream_));
+    HIPCHK(rb_sync(stream_));
     lists = ovf == 0;
+    uint8_t long_left = 0;
+    HIPCHK(hipMemsetAsync(hlong_.p + nb, 0, 1, stream_));
     HIPCHK(launch_chain(a, mode, lists ? kStageCheck : kStageCount, stream_));  // count + validate
-    HIPCHK(hipMemcpyAsync(&need, need_.p, 8, hipMemcpyDeviceToHost, stream_));
-    HIPCHK(hipStreamSynchronize(stream_));
+    HIPCHK(rb(&need, need_.p, 8, stream_));
+    HIPCHK(rb(&long_left, hlong_.p + nb, 1, stream_));
+    HIPCHK(rb_sync(stream_));
+    if (long_left) HIPCHK(launch_chain(a, mode, kStageCheckLong, stream_));  // long cigars, a wave each
     const uint64_t final_pos = sm[0];
     const bool stopped = sm[1] != 0;
     if (need > a.e_inf && inf_end < nblk) {  // a record needs bytes beyond the inflated range
@@ -787,11 +839,12 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
   HIPCHK(hipMemcpyAsync(flags_.p + 3, &none, 4, hipMemcpyHostToDevice, stream_));
   HIPCHK(launch_first_error_i32(errv_.p, nb, flags_.p + 3, stream_));
   uint32_t first = none;
-  HIPCHK(hipMemcpyAsync(&first, flags_.p + 3, 4, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(rb(&first, flags_.p + 3, 4, stream_));
+  HIPCHK(rb_sync(stream_));
   if (first != none) {
     int32_t code = 0;
-    HIPCHK(hipMemcpy(&code, errv_.p + first, 4, hipMemcpyDeviceToHost));
+    HIPCHK(rb(&code, errv_.p + first, 4, stream_));
+    HIPCHK(rb_sync(stream_));
     HIPCHK(launch_truncate_counts(cnt_.p, nb, flags_.p + 3, stream_));
     out->status = code;
     const BlockInfo& b = hblocks_[k0 + first];
@@ -808,9 +861,9 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
   HIPCHK(scan_u32_to_u64(scan_tmp_.p, &tb, cnt_.p, base_arr_.p, nb, stream_));
   uint64_t last_base = 0;
   uint32_t last_cnt = 0;
-  HIPCHK(hipMemcpyAsync(&last_base, base_arr_.p + nb - 1, 8, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipMemcpyAsync(&last_cnt, cnt_.p + nb - 1, 4, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(rb(&last_base, base_arr_.p + nb - 1, 8, stream_));
+  HIPCHK(rb(&last_cnt, cnt_.p + nb - 1, 4, stream_));
+  HIPCHK(rb_sync(stream_));
   const uint64_t total = last_base + last_cnt;
   HIPCHK(rec_pos_.reserve(total + 1));
   HIPCHK(rec_voff_.reserve(total + 1));
@@ -839,9 +892,9 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
   // the next record's start: the chain successor of the last record
   HIPCHK(scalars_.reserve(8));
   HIPCHK(launch_next_pos(du_.p, rec_pos_.p, total, p0, mode, scalars_.p, stream_));
-  HIPCHK(hipMemcpyAsync(&out->next_pos, scalars_.p, 8, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(rb(&out->next_pos, scalars_.p, 8, stream_));
   if (timing) HIPCHK(hipEventRecord(ev_[2], stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(rb_sync(stream_));
   if (timing) {
     float all = 0, dcd = 0;
     (void)hipEventElapsedTime(&all, ev_[0], ev_[1]);
@@ -904,10 +957,10 @@ int Pipeline::encoded_bytes(const SpanDev& s, uint64_t* bytes) {
   if (!s.col.rest_off) return fail(kErrState, "span was not decoded in reader mode");
   uint64_t first = 0, last_off = 0;
   uint32_t last_len = 0;
-  HIPCHK(hipMemcpyAsync(&first, s.rec_pos, 8, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipMemcpyAsync(&last_off, s.col.rest_off + (s.n - 1), 8, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipMemcpyAsync(&last_len, s.col.rest_len + (s.n - 1), 4, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(rb(&first, s.rec_pos, 8, stream_));
+  HIPCHK(rb(&last_off, s.col.rest_off + (s.n - 1), 8, stream_));
+  HIPCHK(rb(&last_len, s.col.rest_len + (s.n - 1), 4, stream_));
+  HIPCHK(rb_sync(stream_));
   *bytes = last_off + last_len - first;
   return kOk;
 }
@@ -916,8 +969,8 @@ int Pipeline::encode_writables(const SpanDev& s, uint64_t bytes, uint8_t* dst) {
   if (s.n == 0) return kOk;
   if (!s.col.ref_id) return fail(kErrState, "span was not decoded in reader mode");
   uint64_t first = 0;
-  HIPCHK(hipMemcpyAsync(&first, s.rec_pos, 8, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(rb(&first, s.rec_pos, 8, stream_));
+  HIPCHK(rb_sync(stream_));
   const uint8_t* src = s.data ? s.data : du_.p;
   HIPCHK(launch_wr_encode(src, first, bytes, s.rec_pos, s.col.ref_id, s.col.bin, s.n, dst, stream_));
   return kOk;
@@ -941,8 +994,8 @@ int Pipeline::decode_writables(const uint8_t* buf, uint64_t len, const uint64_t*
   HIPCHK(launch_wr_decode(wbuf_.p, len, woffs_.p, n, c, rec_pos_.p, wbad_.p, stream_));
   HIPCHK(launch_long_hash(wbuf_.p, rec_pos_.p, c, stream_));
   unsigned long long bad = ~0ull;
-  HIPCHK(hipMemcpyAsync(&bad, wbad_.p, sizeof bad, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(rb(&bad, wbad_.p, sizeof bad, stream_));
+  HIPCHK(rb_sync(stream_));
   out->n = n;
   if (bad != ~0ull) {
     out->n = bad >> 8;
@@ -969,8 +1022,8 @@ int Pipeline::splitting_entries(const SpanDev& span, uint32_t g, uint64_t o0, st
   HIPCHK(ent.reserve(m));
   HIPCHK(launch_sbi_emit(span.rec_voff, span.n, g, o0, ent.p, stream_));
   out->resize(m);
-  HIPCHK(hipMemcpyAsync(out->data(), ent.p, m * 8, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(rb(out->data(), ent.p, m * 8, stream_));
+  HIPCHK(rb_sync(stream_));
   return kOk;
 }
 
@@ -980,8 +1033,8 @@ int Pipeline::span_digest(const SpanDev& span, uint64_t out[4]) {
   HIPCHK(scalars_.reserve(8));
   HIPCHK(hipMemsetAsync(scalars_.p + 2, 0, 32, stream_));
   HIPCHK(launch_digest(span.col.key, span.rec_voff, span.n, scalars_.p + 2, stream_));
-  HIPCHK(hipMemcpyAsync(out, scalars_.p + 2, 32, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(rb(out, scalars_.p + 2, 32, stream_));
+  HIPCHK(rb_sync(stream_));
   return kOk;
 }
 

@@ -11,6 +11,7 @@
 // back counters.  There is no CPU fallback: any HIP failure is an error
 // returned to the caller.
 #pragma once
+#include "hbam_feed.h"
 #include "hbam_mem.h"
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -117,6 +118,18 @@ class Pipeline {
   // buffers its callers hand it: BamFile's resident copy, ABI temporaries)
   const StreamSet& streams() const { return streams_; }
   const std::string& error() const { return err_; }
+
+  // Device -> host reads of the host logic: reads above 64 B are queued as
+  // k_readback launches on stream s into a page-locked buffer (shader
+  // engines: a pageable D2H of the block table waited ~13 ms behind a drop-in
+  // batch's D2H on another stream); smaller ones are plain async copies.  The
+  // bytes land in dst when rb_sync(s) returns; rb_sync(s) synchronizes s in
+  // any case.
+  hipError_t rb(void* dst, const void* src, size_t bytes, hipStream_t s);
+  hipError_t rb_sync(hipStream_t s);
+  // dst (device) <- host bytes src [len) through the copy threads and bounce
+  // buffers (HostFeed), synchronously on the pipeline's stream
+  int copy_from_host(uint8_t* dst, const uint8_t* src, uint64_t len);
 
   // Copy file bytes [base, base + len) into the window buffer.  at_eof: the
   // range ends at the end of the file (else the window is open).
@@ -245,6 +258,7 @@ class Pipeline {
   DevBuf<uint8_t> stage_;      // stage(): file bytes [stage_lo_, stage_hi_) in flight / landed
   uint64_t stage_lo_ = 0, stage_hi_ = 0;
   std::thread stage_thr_;      // issues the staged copy (pageable copies block their caller)
+  HostFeed feed_load_, feed_stage_;  // host -> HBM copies of load() and of the stage thread
   hipError_t stage_err_ = hipSuccess;
   int stage_wait();            // the staged copy done (its error, if any)
   uint64_t flen_ = 0, base_ = 0;
@@ -285,6 +299,7 @@ class Pipeline {
   DevBuf<uint64_t> rcand_, force_;  // chain v2
   DevBuf<uint32_t> wcnt_, counters_;
   DevBuf<uint16_t> list_;
+  DevBuf<uint8_t> hlong_;  // check stage: blocks with records for k_rec_check_long
   DevBuf<uint8_t> scan_tmp_;
   DevBuf<uint8_t> cols_;  // SoA backing store
   uint64_t cols_cap_ = 0;
@@ -297,6 +312,16 @@ class Pipeline {
 
   hipEvent_t ev_[8];
   std::vector<hipEvent_t> tev_;     // timing events of overlapped inflate chunks
+
+  // read-back queue (rb / rb_sync)
+  struct RbItem {
+    void* dst;
+    size_t off, bytes;
+  };
+  uint8_t* rb_buf_ = nullptr;
+  size_t rb_cap_ = 0, rb_used_ = 0;
+  hipStream_t rb_stream_ = nullptr;
+  std::vector<RbItem> rb_items_;
 };
 
 }  // namespace hbam

@@ -19,7 +19,10 @@
  * a decode copies into HBM just the window of compressed bytes it works on
  * (opts.window_bytes at a time, the next record's position carried from one
  * window to the next).  Device memory is bounded by the window, whatever the
- * file size.
+ * file size.  hbam_open maps the file read-only: the file must not be
+ * truncated or replaced while a ctx is open (a copy from a page past the new
+ * end raises SIGBUS in the process, where the reference's stream read would
+ * throw an IOException); HDFS block files and completed outputs never are.
  *
  * Threading: a ctx is single-threaded (RecordReader contract); the library is
  * re-entrant across ctxs.  Each ctx owns one HIP stream on its device.
@@ -179,7 +182,12 @@ int hbam_get_splits(hbam_ctx *ctx, const uint64_t *starts, const uint64_t *lengt
  * BAMInputFormat.java:241-257, 322-465): with no usable .splitting-bai, splits
  * come from the linear index of the file's .bai (bai bytes; NULL: no .bai ->
  * probabilistic splits), a split no linear entry starts in getting a guessed
- * start.  At most n splits. */
+ * start.  At most n splits.  Errors as the reference's: a guesser I/O error
+ * inside the BAI planner falls back to probabilistic splits (the IOException
+ * getSplits catches, :249-253); a malformed .bai -> HBAM_E_FORMAT (htsjdk's
+ * unchecked parse error); where addBAISplits dereferences null (no contig
+ * with a linear index, a guessed first split) -> HBAM_E_STATE (the JNI glue
+ * throws NullPointerException). */
 int hbam_get_splits_bai(hbam_ctx *ctx, const uint64_t *starts, const uint64_t *lengths, uint64_t n,
                         const uint8_t *sbi, uint64_t sbi_len, const uint8_t *bai, uint64_t bai_len,
                         uint64_t *vstarts, uint64_t *vends, uint64_t *nout);

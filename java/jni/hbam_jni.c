@@ -232,7 +232,10 @@ JNIEXPORT jlongArray FN(getSplits)(JNIEnv *env, jclass c, jlong h, jlongArray st
                                      (const uint8_t *)bb, (uint64_t)blen, vs, ve, &nout);
   if (ib) (*env)->ReleaseByteArrayElements(env, sbi, ib, JNI_ABORT);
   if (bb) (*env)->ReleaseByteArrayElements(env, bai, bb, JNI_ABORT);
-  if (rc != HBAM_OK) {
+  if (rc == HBAM_E_STATE) {  /* where BAMInputFormat.addBAISplits dereferences null */
+    jclass npe = (*env)->FindClass(env, "java/lang/NullPointerException");
+    if (npe) (*env)->ThrowNew(env, npe, hbam_last_error(CTX(h)));
+  } else if (rc != HBAM_OK) {
     throw_for(env, rc, hbam_last_error(CTX(h)));
   } else {
     uint64_t *pairs = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(2 * nout + 1));

@@ -94,6 +94,7 @@ static const int DELTAS[NDELTA] = {0, 16, 32, 48, 64, 96, 128, 192, 256};
 static uint64_t lanes = 0, mism[NDELTA], waves = 0, wmism[NDELTA], warm_syms[NDELTA], slice_syms = 0;
 static uint64_t blocks_seen = 0;
 
+static void sim_sync(uint64_t b0, uint64_t bend, const uint8_t* tb);
 static void sim_block(uint64_t b0, uint64_t bend) {
   // true boundaries
   uint64_t R = bend - b0;
@@ -143,8 +144,70 @@ static void sim_block(uint64_t b0, uint64_t bend) {
     waves++;
     for (int k = 0; k < NDELTA; ++k) wmism[k] += wm[k];
   }
+  sim_sync(b0, bend, tb);
   free(ft);
   free(tb);
+}
+
+
+#define NSET 4
+static const char* SETN[NSET] = {"4,8,16,32", "every 4 to 32", "every 4 to 64", "every boundary"};
+static double set_wave_cost[NSET], set_lane_cost[NSET], slice_cost_sum = 0;
+static uint64_t set_waves = 0, set_lanes = 0;
+static int in_set(int k, int sym) {  // sym = 1-based symbol count of the spec walk at a boundary
+  if (k == 0) return sym == 4 || sym == 8 || sym == 16 || sym == 32;
+  if (k == 1) return sym % 4 == 0 && sym <= 32;
+  if (k == 2) return sym % 4 == 0 && sym <= 64;
+  return 1;
+}
+static void sim_sync(uint64_t b0, uint64_t bend, const uint8_t* tb) {
+  uint64_t R = bend - b0, S = (R + 255) / 256;
+  static uint64_t bpos[4096];
+  static uint8_t bset[4096];
+  for (int w = 0; w < 4; ++w) {
+    double wmax[NSET] = {0};
+    for (int l = w * 64; l < w * 64 + 64; ++l) {
+      uint64_t a = b0 + l * S, stop = a + S;
+      if (a >= bend) continue;
+      if (stop > bend) stop = bend;
+      // spec walk from a to stop: boundary after each symbol
+      int ns = 0;
+      uint64_t q = a;
+      while (q < stop && ns < 4096) {
+        int eob, n = step(q, &eob);
+        if (!n || eob) break;
+        q += n;
+        bpos[ns++] = q;
+      }
+      // true start: first true boundary >= a
+      uint64_t t = a;
+      while (t < bend && !((tb[(t - b0) >> 3] >> ((t - b0) & 7)) & 1)) ++t;
+      // symbols of the true walk (slice) for the full-slice cost
+      int full = 0;
+      { uint64_t z = t; while (z < stop) { int eob, n = step(z, &eob); if (!n || eob) break; z += n; ++full; } }
+      slice_cost_sum += full;
+      for (int k = 0; k < NSET; ++k) {
+        // sync walk from t: count symbols until its position equals a checkpoint boundary of the spec walk
+        uint64_t z = t;
+        int c = 0, merged = 0;
+        int j = 0;
+        while (z < stop) {
+          while (j < ns && bpos[j] < z) ++j;
+          if (j < ns && bpos[j] == z && in_set(k, j + 1)) { merged = 1; break; }
+          int eob, n = step(z, &eob);
+          if (!n || eob) break;
+          z += n;
+          ++c;
+        }
+        (void)merged;
+        set_lane_cost[k] += c;
+        if (c > wmax[k]) wmax[k] = c;
+      }
+      ++set_lanes;
+    }
+    for (int k = 0; k < NSET; ++k) set_wave_cost[k] += wmax[k];
+    ++set_waves;
+  }
 }
 
 int main(int argc, char** argv) {
@@ -212,5 +275,10 @@ int main(int argc, char** argv) {
   for (int k = 0; k < NDELTA; ++k)
     printf("warm-up %3d bits: lane mismatch %.4f  waves with a mismatch %.4f  warm-up symbols/lane %.1f\n", DELTAS[k],
            (double)mism[k] / lanes, (double)wmism[k] / waves, (double)warm_syms[k] / lanes);
+  printf("true-walk symbols per slice %.1f\n", slice_cost_sum / set_lanes);
+  for (int k = 0; k < NSET; ++k)
+    printf("sync checkpoints %-16s mean lane walk %.1f symbols, mean wave max %.1f\n", SETN[k],
+           set_lane_cost[k] / set_lanes, set_wave_cost[k] / set_waves);
   return 0;
 }
+// (appended) -- see main2: sync-walk cost model with checkpoint sets

@@ -33,5 +33,6 @@ def test_bai_splits_match_oracle(placement, split_size):
 def test_bad_bai_is_an_error():
     data = spread_bam(2000, PLACEMENTS[0])
     with hbam.BamFile(data) as f:
-        with pytest.raises(hbam.HbamError):
+        with pytest.raises(hbam.HbamError) as e:
             f.get_splits([0, 100000], [100000, len(data) - 100000], bai=b"BAM\1junk")
+        assert e.value.code == hbam.E_FORMAT  # htsjdk's parse error is unchecked (not the IOException fallback)

@@ -314,3 +314,49 @@ def test_reopened_splits_reuse_cached_blocks(tmp_path):
     path, want, u = files[0]
     with hbam.BamFile(path=path) as f:
         assert_same_records(f.decode_all(), want, u)
+
+
+def _long_cigar_cases():
+    """(record, op index, new op, new len) on the 40-record long-read BAM:
+    each edit breaks (or keeps) one Cigar.isValid / alignment rule inside a
+    cigar of 150-750 operators -- the records k_rec_check validates with a
+    whole wave (record_invalid_wave)."""
+    return [
+        (1, 100, 1, 3), (1, 101, 1, 3),      # I next to I / an I inside a run
+        (2, 200, 2, 4), (2, 0, 2, 4),        # D in the middle, D first
+        (3, 57, 5, 10), (3, -1, 5, 10),      # H in the middle / last
+        (4, 1, 4, 7), (4, 120, 4, 7),        # S second / in the middle
+        (6, 30, 6, 2), (6, -1, 6, 2),        # P between real ops / last
+        (7, 300, 0, 0), (7, 64, 0, 0),       # zero-length M (chunk boundary)
+        (8, 63, 1, 2), (8, 127, 2, 2),       # I / D at chunk ends
+        (9, 200, 9, 5),                      # operator 9 (structural: LENIENT too)
+        (10, 10, 3, 200000000),              # N run off the reference end
+        (11, 250, 0, 151),                   # M length: cigar read length != l_seq
+        (13, 70, "X", 0), (14, 140, "=", 0),  # an M relabelled X / = (same length): still valid
+    ]
+
+
+@pytest.mark.parametrize("case", _long_cigar_cases(), ids=[str(i) for i in range(len(_long_cigar_cases()))])
+def test_long_cigar_validation_matches_oracle(case):
+    rec, k, op, ln = case
+    data, _ = synth.make_bam(40, mode="long")
+    s0 = orc.Stream(data, stringency=orc.SILENT)
+    rc, r = s0.decode_all()
+    ncig = int(r["n_cigar"][rec])
+    assert ncig > 64
+    lrn = int(r["l_read_name"][rec])
+    k = k % ncig
+    if isinstance(op, str):  # relabel the first M at or after k, keeping its length
+        u = s0.data
+        at = int(r["offset"][rec]) + 36 + lrn
+        while struct.unpack_from("<I", u, at + 4 * k)[0] & 15:
+            k += 1
+        ln = struct.unpack_from("<I", u, at + 4 * k)[0] >> 4
+        op = {"X": 8, "=": 7}[op]
+    bad = _patched(data, rec, 36 + lrn + 4 * k, "<I", (ln << 4) | op)
+    for stringency in (hbam.STRICT, hbam.LENIENT):
+        want_rc, want = orc.Stream(bad, stringency=stringency).decode_all()
+        with hbam.BamFile(bad, stringency=stringency) as f:
+            got = f.decode_all(raise_on_error=False)
+        assert got["status"] == want_rc, (case, stringency)
+        assert_same_records(got, want)
