@@ -41,6 +41,9 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "hadoop-bam_amd"))
+# 8 hardware queues per device for the context's streams (libhbam asks for it
+# when it loads first; at N > 1 torch initializes HIP before libhbam loads)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 METRIC = "uncompressed BAM decode GB/s + records/sec per GPU and 8-GPU node"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
@@ -142,6 +145,8 @@ def cpu_baseline(path, size, seconds):
     dt1 = time.perf_counter() - t
     model = cpu_model()
     out = {"value": round(full["u_bytes"] / dt_all / 1e9, 4), "unit": "GB/s", "cores": cores, "kind": "port",
+           "host_cores_total": os.cpu_count(), "cores_note": "cores = the threads used: every CPU the process may "
+           "use (affinity set capped by the cgroup quota); host_cores_total = the machine's logical CPUs",
            "records_per_s": round(full["records"] / dt_all, 1), "cpu_model": model,
            "sample": f"whole file ({full['u_bytes']} inflated bytes, {full['records']} records) through "
                      f"oracle/orc_scan.c (system zlib, htsjdk reader rules, STRICT) on {cores} threads "
@@ -695,6 +700,12 @@ def run_c2(D, args, steps, warmup, extras):
                         extra[name] = {"error": repr(e)}
                     log(f"[extra] {name} {time.time() - t:.1f}s")
                 out["extra"] = extra
+                d2d = (extra.get("write_path") or {}).get("d2d_copy_GBps_measured")
+                if d2d:  # the read path against the measured device-to-device copy rate
+                    rf = out["roofline"]
+                    rf["measured_d2d_GBps"] = d2d
+                    rf["frac_of_measured_d2d"] = round(rf["achieved"] / d2d, 5)
+                    rf["whole_pass"]["frac_of_measured_d2d"] = round(rf["whole_pass"]["achieved"] / d2d, 5)
         return out
     finally:
         D.barrier()

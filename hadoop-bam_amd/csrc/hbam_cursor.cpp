@@ -14,6 +14,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 
@@ -31,6 +34,20 @@ using hbam::kErrState;
 using hbam::kOk;
 
 namespace {
+// HBAM_CURSOR_TRACE: developer timing lines on stderr (ms since the last one)
+bool cursor_trace() {
+  static const bool t = getenv("HBAM_CURSOR_TRACE") != nullptr;
+  return t;
+}
+void ctrace(const char* what, uint64_t a = 0) {
+  if (!cursor_trace()) return;
+  static auto last = std::chrono::steady_clock::now();
+  const auto now = std::chrono::steady_clock::now();
+  fprintf(stderr, "[cursor] +%.3f ms %s %llu\n", std::chrono::duration<double, std::milli>(now - last).count(), what,
+          (unsigned long long)a);
+  last = now;
+}
+
 hbam::Columns offset_columns(const hbam::Columns& c, uint64_t k) {
   hbam::Columns o = c;
   o.ref_id += k;
@@ -69,9 +86,11 @@ SpanCursor::~SpanCursor() {
   (void)drain();
   (void)own_.sync();
   own_.n = 0;  // drained: the slot buffers release without waiting
+  slot_owner_.n = 0;
   for (auto& w : win_) {
     w.cols.release();
     w.bytes.release();
+    w.packed.release();
     if (w.ready) (void)hipEventDestroy(w.ready);
   }
   for (auto& s : slot_) {
@@ -106,7 +125,9 @@ int SpanCursor::ensure_streams(hbam::Pipeline& p, std::string* err) {
   own_.s[1] = d2h_;
   own_.s[2] = meta_;
   own_.n = 3;
-  for (auto& w : win_) w.cols.owner = w.bytes.owner = &own_;
+  slot_owner_.s[0] = p.stream();
+  slot_owner_.n = 1;
+  for (auto& w : win_) w.cols.owner = w.bytes.owner = w.packed.owner = &slot_owner_;
   return kOk;
 }
 
@@ -138,9 +159,11 @@ uint64_t SpanCursor::block_end(const std::vector<BlockInfo>& B, uint64_t pos) co
   return B[lo].coff + B[lo].csize;
 }
 
-int SpanCursor::decode_window(BamFile& f, Carry from, bool cont, Window* w, std::string* err) {
+int SpanCursor::decode_window(BamFile& f, Carry from, bool cont, uint64_t m, Window* w, std::string* err) {
   Step st;
+  ctrace("decode_window start", nwin_);
   int rc = f.decode_step(from, vend_, hbam::kReader, true, cont, &st, f.dropin_window_bytes());
+  ctrace("decode_step done", st.span.n);
   if (rc != kOk) {
     *err = f.error();
     return rc;
@@ -156,15 +179,23 @@ int SpanCursor::decode_window(BamFile& f, Carry from, bool cont, Window* w, std:
   w->status = st.status;
   w->error = st.error;
   w->blocks = std::make_shared<const std::vector<BlockInfo>>(p.blocks());
+  w->pack_m = 0;
   if (s.n) {
     const ColLayout L(s.n, true);
     CCHK(w->cols.reserve(L.bytes));
     CCHK(w->bytes.reserve(w->nbytes + 16));
     w->col = L.at(w->cols.p, &w->rec_pos);
-    CCHK(hbam::launch_export_records(s.col, s.rec_pos, w->col, w->rec_pos, s.n, s.p0, w->nbytes, p.stream()));
+    if (m) {  // batch-major columns for batches of m records (the caller's batch size)
+      const uint64_t nb = (s.n + m - 1) / m;
+      CCHK(w->packed.reserve((nb - 1) * ColLayout(m, false).bytes + ColLayout(s.n - (nb - 1) * m, false).bytes));
+      w->pack_m = m;
+    }
+    CCHK(hbam::launch_export_records(s.col, s.rec_pos, w->col, w->rec_pos, s.n, s.p0, w->nbytes,
+                                     w->pack_m ? w->packed.p : nullptr, w->pack_m, p.stream()));
     CCHK(hipMemcpyAsync(w->bytes.p, p.d_u() + s.p0, w->nbytes, hipMemcpyDeviceToDevice, p.stream()));
   }
   CCHK(hipEventRecord(w->ready, p.stream()));
+  ctrace("export queued");
   return kOk;
 }
 
@@ -207,25 +238,33 @@ int SpanCursor::issue(const Window& w, uint64_t k, uint64_t m, Slot* s, std::str
     return hipMemcpyAsync(h + L.off[c], from, m * ColLayout::size_of(c), hipMemcpyDeviceToHost, d2h_);
   };
   CCHK(hipStreamWaitEvent(d2h_, w.ready, 0));
-  CCHK(col(ColLayout::kKey, src.key));
-  CCHK(col(ColLayout::kRestOff, src.rest_off));
-  CCHK(col(ColLayout::kVoff, src.voff));
-  CCHK(col(ColLayout::kRefId, src.ref_id));
-  CCHK(col(ColLayout::kPos, src.pos));
-  CCHK(col(ColLayout::kLSeq, src.l_seq));
-  CCHK(col(ColLayout::kNextRefId, src.next_ref_id));
-  CCHK(col(ColLayout::kNextPos, src.next_pos));
-  CCHK(col(ColLayout::kTlen, src.tlen));
-  CCHK(col(ColLayout::kRestLen, src.rest_len));
-  CCHK(col(ColLayout::kBin, src.bin));
-  CCHK(col(ColLayout::kNCigar, src.n_cigar));
-  CCHK(col(ColLayout::kFlag, src.flag));
-  CCHK(col(ColLayout::kLReadName, src.l_read_name));
-  CCHK(col(ColLayout::kMapq, src.mapq));
+  // the batch-major copy of the columns when this batch is one of its blocks
+  s->packed = w.pack_m && k % w.pack_m == 0 && (m == w.pack_m || k + m == w.n);
+  if (s->packed) {
+    CCHK(hipMemcpyAsync(h, w.packed.p + (k / w.pack_m) * ColLayout(w.pack_m, false).bytes, L.bytes,
+                        hipMemcpyDeviceToHost, d2h_));
+  } else {
+    CCHK(col(ColLayout::kKey, src.key));
+    CCHK(col(ColLayout::kRestOff, src.rest_off));
+    CCHK(col(ColLayout::kVoff, src.voff));
+    CCHK(col(ColLayout::kRefId, src.ref_id));
+    CCHK(col(ColLayout::kPos, src.pos));
+    CCHK(col(ColLayout::kLSeq, src.l_seq));
+    CCHK(col(ColLayout::kNextRefId, src.next_ref_id));
+    CCHK(col(ColLayout::kNextPos, src.next_pos));
+    CCHK(col(ColLayout::kTlen, src.tlen));
+    CCHK(col(ColLayout::kRestLen, src.rest_len));
+    CCHK(col(ColLayout::kBin, src.bin));
+    CCHK(col(ColLayout::kNCigar, src.n_cigar));
+    CCHK(col(ColLayout::kFlag, src.flag));
+    CCHK(col(ColLayout::kLReadName, src.l_read_name));
+    CCHK(col(ColLayout::kMapq, src.mapq));
+  }
   if (s->end > s->start)
     CCHK(hipMemcpyAsync(h + L.bytes, w.bytes.p + s->start, s->end - s->start, hipMemcpyDeviceToHost, d2h_));
   CCHK(hipEventRecord(s->done, d2h_));
   s->busy = true;
+  ctrace("batch issued", k);
   return kOk;
 }
 
@@ -240,7 +279,7 @@ int SpanCursor::next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t 
   if (!cont) {  // a seek to the split start (or anywhere in it)
     reset();
     vend_ = vend;
-    rc = decode_window(f, Carry{vstart >> 16, vstart & 0xffff}, false, &win_[0], err);
+    rc = decode_window(f, Carry{vstart >> 16, vstart & 0xffff}, false, max_records, &win_[0], err);
     if (rc != kOk) return rc;
     nwin_ = 1;
     valid_ = true;
@@ -248,7 +287,7 @@ int SpanCursor::next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t 
   last_bounded_ = true;
   last_m_ = 0;
   auto decode_next = [&](const Window& w) -> int {
-    const int r = decode_window(f, w.next, true, &win_[nwin_ % 2], err);
+    const int r = decode_window(f, w.next, true, max_records, &win_[nwin_ % 2], err);
     if (r != kOk) {
       valid_ = false;
       return r;
@@ -301,15 +340,19 @@ int SpanCursor::next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t 
     e1 = small_[4];
     ahead = block_end(*N->blocks, N->base_pos + e1 - 1);
   }
+  ctrace("wait batch", k_);
   CCHK(hipEventSynchronize(S.done));
+  ctrace("batch landed", k_);
   S.busy = false;
   // the batch: columns at ColLayout(m), bytes after them; rest_off from the
   // batch's first record (the export kept them slot-relative)
   const ColLayout L(m, false);
   uint8_t* h = S.mem;
-  uint64_t* ro = reinterpret_cast<uint64_t*>(h + L.off[ColLayout::kRestOff]);
-  const uint64_t base = S.start;
-  for (uint64_t i = 0; i < m; ++i) ro[i] -= base;
+  if (!S.packed) {  // rest_off from the slot start -> from the batch's first record
+    uint64_t* ro = reinterpret_cast<uint64_t*>(h + L.off[ColLayout::kRestOff]);
+    const uint64_t base = S.start;
+    for (uint64_t i = 0; i < m; ++i) ro[i] -= base;
+  }
   const hbam::Columns c = L.at(h, nullptr);
   out->n = m;
   out->ref_id = c.ref_id;

@@ -7,6 +7,7 @@
 //   tokens  : per-chunk LZ77 token stream (phase A -> phase B of inflate)
 //   records : rec_pos / voff / SoA columns (one slot per record of the span)
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace hbam {
@@ -96,8 +97,11 @@ struct ColLayout {
   };
   uint64_t off[kCount];
   uint64_t bytes;
-  static constexpr uint32_t size_of(int c) { return c <= kRecPos ? 8 : c <= kRestLen ? 4 : c <= kFlag ? 2 : 1; }
-  ColLayout(uint64_t n, bool rec_pos) {
+  __host__ __device__ static constexpr uint32_t size_of(int c) {
+    return c <= kRecPos ? 8 : c <= kRestLen ? 4 : c <= kFlag ? 2 : 1;
+  }
+  ColLayout() = default;
+  __host__ __device__ ColLayout(uint64_t n, bool rec_pos) {
     uint64_t p = 0;
     for (int c = 0; c < kCount; ++c) {
       off[c] = p;
@@ -107,7 +111,7 @@ struct ColLayout {
     bytes = p;
   }
   // the Columns (no long-key list) of a buffer laid out this way
-  Columns at(uint8_t* b, uint64_t** rec_pos) const {
+  __host__ __device__ Columns at(uint8_t* b, uint64_t** rec_pos) const {
     Columns c{};
     c.key = reinterpret_cast<int64_t*>(b + off[kKey]);
     c.rest_off = reinterpret_cast<uint64_t*>(b + off[kRestOff]);

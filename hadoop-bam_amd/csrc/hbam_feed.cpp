@@ -4,6 +4,8 @@
 #include "hbam_feed.h"
 
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -162,14 +164,22 @@ hipError_t HostFeed::copy(uint8_t* dst, const uint8_t* src, size_t len, hipStrea
     if (!ev_[i] && (e = hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming)) != hipSuccess) return e;
   }
   CopyPool& cp = pool();
+  static const bool trace = getenv("HBAM_FEED_TRACE") != nullptr;  // developer timing lines on stderr
+  using clk = std::chrono::steady_clock;
   for (size_t o = 0, k = 0; o < len; o += kPiece, ++k) {
     const int j = (int)(k & 1);
+    const auto t0 = clk::now();
     if (busy_[j]) {  // this buffer's previous piece has crossed
       if ((e = hipEventSynchronize(ev_[j])) != hipSuccess) return e;
       busy_[j] = false;
     }
+    const auto t1 = clk::now();
     const size_t n = len - o < kPiece ? len - o : kPiece;
     cp.copy(buf_[j], src + o, n);
+    if (trace)
+      fprintf(stderr, "[feed %p] piece %zu: wait %.3f ms, fill %.3f ms (%zu B)\n", (void*)this, k,
+              std::chrono::duration<double, std::milli>(t1 - t0).count(),
+              std::chrono::duration<double, std::milli>(clk::now() - t1).count(), n);
     if ((e = hipMemcpyAsync(dst + o, buf_[j], n, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
     if ((e = hipEventRecord(ev_[j], s)) != hipSuccess) return e;
     busy_[j] = true;

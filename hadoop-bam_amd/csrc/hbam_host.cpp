@@ -12,6 +12,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 
 namespace hadoop_bam {
@@ -351,8 +352,20 @@ int BamFile::parse_header() {
   }
 }
 
+namespace {
+void htrace(const char* what) {  // HBAM_CURSOR_TRACE: developer timing lines on stderr
+  static const bool t = getenv("HBAM_CURSOR_TRACE") != nullptr;
+  if (!t) return;
+  static auto last = std::chrono::steady_clock::now();
+  const auto now = std::chrono::steady_clock::now();
+  fprintf(stderr, "[step] +%.3f ms %s\n", std::chrono::duration<double, std::milli>(now - last).count(), what);
+  last = now;
+}
+}  // namespace
+
 int BamFile::decode_step(Carry from, uint64_t vend, hbam::ChainMode mode, bool decode, bool continuation,
                          Step* out, uint64_t window) {
+  htrace("decode_step");
   *out = Step();
   Carry c = from;
   uint64_t span_w = window ? std::max<uint64_t>(window, 1ull << 16) : window_bytes_;
@@ -367,6 +380,7 @@ int BamFile::decode_step(Carry from, uint64_t vend, hbam::ChainMode mode, bool d
     if (clamp) hi = std::min(hi, std::max((vend >> 16) + 0x20000, c.coff + 0x20000));
     int rc = load_window(c.coff, hi, false, host_only);
     if (rc != kOk) return rc;
+    htrace("load_window + locate");
     hbam::Pipeline& p = *pipe_;
     // the split goes on past this window: start the next window's new bytes
     // on their way to HBM while this one decodes (Pipeline::stage)
@@ -416,7 +430,9 @@ int BamFile::decode_step(Carry from, uint64_t vend, hbam::ChainMode mode, bool d
       continue;
     }
     SpanDev s;
+    htrace("stage started");
     rc = p.decode_span_pos(p0, vend, mode, decode, &s);
+    htrace("decode_span_pos");
     if (rc != kOk) {
       err_ = p.error();
       return rc;

@@ -367,6 +367,8 @@ class SpanCursor {
  private:
   struct Window {  // one decoded window's records, exported out of the pipeline
     hbam::DevBuf<uint8_t> cols, bytes;
+    hbam::DevBuf<uint8_t> packed;  // the columns again, batch-major in batches of pack_m (one D2H per batch)
+    uint64_t pack_m = 0;
     hbam::Columns col{};
     uint64_t* rec_pos = nullptr;  // n + 1 entries: slot byte offsets, [n] = nbytes
     uint64_t n = 0, nbytes = 0, base_pos = 0, id = 0;
@@ -382,10 +384,11 @@ class SpanCursor {
     size_t cap = 0;
     hipEvent_t done = nullptr;
     bool busy = false;            // copies queued
+    bool packed = false;          // columns came batch-major (rest_off already batch-relative)
     uint64_t win = 0, k = 0, m = 0, start = 0, end = 0, ahead_end = 0, next_voff = 0;
   };
   int ensure_streams(hbam::Pipeline& p, std::string* err);
-  int decode_window(BamFile& f, Carry from, bool cont, Window* w, std::string* err);
+  int decode_window(BamFile& f, Carry from, bool cont, uint64_t m, Window* w, std::string* err);
   int issue(const Window& w, uint64_t k, uint64_t m, Slot* s, std::string* err);
   int drain();
   int next_batch_all(BamFile& f, uint64_t vstart, uint64_t vend, BatchView* out, uint64_t* next_voff,
@@ -396,7 +399,12 @@ class SpanCursor {
   uint64_t vend_ = 0, next_voff_ = 0;
   hipStream_t d2h_ = nullptr, meta_ = nullptr;
   int device_ = -1;
-  hbam::StreamSet own_;            // the pipeline stream + d2h_ + meta_ (owner of the slots' device buffers)
+  hbam::StreamSet own_;            // the pipeline stream + d2h_ + meta_
+  // owner of the window slots' device buffers: the pipeline stream only (the
+  // export writes them there).  A slot is decoded into again only after every
+  // batch of its previous window has landed, so its regrowth need not wait for
+  // the batch copies of the other slot's window in flight on d2h_.
+  hbam::StreamSet slot_owner_;
   Window win_[2];
   uint64_t front_ = 0, nwin_ = 0;  // window ids: front_ = the one being handed out; nwin_ decoded so far
   uint64_t k_ = 0;                 // next record of the front window

@@ -3221,8 +3221,6 @@ __device__ __forceinline__ void copy_record_fields(const Columns& s, uint64_t i,
   d.mapq[j] = s.mapq[i];
 }
 
-// slot <- records [0, n) of a span; positions rebased so that window position
-// `base` (the first record's start) is slot byte 0; dpos[n] = the slot's bytes
 // Device -> page-locked host bytes written by the shader engines: a host
 // read-back that never waits behind copy-engine traffic of other streams (a
 // pageable hipMemcpy D2H of the block table queued ~13 ms behind a drop-in
@@ -3240,12 +3238,26 @@ __global__ __launch_bounds__(256) void k_readback(uint8_t* __restrict__ dst, con
   }
 }
 
+// slot <- records [0, n) of a span; positions rebased so that window position
+// `base` (the first record's start) is slot byte 0; dpos[n] = the slot's bytes
+// Also (packed != nullptr) the columns once more, batch-major: the records
+// [b*m, b*m + m) of batch b as one ColLayout(m) block at packed + b * lf.bytes
+// (the last, shorter batch as ColLayout(n - b*m) = ll), with rest_off counted
+// from the batch's first record -- exactly a drop-in host slot's column area,
+// so a batch's columns cross PCIe as one copy instead of fifteen.
 __global__ __launch_bounds__(256) void k_export_records(Columns s, const uint64_t* __restrict__ spos, Columns d,
                                                         uint64_t* __restrict__ dpos, uint64_t n, uint64_t base,
-                                                        uint64_t nbytes) {
+                                                        uint64_t nbytes, uint8_t* __restrict__ packed, ColLayout lf,
+                                                        ColLayout ll, uint64_t m) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     copy_record_fields(s, i, d, i, base);
     dpos[i] = spos[i] - base;
+    if (packed) {
+      const uint64_t b = i / m, j = i - b * m;
+      const bool last = (b + 1) * m > n;
+      const Columns c = (last ? ll : lf).at(packed + b * lf.bytes, nullptr);
+      copy_record_fields(s, i, c, j, spos[b * m]);
+    }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) dpos[n] = nbytes;
 }
@@ -3590,9 +3602,11 @@ hipError_t launch_readback(void* dst, const void* src, uint64_t n, hipStream_t s
   return hipGetLastError();
 }
 hipError_t launch_export_records(const Columns& src, const uint64_t* src_pos, const Columns& dst, uint64_t* dst_pos,
-                                 uint64_t n, uint64_t base, uint64_t nbytes, hipStream_t s) {
+                                 uint64_t n, uint64_t base, uint64_t nbytes, uint8_t* packed, uint64_t m,
+                                 hipStream_t s) {
+  const ColLayout lf(m ? m : 1, false), ll(m ? n - (n ? (n - 1) / m : 0) * m : 1, false);
   hipLaunchKernelGGL(k_export_records, dim3(grid_for(std::max<uint64_t>(n, 1), 256, 8192)), dim3(256), 0, s, src,
-                     src_pos, dst, dst_pos, n, base, nbytes);
+                     src_pos, dst, dst_pos, n, base, nbytes, m ? packed : nullptr, lf, ll, m ? m : 1);
   return hipGetLastError();
 }
 hipError_t launch_digest(const int64_t* keys, const uint64_t* voffs, uint64_t n, uint64_t* out, hipStream_t s) {

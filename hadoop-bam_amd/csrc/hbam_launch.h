@@ -104,9 +104,12 @@ hipError_t launch_sbi_emit(const uint64_t* voff, uint64_t n, uint32_t g, uint64_
 hipError_t launch_next_pos(const uint8_t* u, const uint64_t* rec_pos, uint64_t n, uint64_t p0, int mode,
                            uint64_t* out, hipStream_t s);
 // drop-in batches: records [0, n) of a decoded span -> an export slot
-// (ColLayout with rec_pos; positions rebased by base, dst_pos[n] = nbytes)
+// (ColLayout with rec_pos; positions rebased by base, dst_pos[n] = nbytes);
+// m > 0: also batch-major column blocks of m records at `packed`
+// (k_export_records)
 hipError_t launch_export_records(const Columns& src, const uint64_t* src_pos, const Columns& dst, uint64_t* dst_pos,
-                                 uint64_t n, uint64_t base, uint64_t nbytes, hipStream_t s);
+                                 uint64_t n, uint64_t base, uint64_t nbytes, uint8_t* packed, uint64_t m,
+                                 hipStream_t s);
 // n bytes device -> page-locked host by a kernel (no copy engine)
 hipError_t launch_readback(void* dst, const void* src, uint64_t n, hipStream_t s);
 // out[0] ^= xor of keys (if keys), out[1] += sum of voffs, out[2..3] += the

@@ -5,6 +5,7 @@
 #include <thread>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -31,14 +32,23 @@ Pipeline::Pipeline(int device) : device_(device) {
   if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&stream_b_, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&stream_t_, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&stream_copy_, hipStreamNonBlocking) != hipSuccess)
+      hipStreamCreateWithFlags(&stream_copy_, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&stream_stage_, hipStreamNonBlocking) != hipSuccess)
     err_ = "hipStreamCreate failed";
   streams_.s[0] = stream_;
   streams_.s[1] = stream_b_;
   streams_.s[2] = stream_t_;
   streams_.s[3] = stream_copy_;
   streams_.n = 4;
-  own(own_file_, own_spare_, stage_, dblocks_, ref_len_, du_, tokens_[0], tokens_[1], hout_, tables_[0], tables_[1],
+  // the staging copy (stage()) runs on its own stream, outside streams_: a
+  // buffer of the decode that grows waits for the decode's streams only, not
+  // for the next window's bytes on their way (that wait cost 5-13 ms per
+  // drop-in window); stage_ itself is written there and read on stream_
+  stage_owner_.s[0] = stream_stage_;
+  stage_owner_.s[1] = stream_;
+  stage_owner_.n = 2;
+  stage_.owner = &stage_owner_;
+  own(own_file_, own_spare_, dblocks_, ref_len_, du_, tokens_[0], tokens_[1], hout_, tables_[0], tables_[1],
       tinfo_[0], tinfo_[1], g_, x_, x2_, entry_, base_arr_, summary_, dead_, cand_, sorted_, isz_, ust_, cnt_, flags_,
       errv_, need_, rec_pos_, rec_voff_, rcand_, force_, wcnt_, counters_, list_, hlong_, scan_tmp_, cols_, long_rec_,
       long_n_, wbuf_, woffs_, wbad_, scalars_);
@@ -53,7 +63,9 @@ Pipeline::~Pipeline() {
   (void)hipSetDevice(device_);
   // this pipeline's own streams only: other contexts on the GPU run on
   (void)streams_.sync();
+  (void)stage_owner_.sync();
   streams_.n = 0;  // drained: the member buffers release without waiting (the streams go below)
+  stage_owner_.n = 0;
   if (rb_buf_) pinned_free(rb_buf_, rb_cap_);
   for (auto& e : ev_) (void)hipEventDestroy(e);
   for (auto& e : sync_ev_) (void)hipEventDestroy(e);
@@ -61,7 +73,7 @@ Pipeline::~Pipeline() {
   for (auto& e : hdone_ev_) (void)hipEventDestroy(e);
   for (auto& e : tev_) (void)hipEventDestroy(e);
   for (auto& e : copy_ev_) (void)hipEventDestroy(e);
-  for (hipStream_t s : {stream_b_, stream_t_, stream_copy_, stream_})
+  for (hipStream_t s : {stream_b_, stream_t_, stream_copy_, stream_stage_, stream_})
     if (s) (void)hipStreamDestroy(s);
 }
 
@@ -84,6 +96,8 @@ int Pipeline::hip_check(hipError_t e, const char* what) {
 
 int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof, uint64_t* host_bytes) {
   HIPCHK(hipSetDevice(device_));
+  static const bool tr = getenv("HBAM_CURSOR_TRACE") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
   // the prefix of [base, base + len) that the window in place already holds
   uint64_t keep = 0;
   if (dfile_ && own_file_.p && dfile_ == own_file_.p + (base_ & 15) && base >= base_ && base < base_ + flen_)
@@ -113,6 +127,10 @@ int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof
   if (host_bytes) *host_bytes = host;
   HIPCHK(hipMemsetAsync(dfile_ + len, 0, kFilePad, stream_));
   HIPCHK(rb_sync(stream_));
+  if (tr)
+    fprintf(stderr, "[load] %.3f ms: %llu B kept, %llu B from host\n",
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+            (unsigned long long)keep, (unsigned long long)host);
   flen_ = len;
   base_ = base;
   at_eof_ = at_eof;
@@ -190,7 +208,7 @@ int Pipeline::stage(const uint8_t* host, uint64_t lo, uint64_t hi) {
   // window's decode while the next window's bytes cross the link.
   uint8_t* dst = stage_.p;
   const int dev = device_;
-  hipStream_t cs = stream_copy_;
+  hipStream_t cs = stream_stage_;
   stage_thr_ = std::thread([this, dst, host, lo, hi, dev, cs]() {
     hipError_t e = hipSetDevice(dev);
     if (e == hipSuccess) e = feed_stage_.copy(dst, host + lo, hi - lo, cs);
@@ -398,7 +416,7 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
   if (!dfile_ || dfile_ != own_file_.p || len != flen_ || base_ != 0 || !at_eof_)
     return fail(kErrState, "run_streamed needs the whole file loaded in one window");
   HIPCHK(hipSetDevice(device_));
-  if (int rc = stage_wait()) return rc;  // a staged copy shares stream_copy_
+  if (int rc = stage_wait()) return rc;  // no staged copy in flight over the window being replaced
   piece = std::max<uint64_t>(piece, 1ull << 20);
   const uint64_t np = std::max<uint64_t>(1, (len + piece - 1) / piece);
   // capacity up front, so that nothing reallocates under queued work (grow()

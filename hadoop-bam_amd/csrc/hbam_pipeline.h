@@ -249,6 +249,8 @@ class Pipeline {
   StreamSet streams_;
   hipStream_t stream_ = nullptr;
   hipStream_t stream_copy_ = nullptr;  // run_streamed: host->HBM pieces
+  hipStream_t stream_stage_ = nullptr;  // stage(): the next window's bytes (not in streams_)
+  StreamSet stage_owner_;              // stage_'s owner: stream_stage_ + stream_
   std::vector<hipEvent_t> copy_ev_;
   std::string err_;
 

@@ -19,6 +19,10 @@
   } while (0)
 
 __global__ void k_read(unsigned long long* dst, const unsigned long long* src) { *dst = *src; }
+__global__ void k_copy(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n16) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
 
 static double now_ms() {
   using namespace std::chrono;
@@ -69,6 +73,39 @@ int main() {
       double t3 = now_ms();
       printf("rep %d %-40s small done after %7.3f ms, big done after %7.3f ms (issue %.3f)\n", rep, what, t2 - t1,
              t3 - t1, t1 - t0);
+    }
+  }
+  // full duplex?  a 1 GiB H2D (page-locked) beside a 1 GiB D2H, both by copy
+  // engines, then the D2H by a kernel writing page-locked memory
+  void *hbig2, *dbig2;
+  CK(hipHostMalloc(&hbig2, big, hipHostMallocDefault));
+  CK(hipMalloc(&dbig2, big));
+  for (int rep = 0; rep < 2; ++rep) {
+    double t0 = now_ms();
+    CK(hipMemcpyAsync(dbig2, hbig2, big, hipMemcpyHostToDevice, b));
+    CK(hipStreamSynchronize(b));
+    double t1 = now_ms();
+    CK(hipMemcpyAsync(hbig, dbig, big, hipMemcpyDeviceToHost, a));
+    CK(hipMemcpyAsync(dbig2, hbig2, big, hipMemcpyHostToDevice, b));
+    CK(hipStreamSynchronize(b));
+    double t2 = now_ms();
+    CK(hipStreamSynchronize(a));
+    double t3 = now_ms();
+    printf("H2D alone %.2f ms; H2D beside D2H: H2D %.2f ms, both %.2f ms\n", t1 - t0, t2 - t1, t3 - t1);
+    for (int wg : {16, 32, 64, 128}) {
+      double u0 = now_ms();
+      k_copy<<<wg, 256, 0, a>>>((uint4*)hbig, (const uint4*)dbig, big / 16);
+      CK(hipGetLastError());
+      CK(hipStreamSynchronize(a));
+      double u1 = now_ms();
+      k_copy<<<wg, 256, 0, a>>>((uint4*)hbig, (const uint4*)dbig, big / 16);
+      CK(hipMemcpyAsync(dbig2, hbig2, big, hipMemcpyHostToDevice, b));
+      CK(hipStreamSynchronize(b));
+      double u2 = now_ms();
+      CK(hipStreamSynchronize(a));
+      double u3 = now_ms();
+      printf("  kernel D2H (%d WG) alone %.2f ms (%.1f GB/s); beside SDMA H2D: H2D %.2f ms, both %.2f ms\n", wg,
+             u1 - u0, big / (u1 - u0) / 1e6, u2 - u1, u3 - u1);
     }
   }
   return 0;
