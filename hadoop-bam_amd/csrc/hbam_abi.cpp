@@ -195,18 +195,6 @@ int decode_device(BamFile& f, uint64_t vstart, uint64_t vend, int32_t flags, hba
   if (rc != HBAM_OK) st->status = rc;
   return rc != HBAM_OK ? rc : st->status;
 }
-
-// Hardware queues.  A context drives up to seven streams (decode, phase B,
-// tables, run_streamed copies, staging; the drop-in batches' D2H and meta
-// reads).  With HIP's default of 4 hardware queues per device, streams share
-// queues, and an event or stream wait queued behind a batch's D2H on a shared
-// queue holds the decode kernels behind it: the resident drop-in loop ran at
-// 32 GB/s U with 4 queues and 42-44 with 8 (same build, same box).  When the
-// process has not chosen a value, ask for 8 -- read by the HIP runtime when
-// it initializes, so this takes effect when libhbam is the first HIP user of
-// the process (a JVM executor; a Python process that imports torch first
-// should export it itself).
-__attribute__((constructor)) void hbam_default_hw_queues() { setenv("GPU_MAX_HW_QUEUES", "8", 0); }
 }  // namespace
 
 extern "C" {

@@ -3,12 +3,13 @@
 // 223-232), with the next batch and the next window in flight (hbam_host.h).
 //
 // Per window: BamFile::decode_step decodes it in the pipeline, k_export_records
-// + one D2D copy move its records (columns, record bytes) into window slot
+// + k_pack_rests move its records (columns, record bytes, rests) into window slot
 // (id % 2), positions rebased to the slot.  Per batch (records [k, k + m) of
 // one window): three boundary reads (record k's start, the batch end, the
-// read-ahead record's end) and the next voff on the meta stream, then the 15
-// column slices and the record bytes go HBM -> page-locked host slot on the
-// d2h stream (SDMA only: no kernel shares a hardware queue with the decode).
+// read-ahead record's end) and the next voff, gathered by one small kernel on
+// the meta stream, then the batch's columns (one batch-major block) and its
+// rests (no fixed fields) go HBM -> page-locked host slot on the d2h stream.  Both are
+// high-priority streams, on hardware queues of their own (hbam_pipeline.h).
 // The batch handed out lives in one host slot while the next one fills the
 // other.
 #include <hip/hip_runtime.h>
@@ -91,6 +92,7 @@ SpanCursor::~SpanCursor() {
     w.cols.release();
     w.bytes.release();
     w.packed.release();
+    w.rests.release();
     if (w.ready) (void)hipEventDestroy(w.ready);
   }
   for (auto& s : slot_) {
@@ -112,8 +114,8 @@ int SpanCursor::ensure_streams(hbam::Pipeline& p, std::string* err) {
   if (device_ != p.device()) {
     if (d2h_) (void)hipStreamDestroy(d2h_);
     if (meta_) (void)hipStreamDestroy(meta_);
-    CCHK(hipStreamCreateWithFlags(&d2h_, hipStreamNonBlocking));
-    CCHK(hipStreamCreateWithFlags(&meta_, hipStreamNonBlocking));
+    CCHK(hbam::create_stream(&d2h_, hbam::StreamLevel::kHigh));  // own queues (hbam_pipeline.h)
+    CCHK(hbam::create_stream(&meta_, hbam::StreamLevel::kHigh));
     if (!small_) CCHK(hipHostMalloc(reinterpret_cast<void**>(&small_), 64, hipHostMallocDefault));
     for (auto& w : win_)
       if (!w.ready) CCHK(hipEventCreateWithFlags(&w.ready, hipEventDisableTiming));
@@ -127,7 +129,7 @@ int SpanCursor::ensure_streams(hbam::Pipeline& p, std::string* err) {
   own_.n = 3;
   slot_owner_.s[0] = p.stream();
   slot_owner_.n = 1;
-  for (auto& w : win_) w.cols.owner = w.bytes.owner = w.packed.owner = &slot_owner_;
+  for (auto& w : win_) w.cols.owner = w.bytes.owner = w.packed.owner = w.rests.owner = &slot_owner_;
   return kOk;
 }
 
@@ -192,7 +194,11 @@ int SpanCursor::decode_window(BamFile& f, Carry from, bool cont, uint64_t m, Win
     }
     CCHK(hbam::launch_export_records(s.col, s.rec_pos, w->col, w->rec_pos, s.n, s.p0, w->nbytes,
                                      w->pack_m ? w->packed.p : nullptr, w->pack_m, p.stream()));
-    CCHK(hipMemcpyAsync(w->bytes.p, p.d_u() + s.p0, w->nbytes, hipMemcpyDeviceToDevice, p.stream()));
+    // the record bytes (encode_writables of the last batch) and the rests alone (the batches)
+    const uint8_t* u = s.data ? s.data : p.d_u();
+    CCHK(hipMemcpyAsync(w->bytes.p, u + s.p0, w->nbytes, hipMemcpyDeviceToDevice, p.stream()));
+    CCHK(w->rests.reserve(w->nbytes - 36 * s.n + 16));
+    CCHK(hbam::launch_pack_rests(u, s.col.rest_off, s.col.rest_len, s.n, s.p0, w->rests.p, p.stream()));
   }
   CCHK(hipEventRecord(w->ready, p.stream()));
   ctrace("export queued");
@@ -204,10 +210,9 @@ int SpanCursor::issue(const Window& w, uint64_t k, uint64_t m, Slot* s, std::str
   // record's end (slot positions) and the next record's voff
   const uint64_t e = k + m;
   CCHK(hipStreamWaitEvent(meta_, w.ready, 0));
-  CCHK(hipMemcpyAsync(small_ + 0, w.rec_pos + k, 8, hipMemcpyDeviceToHost, meta_));
-  CCHK(hipMemcpyAsync(small_ + 1, w.rec_pos + e, 8, hipMemcpyDeviceToHost, meta_));
-  CCHK(hipMemcpyAsync(small_ + 2, w.rec_pos + std::min(e + 1, w.n), 8, hipMemcpyDeviceToHost, meta_));
-  if (e < w.n) CCHK(hipMemcpyAsync(small_ + 3, w.col.voff + e, 8, hipMemcpyDeviceToHost, meta_));
+  // read by a kernel: a DMA copy would queue behind the other slot's batch
+  const uint64_t* bounds[4] = {w.rec_pos + k, w.rec_pos + e, w.rec_pos + std::min(e + 1, w.n), w.col.voff + e};
+  CCHK(hbam::launch_gather_u64(small_, bounds, e < w.n ? 4 : 3, meta_));
   CCHK(hipStreamSynchronize(meta_));
   s->win = w.id;
   s->k = k;
@@ -217,7 +222,9 @@ int SpanCursor::issue(const Window& w, uint64_t k, uint64_t m, Slot* s, std::str
   s->ahead_end = e < w.n ? small_[2] : ~0ull;
   s->next_voff = e < w.n ? small_[3] : ~0ull;
   const ColLayout L(m, false);
-  const size_t need = L.bytes + (s->end - s->start) + 64;
+  // the batch's rests: [start - 36 k, end - 36 e) of the window's packed rests
+  const uint64_t rest_lo = s->start - 36 * k, rest_bytes = (s->end - s->start) - 36 * m;
+  const size_t need = L.bytes + rest_bytes + 64;
   if (s->cap < need) {
     if (s->mem) hbam::pinned_free(s->mem, s->cap);
     s->mem = nullptr;
@@ -239,7 +246,8 @@ int SpanCursor::issue(const Window& w, uint64_t k, uint64_t m, Slot* s, std::str
   };
   CCHK(hipStreamWaitEvent(d2h_, w.ready, 0));
   // the batch-major copy of the columns when this batch is one of its blocks
-  s->packed = w.pack_m && k % w.pack_m == 0 && (m == w.pack_m || k + m == w.n);
+  // (block k / pack_m holds min(pack_m, n - k) records)
+  s->packed = w.pack_m && k % w.pack_m == 0 && m == std::min(w.pack_m, w.n - k);
   if (s->packed) {
     CCHK(hipMemcpyAsync(h, w.packed.p + (k / w.pack_m) * ColLayout(w.pack_m, false).bytes, L.bytes,
                         hipMemcpyDeviceToHost, d2h_));
@@ -260,8 +268,7 @@ int SpanCursor::issue(const Window& w, uint64_t k, uint64_t m, Slot* s, std::str
     CCHK(col(ColLayout::kLReadName, src.l_read_name));
     CCHK(col(ColLayout::kMapq, src.mapq));
   }
-  if (s->end > s->start)
-    CCHK(hipMemcpyAsync(h + L.bytes, w.bytes.p + s->start, s->end - s->start, hipMemcpyDeviceToHost, d2h_));
+  if (rest_bytes) CCHK(hipMemcpyAsync(h + L.bytes, w.rests.p + rest_lo, rest_bytes, hipMemcpyDeviceToHost, d2h_));
   CCHK(hipEventRecord(s->done, d2h_));
   s->busy = true;
   ctrace("batch issued", k);
@@ -335,7 +342,8 @@ int SpanCursor::next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t 
   } else if (N && N->n) {
     uint64_t e1 = 0;
     CCHK(hipStreamWaitEvent(meta_, N->ready, 0));
-    CCHK(hipMemcpyAsync(small_ + 4, N->rec_pos + 1, 8, hipMemcpyDeviceToHost, meta_));
+    const uint64_t* src[1] = {N->rec_pos + 1};
+    CCHK(hbam::launch_gather_u64(small_ + 4, src, 1, meta_));
     CCHK(hipStreamSynchronize(meta_));
     e1 = small_[4];
     ahead = block_end(*N->blocks, N->base_pos + e1 - 1);
@@ -344,14 +352,15 @@ int SpanCursor::next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t 
   CCHK(hipEventSynchronize(S.done));
   ctrace("batch landed", k_);
   S.busy = false;
-  // the batch: columns at ColLayout(m), bytes after them; rest_off from the
-  // batch's first record (the export kept them slot-relative)
+  // the batch: columns at ColLayout(m), the rests after them; rest_off in
+  // the rests from the batch's first record (the export kept them slot-
+  // relative in the record bytes)
   const ColLayout L(m, false);
   uint8_t* h = S.mem;
-  if (!S.packed) {  // rest_off from the slot start -> from the batch's first record
+  if (!S.packed) {  // slot position of record i's rest -> its offset among the batch's rests
     uint64_t* ro = reinterpret_cast<uint64_t*>(h + L.off[ColLayout::kRestOff]);
     const uint64_t base = S.start;
-    for (uint64_t i = 0; i < m; ++i) ro[i] -= base;
+    for (uint64_t i = 0; i < m; ++i) ro[i] -= base + 36 * (i + 1);
   }
   const hbam::Columns c = L.at(h, nullptr);
   out->n = m;
@@ -371,7 +380,7 @@ int SpanCursor::next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t 
   out->rest_off = c.rest_off;
   out->rest_len = c.rest_len;
   out->data = h + L.bytes;
-  out->data_len = S.end - S.start;
+  out->data_len = (S.end - S.start) - 36 * m;
   cur_ = s;
   last_win_ = W.id;
   last_k_ = k_;
@@ -473,7 +482,8 @@ int SpanCursor::reader_position(uint64_t i, uint64_t* pos, std::string* err) con
   }
   auto last_byte_end = [&](uint64_t j) -> uint64_t {
     const uint64_t rel = v.rest_off[j] + v.rest_len[j] - 1;  // from data[0]
-    if (last_bounded_) return block_end(*last_blocks_, last_base_pos_ + last_start_ + rel);
+    // a bounded batch's data holds the rests alone: 36 B per record before j's end
+    if (last_bounded_) return block_end(*last_blocks_, last_base_pos_ + last_start_ + rel + 36 * (j + 1));
     // whole-split batch: the segment (window) of record j
     size_t g = all_seg_.size() - 1;
     while (g > 0 && all_seg_[g].first > j) --g;
@@ -496,7 +506,7 @@ int SpanCursor::initial_position(uint64_t* pos, std::string* err) const {
   }
   // record 0's own last byte (nothing has been read ahead yet)
   const uint64_t rel = last_view_.rest_off[0] + last_view_.rest_len[0] - 1;
-  *pos = last_bounded_ ? block_end(*last_blocks_, last_base_pos_ + last_start_ + rel)
+  *pos = last_bounded_ ? block_end(*last_blocks_, last_base_pos_ + last_start_ + rel + 36)
                        : block_end(*all_seg_[0].second, all_.window_pos[0] + rel);
   return kOk;
 }

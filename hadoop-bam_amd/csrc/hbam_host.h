@@ -368,6 +368,7 @@ class SpanCursor {
   struct Window {  // one decoded window's records, exported out of the pipeline
     hbam::DevBuf<uint8_t> cols, bytes;
     hbam::DevBuf<uint8_t> packed;  // the columns again, batch-major in batches of pack_m (one D2H per batch)
+    hbam::DevBuf<uint8_t> rests;   // the records' rests back to back (k_pack_rests): what a batch sends
     uint64_t pack_m = 0;
     hbam::Columns col{};
     uint64_t* rec_pos = nullptr;  // n + 1 entries: slot byte offsets, [n] = nbytes
@@ -379,7 +380,7 @@ class SpanCursor {
     std::string error;
     hipEvent_t ready = nullptr;  // export done
   };
-  struct Slot {  // a page-locked batch: ColLayout(m) columns, then the bytes
+  struct Slot {  // a page-locked batch: ColLayout(m) columns, then the records' rests
     uint8_t* mem = nullptr;
     size_t cap = 0;
     hipEvent_t done = nullptr;

@@ -243,6 +243,13 @@ constexpr int kDistSubCap = 512;
 enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_LONG = 3, K_BAD = 4, K_SLOW = 5 };
 constexpr uint32_t kBadEntry = K_BAD << 26;
 constexpr uint32_t kLongTag = 0xF0000000u;  // build-time mark: kLongTag | (max len - root)
+#ifndef HBAM_FILL_BY_INDEX
+#define HBAM_FILL_BY_INDEX 0
+#endif
+#ifndef HBAM_FILL_CHECK
+#define HBAM_FILL_CHECK 0
+#endif
+constexpr bool kFillByIndex = HBAM_FILL_BY_INDEX != 0;  // build_table's root fill (below)
 constexpr uint32_t kKindLit = 1u << 26;  // e < kKindLit  <=>  literal entry
 
 __constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
@@ -341,11 +348,20 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
     else if (left > 0 && (mode == 2 || maxl != 1)) st = 1;
     L.bt_status = st;
   }
-  for (int i = lane; i < (1 << root); i += 64) tab[i] = kBadEntry;
+  // by index (below): every entry is written by the fill, none beforehand
+  const bool by_index = kFillByIndex && sub != nullptr;
+  if (!by_index)
+    for (int i = lane; i < (1 << root); i += 64) tab[i] = kBadEntry;
   wave_sync();
   const uint32_t st = rfl(L.bt_status);
   if (st == 1) return 1;
-  if (st == 2) return 0;  // no codes: all-invalid table
+  if (st == 2) {  // no codes: all-invalid table
+    if (by_index) {
+      for (int i = lane; i < (1 << root); i += 64) tab[i] = kBadEntry;
+      wave_sync();
+    }
+    return 0;
+  }
   const uint32_t rmask = (1u << root) - 1;
   const uint64_t ltmask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   bool any_long = false;
@@ -371,14 +387,63 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
       L.rev_of[s] = (uint16_t)rev;
       if ((int)l <= root) {
         const uint32_t e = make_entry(mode, (uint32_t)s, l);
-        for (uint32_t i = rev; i < (1u << root); i += (1u << l)) tab[i] = e;
+        if (by_index) sub[L.offs[l] + rank] = e;  // entries in canonical order (sub[] is free until below)
+        else
+          for (uint32_t i = rev; i < (1u << root); i += (1u << l)) tab[i] = e;
       } else {
-        atomicMax(&tab[rev & rmask], kLongTag | (l - (uint32_t)root));  // widest sub-table under the prefix
+        if (!by_index) atomicMax(&tab[rev & rmask], kLongTag | (l - (uint32_t)root));  // widest sub-table under the prefix
         any_long = true;
       }
     }
   }
   wave_sync();
+  if (by_index) {
+    // Root fill by table index, the same work for every lane (the per-symbol
+    // fill loops 2^(root - l) times, and the lane of the shortest code sets
+    // the wave's pace).  Canonical codes of length l <= root cover the
+    // left-aligned values [A_l, B_l), A_l = firstc[l] << (root - l),
+    // B_l = (firstc[l] + cnt[l]) << (root - l), contiguous in l: value v
+    // belongs to the code of rank (v - A_l) >> (root - l) of its length, and
+    // values >= B_root to no code of length <= root (a sub-table prefix or,
+    // in an incomplete code, nothing).  Lane j takes values [j K, j K + K),
+    // K = 2^root / 64; table index = v bit-reversed.
+    const uint32_t K = (1u << root) >> 6, v0 = lane * K;
+    for (uint32_t v = v0; v < v0 + K; ++v) {
+      uint32_t e = kBadEntry;
+      for (int l = 1; l <= root; ++l) {
+        const uint32_t a = L.firstc[l] << (root - l), c = cnt[l] << (root - l);
+        if (v - a < c) e = sub[L.offs[l] + ((v - a) >> (root - l))];
+      }
+      tab[__brev(v) >> (32 - root)] = e;
+    }
+    wave_sync();
+    if (__ballot(any_long) != 0) {
+      for (int s2 = lane; s2 < nsym; s2 += 64) {
+        const uint32_t l = lens[s2];
+        if ((int)l > root) atomicMax(&tab[L.rev_of[s2] & rmask], kLongTag | (l - (uint32_t)root));
+      }
+      wave_sync();
+    }
+#if HBAM_FILL_CHECK
+    // check build: every entry against the per-symbol fill
+    uint32_t bad = 0;
+    for (int s2 = 0; s2 < nsym; ++s2) {
+      const uint32_t l = lens[s2];
+      if (l == 0 || (int)l > root) continue;
+      const uint32_t e = make_entry(mode, (uint32_t)s2, l);
+      for (uint32_t i = L.rev_of[s2] + (lane << l); i < (1u << root); i += (64u << l)) bad += tab[i] != e;
+    }
+    for (uint32_t i = lane; i < (1u << root); i += 64) {
+      const uint32_t v = __brev(i) >> (32 - root);
+      const uint32_t end = (L.firstc[root] + cnt[root]);
+      if (v >= end && tab[i] != kBadEntry && tab[i] < kLongTag) bad++;
+    }
+    if (__ballot(bad != 0)) {
+      if (lane == 0) printf("hbam fill check: mode %d root %d nsym %d: mismatching entries\n", mode, root, nsym);
+      return 1;
+    }
+#endif
+  }
   if (__ballot(any_long) == 0) return 0;
   // sub-table bases: exclusive scan of the sub-table sizes in root-index order
   uint32_t used = 0;
@@ -3238,13 +3303,24 @@ __global__ __launch_bounds__(256) void k_readback(uint8_t* __restrict__ dst, con
   }
 }
 
+// host[i] <- *src[i] for i < n (n <= kGatherMax): a few scattered values read
+// back by one launch, with no DMA-engine copy to queue behind larger ones
+struct U64Srcs {
+  const uint64_t* p[kGatherMax];
+};
+__global__ __launch_bounds__(64) void k_gather_u64(uint64_t* __restrict__ dst, U64Srcs src, int n) {
+  const int i = threadIdx.x;
+  if (i < n) dst[i] = *src.p[i];
+}
+
 // slot <- records [0, n) of a span; positions rebased so that window position
 // `base` (the first record's start) is slot byte 0; dpos[n] = the slot's bytes
 // Also (packed != nullptr) the columns once more, batch-major: the records
 // [b*m, b*m + m) of batch b as one ColLayout(m) block at packed + b * lf.bytes
 // (the last, shorter batch as ColLayout(n - b*m) = ll), with rest_off counted
-// from the batch's first record -- exactly a drop-in host slot's column area,
-// so a batch's columns cross PCIe as one copy instead of fifteen.
+// in the packed rests (k_pack_rests) from the batch's first record -- exactly
+// a drop-in host slot's column area, so a batch's columns cross PCIe as one
+// copy instead of fifteen.
 __global__ __launch_bounds__(256) void k_export_records(Columns s, const uint64_t* __restrict__ spos, Columns d,
                                                         uint64_t* __restrict__ dpos, uint64_t n, uint64_t base,
                                                         uint64_t nbytes, uint8_t* __restrict__ packed, ColLayout lf,
@@ -3257,6 +3333,7 @@ __global__ __launch_bounds__(256) void k_export_records(Columns s, const uint64_
       const bool last = (b + 1) * m > n;
       const Columns c = (last ? ll : lf).at(packed + b * lf.bytes, nullptr);
       copy_record_fields(s, i, c, j, spos[b * m]);
+      c.rest_off[j] -= 36 * (j + 1);  // into the batch's packed rests (k_pack_rests)
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) dpos[n] = nbytes;
@@ -3285,6 +3362,51 @@ __device__ __forceinline__ uint4 shift16(const uint4 a, const uint4 b, uint32_t 
   }
   return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
                     __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r));
+}
+
+// Drop-in batches carry each record's rest only (read name .. aux): the 36
+// bytes of block_size + fixed fields are in the columns already, and leaving
+// them out cuts a batch's D2H by ~10 % (the drop-in loop is PCIe-bound).
+// dst <- the rests of records [0, n) of a span, back to back: record i's rest
+// lands at cp(i) = rest_off[i] - p0 - 36 (i + 1) (records are contiguous from
+// p0, so cp(i + 1) = cp(i) + rest_len[i]).  A workgroup takes 256 records:
+// their cp() in LDS, then 16-byte output chunks, each a shifted 16 B load
+// when the chunk lies in one rest (most of them) and bytes otherwise.
+constexpr uint32_t kPackRecs = 256;
+__global__ __launch_bounds__(256) void k_pack_rests(const uint8_t* __restrict__ u,
+                                                    const uint64_t* __restrict__ rest_off,
+                                                    const uint32_t* __restrict__ rest_len, uint64_t n, uint64_t p0,
+                                                    uint8_t* __restrict__ dst) {
+  __shared__ uint64_t cp[kPackRecs + 1];
+  const uint64_t r0 = (uint64_t)blockIdx.x * kPackRecs;
+  if (r0 >= n) return;
+  const uint32_t cnt = (uint32_t)min<uint64_t>(kPackRecs, n - r0), t = threadIdx.x;
+  if (t < cnt) {
+    const uint64_t c = rest_off[r0 + t] - p0 - 36 * (r0 + t + 1);
+    cp[t] = c;
+    if (t == cnt - 1) cp[cnt] = c + rest_len[r0 + t];
+  }
+  __syncthreads();
+  const uint64_t lo = cp[0], hi = cp[cnt];
+  const uint64_t skew = p0 + 36 * (r0 + 1);  // source = output + skew + 36 * (local record)
+  for (uint64_t c = (lo & ~15ull) + 16ull * t; c < hi; c += 16ull * blockDim.x) {
+    const uint64_t o0 = max(c, lo), o1 = min(c + 16, hi);
+    uint32_t a = 0, b = cnt - 1;  // the last record with cp <= o0
+    while (a < b) {
+      const uint32_t mid = (a + b + 1) >> 1;
+      if (cp[mid] <= o0) a = mid; else b = mid - 1;
+    }
+    if (o0 == c && o1 == c + 16 && cp[a + 1] >= c + 16) {
+      const uint64_t src = c + skew + 36ull * a;
+      const uint4* q = reinterpret_cast<const uint4*>(u + (src & ~15ull));
+      *reinterpret_cast<uint4*>(dst + c) = shift16(q[0], q[1], (uint32_t)(src & 15));
+    } else {
+      for (uint64_t o = o0; o < o1; ++o) {
+        while (cp[a + 1] <= o) ++a;
+        dst[o] = u[o + skew + 36ull * a];
+      }
+    }
+  }
 }
 
 constexpr int kWrUnroll = 4;  // 16 B chunks in flight per thread
@@ -3599,6 +3721,20 @@ hipError_t launch_readback(void* dst, const void* src, uint64_t n, hipStream_t s
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_readback, dim3(grid_for((n + 15) / 16, 256, 64)), dim3(256), 0, s,
                      static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), n);
+  return hipGetLastError();
+}
+hipError_t launch_pack_rests(const uint8_t* u, const uint64_t* rest_off, const uint32_t* rest_len, uint64_t n,
+                             uint64_t p0, uint8_t* dst, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pack_rests, dim3((unsigned)((n + kPackRecs - 1) / kPackRecs)), dim3(256), 0, s, u, rest_off,
+                     rest_len, n, p0, dst);
+  return hipGetLastError();
+}
+hipError_t launch_gather_u64(uint64_t* dst, const uint64_t* const* src, int n, hipStream_t s) {
+  if (n <= 0 || n > kGatherMax) return n == 0 ? hipSuccess : hipErrorInvalidValue;
+  U64Srcs g{};
+  for (int i = 0; i < n; ++i) g.p[i] = src[i];
+  hipLaunchKernelGGL(k_gather_u64, dim3(1), dim3(64), 0, s, dst, g, n);
   return hipGetLastError();
 }
 hipError_t launch_export_records(const Columns& src, const uint64_t* src_pos, const Columns& dst, uint64_t* dst_pos,

@@ -112,6 +112,14 @@ hipError_t launch_export_records(const Columns& src, const uint64_t* src_pos, co
                                  hipStream_t s);
 // n bytes device -> page-locked host by a kernel (no copy engine)
 hipError_t launch_readback(void* dst, const void* src, uint64_t n, hipStream_t s);
+// dst <- the rests of a span's records [0, n) back to back (record i's at
+// rest_off[i] - p0 - 36 (i + 1)); u = the stream rest_off indexes; dst holds
+// the rests' total + 16 bytes, u is readable 32 bytes past the last rest
+hipError_t launch_pack_rests(const uint8_t* u, const uint64_t* rest_off, const uint32_t* rest_len, uint64_t n,
+                             uint64_t p0, uint8_t* dst, hipStream_t s);
+// dst[i] <- *src[i], i < n <= kGatherMax (dst: page-locked host or device)
+constexpr int kGatherMax = 8;
+hipError_t launch_gather_u64(uint64_t* dst, const uint64_t* const* src, int n, hipStream_t s);
 // out[0] ^= xor of keys (if keys), out[1] += sum of voffs, out[2..3] += the
 // order-sensitive key / voff digests (see k_digest)
 hipError_t launch_digest(const int64_t* keys, const uint64_t* voffs, uint64_t n, uint64_t* out, hipStream_t s);

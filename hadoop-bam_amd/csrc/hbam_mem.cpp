@@ -13,8 +13,11 @@
 namespace hbam {
 namespace {
 
-// Blocks below kMinCached bytes are not worth caching (hipMalloc is cheap
-// for them); the caps bound what a process keeps after its splits close.
+// Every device block is cached, however small: hipFree waits for the whole
+// device, so freeing even a 40 KB candidate list behind a drop-in batch's
+// D2H held a window's locate for 13 ms.  Page-locked blocks below
+// kMinCached are not worth keeping.  The caps bound what a process keeps
+// after its splits close.
 constexpr size_t kMinCached = 1ull << 20;
 constexpr size_t kDevCap = 32ull << 30;     // of 288 GB HBM per MI355X
 constexpr size_t kPinnedCap = 8ull << 30;
@@ -75,11 +78,9 @@ int current_device() {
 hipError_t dev_alloc(void** p, size_t bytes, size_t* got) {
   if (bytes == 0) bytes = 1;
   const int dev = current_device();
-  if (bytes >= kMinCached) {
-    if (void* q = dev_cache().take(bytes, dev, got)) {
-      *p = q;
-      return hipSuccess;
-    }
+  if (void* q = dev_cache().take(bytes, dev, got)) {
+    *p = q;
+    return hipSuccess;
   }
   *got = bytes;
   return hipMalloc(p, bytes);
@@ -94,7 +95,7 @@ int device_of(void* p) {
 
 void dev_free(void* p, size_t bytes) {
   if (!p) return;
-  const int dev = bytes >= kMinCached ? device_of(p) : -1;
+  const int dev = device_of(p);
   if (dev < 0) {
     (void)hipFree(p);
     return;

@@ -24,16 +24,24 @@ constexpr int kMaxFreeStarts = 64;    // header candidates tried by a free-start
 constexpr uint64_t kOpenEnd = 1ull << 62;
 }  // namespace
 
+hipError_t create_stream(hipStream_t* s, StreamLevel level) {
+  if (level == StreamLevel::kNormal) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  int least = 0, greatest = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e != hipSuccess) return e;
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, level == StreamLevel::kHigh ? greatest : least);
+}
+
 Pipeline::Pipeline(int device) : device_(device) {
   if (hipSetDevice(device) != hipSuccess) {
     err_ = "hipSetDevice failed";
     return;
   }
-  if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&stream_b_, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&stream_t_, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&stream_copy_, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&stream_stage_, hipStreamNonBlocking) != hipSuccess)
+  if (create_stream(&stream_, StreamLevel::kNormal) != hipSuccess ||
+      create_stream(&stream_b_, StreamLevel::kNormal) != hipSuccess ||
+      create_stream(&stream_t_, StreamLevel::kNormal) != hipSuccess ||
+      create_stream(&stream_copy_, StreamLevel::kNormal) != hipSuccess ||
+      create_stream(&stream_stage_, StreamLevel::kLow) != hipSuccess)
     err_ = "hipStreamCreate failed";
   streams_.s[0] = stream_;
   streams_.s[1] = stream_b_;
@@ -143,10 +151,10 @@ int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof
 
 hipError_t Pipeline::rb(void* dst, const void* src, size_t bytes, hipStream_t s) {
   if (bytes == 0) return hipSuccess;
-  // a few bytes (counters, flags, one position) take the copy directly: a
-  // small D2H does not wait behind other streams' copies, and a kernel launch
-  // per value costs more; bigger reads (the block table) go through k_readback
-  if (bytes <= 64) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s);
+  // every read, a counter as the block table, goes through k_readback into
+  // page-locked memory: a D2H copy into pageable memory waits behind other
+  // copies on the DMA engines (a drop-in batch's columns: the 4-byte candidate
+  // count of a window's locate took 13 ms behind them)
   hipError_t e;
   if (rb_stream_ && rb_stream_ != s && (e = rb_sync(rb_stream_)) != hipSuccess) return e;
   size_t off = (rb_used_ + 15) & ~size_t(15);
@@ -294,8 +302,10 @@ int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_sta
   const uint32_t walk_cap = (uint32_t)std::min<uint64_t>(len / 26 + 16, 0x7fffffffu);
   HIPCHK(cand_.reserve(cap));
   HIPCHK(flags_.reserve(4));
-  uint32_t init[4] = {0, 0, 0xffffffffu, 0};
-  HIPCHK(hipMemcpyAsync(flags_.p, init, sizeof init, hipMemcpyHostToDevice, s));
+  // {0, 0, 0xffffffff, 0} by fill kernels: a small pageable H2D can wait
+  // behind other contexts' or the drop-in batches' copies on the DMA engines
+  HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags_.p), 0, 4, s));
+  HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags_.p + 2), -1, 1, s));
   // flags_[0] = candidate count, [1] = chain break, [2] = first big ISIZE, [3] = cut tail
   HIPCHK(launch_bgzf_scan(fbase, base_, lo, hi, cand_.p, cap, flags_.p, s));
   uint32_t count = 0;
@@ -479,7 +489,7 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
   HIPCHK(flags_.reserve(4));
   const uint32_t none = 0xffffffffu;
   uint32_t first = none;
-  HIPCHK(hipMemcpyAsync(flags_.p + 3, &none, 4, hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags_.p + 3), (int)none, 1, stream_));
   HIPCHK(launch_first_error_hout(hout_.p, 0, nb, flags_.p + 3, stream_));
   HIPCHK(rb(&first, flags_.p + 3, 4, stream_));
   HIPCHK(rb_sync(stream_));
@@ -619,7 +629,7 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
   if (!check) return kOk;  // the caller checks hout_ once all blocks are queued
   HIPCHK(flags_.reserve(4));
   const uint32_t none = 0xffffffffu;
-  HIPCHK(hipMemcpyAsync(flags_.p + 3, &none, 4, hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags_.p + 3), (int)none, 1, stream_));
   HIPCHK(launch_first_error_hout(hout_.p, b0, b1 - b0, flags_.p + 3, stream_));
   uint32_t first = none;
   HIPCHK(rb(&first, flags_.p + 3, 4, stream_));
@@ -854,7 +864,7 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
   const uint32_t nb = k1 - k0;
   // first failing block: records before it stand, later blocks are dropped
   const uint32_t none = 0xffffffffu;
-  HIPCHK(hipMemcpyAsync(flags_.p + 3, &none, 4, hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags_.p + 3), (int)none, 1, stream_));
   HIPCHK(launch_first_error_i32(errv_.p, nb, flags_.p + 3, stream_));
   uint32_t first = none;
   HIPCHK(rb(&first, flags_.p + 3, 4, stream_));

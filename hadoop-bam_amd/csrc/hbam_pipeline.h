@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
 #include <thread>
 #include <vector>
@@ -60,7 +61,14 @@ struct DevBuf {
     if (e != hipSuccess) return e;
     if (p) {
       if ((e = quiesce()) != hipSuccess) return e;
-      if ((e = hipMemcpy(q, p, n * sizeof(T), hipMemcpyDeviceToDevice)) != hipSuccess) return e;
+      // on the owner's stream: a plain hipMemcpy waits for the whole device
+      if (owner && owner->n) {
+        if ((e = hipMemcpyAsync(q, p, n * sizeof(T), hipMemcpyDeviceToDevice, owner->s[0])) != hipSuccess ||
+            (e = hipStreamSynchronize(owner->s[0])) != hipSuccess)
+          return e;
+      } else if ((e = hipMemcpy(q, p, n * sizeof(T), hipMemcpyDeviceToDevice)) != hipSuccess) {
+        return e;
+      }
       dev_free(p, n * sizeof(T));
     }
     p = static_cast<T*>(q);
@@ -70,8 +78,10 @@ struct DevBuf {
   // grow-only (contents not preserved)
   hipError_t reserve(size_t count) {
     if (count <= n && p) return hipSuccess;
+    // half again the old size at least: a count that creeps up window by
+    // window does not reallocate every time
+    const size_t c = std::max<size_t>(count ? count : 1, p ? n + n / 2 : 0);
     release();
-    size_t c = count ? count : 1;
     void* q = nullptr;
     size_t got = 0;
     hipError_t e = dev_alloc(&q, c * sizeof(T), &got);
@@ -101,6 +111,17 @@ struct StageTimes {  // milliseconds of the last decode (HIP events)
   float tables = 0;  // k_huff_tables (huff: k_inflate_huff only)
 };
 
+// Streams and hardware queues.  HIP maps streams onto GPU_MAX_HW_QUEUES
+// hardware queues (default 4) per priority level, and a context drives seven
+// streams: four decode streams, the staging copy, and the drop-in batches'
+// D2H and small reads.  On a shared queue an event or stream wait queued
+// behind a batch's D2H holds the decode kernels behind it (resident drop-in
+// loop: 32 GB/s U on shared queues, 42-44 with 8 queues).  The decode
+// streams take the normal level, the batch streams the high one and the
+// staging copy the low one, so each gets its own queue at the default.
+enum class StreamLevel { kNormal, kHigh, kLow };
+hipError_t create_stream(hipStream_t* s, StreamLevel level);
+
 // Record-level validation ([htsjdk] ValidationStringency, the
 // hadoopbam.samheaderreader.validation-stringency property).
 enum Stringency : int { kStrict = 0, kLenient = 1, kSilent = 2 };
@@ -119,12 +140,11 @@ class Pipeline {
   const StreamSet& streams() const { return streams_; }
   const std::string& error() const { return err_; }
 
-  // Device -> host reads of the host logic: reads above 64 B are queued as
-  // k_readback launches on stream s into a page-locked buffer (shader
-  // engines: a pageable D2H of the block table waited ~13 ms behind a drop-in
-  // batch's D2H on another stream); smaller ones are plain async copies.  The
-  // bytes land in dst when rb_sync(s) returns; rb_sync(s) synchronizes s in
-  // any case.
+  // Device -> host reads of the host logic, queued as k_readback launches on
+  // stream s into a page-locked buffer (shader engines: a pageable D2H of the
+  // block table waited ~13 ms behind a drop-in batch's D2H on another
+  // stream).  The bytes land in dst when rb_sync(s) returns; rb_sync(s)
+  // synchronizes s in any case.
   hipError_t rb(void* dst, const void* src, size_t bytes, hipStream_t s);
   hipError_t rb_sync(hipStream_t s);
   // dst (device) <- host bytes src [len) through the copy threads and bounce

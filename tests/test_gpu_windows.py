@@ -234,6 +234,42 @@ def test_reader_position_follows_htsjdk_read_ahead(window):
         assert e.value.code == hbam.E_STATE
 
 
+@pytest.mark.parametrize("window", [0, 1 << 16])
+def test_batch_size_changing_mid_split(window):
+    """A caller that changes max_records between calls of one split: batches
+    that are not blocks of the window's batch-major columns take the
+    per-column copies.  Every batch's data holds the rests alone, back to
+    back (rest_off[0] = 0, data_len = sum of rest_len), byte-equal to the
+    oracle's, and positions still follow the read-ahead rule."""
+    data, _ = synth.make_bam(6000, block_payload=16384)
+    s = orc.Stream(data)
+    rc, want = s.decode_all()
+    ends = [int(want["offset"][i]) + 36 + int(want["rest_len"][i]) - 1 for i in range(len(want["key"]))]
+    vo = want["voff"]
+    lo, hi = 50, 5500
+    with hbam.BamFile(data, window_bytes=window) as f:
+        v, done, sizes = int(vo[lo]), 0, [700, 333, 700, 1, 1024, 700]
+        j = 0
+        while v < int(vo[hi]):
+            r = f.decode_span(v, int(vo[hi]), max_records=sizes[j % len(sizes)])
+            j += 1
+            n = len(r["key"])
+            assert n and r["status"] == 0
+            k0 = lo + done
+            np.testing.assert_array_equal(r["key"], want["key"][k0:k0 + n])
+            np.testing.assert_array_equal(r["rest_len"], want["rest_len"][k0:k0 + n])
+            assert int(r["rest_off"][0]) == 0 and len(r["data"]) == int(r["rest_len"].astype(np.int64).sum())
+            for i in range(n):
+                off, ln = int(want["offset"][k0 + i]) + 36, int(want["rest_len"][k0 + i])
+                assert r["data"][int(r["rest_off"][i]):int(r["rest_off"][i]) + ln] == s.data[off:off + ln], (k0, i)
+            for i in sorted({0, n // 2, n - 1}):
+                ahead = min(k0 + i + 1, hi - 1)
+                assert f.reader_position(i) == _block_end(s, ends[ahead]), (k0, i)
+            done += n
+            v = r["next_voff"]
+        assert done == hi - lo and j > len(sizes)
+
+
 @pytest.mark.parametrize("g", [1, 2, 10, 4096])
 def test_write_time_index_matches_process_alignment(test_bam, g):
     """SplittingBAMIndexer(out, g).processAlignment over every record, then
