@@ -243,13 +243,6 @@ constexpr int kDistSubCap = 512;
 enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_LONG = 3, K_BAD = 4, K_SLOW = 5 };
 constexpr uint32_t kBadEntry = K_BAD << 26;
 constexpr uint32_t kLongTag = 0xF0000000u;  // build-time mark: kLongTag | (max len - root)
-#ifndef HBAM_FILL_BY_INDEX
-#define HBAM_FILL_BY_INDEX 0
-#endif
-#ifndef HBAM_FILL_CHECK
-#define HBAM_FILL_CHECK 0
-#endif
-constexpr bool kFillByIndex = HBAM_FILL_BY_INDEX != 0;  // build_table's root fill (below)
 constexpr uint32_t kKindLit = 1u << 26;  // e < kKindLit  <=>  literal entry
 
 __constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
@@ -348,20 +341,11 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
     else if (left > 0 && (mode == 2 || maxl != 1)) st = 1;
     L.bt_status = st;
   }
-  // by index (below): every entry is written by the fill, none beforehand
-  const bool by_index = kFillByIndex && sub != nullptr;
-  if (!by_index)
-    for (int i = lane; i < (1 << root); i += 64) tab[i] = kBadEntry;
+  for (int i = lane; i < (1 << root); i += 64) tab[i] = kBadEntry;
   wave_sync();
   const uint32_t st = rfl(L.bt_status);
   if (st == 1) return 1;
-  if (st == 2) {  // no codes: all-invalid table
-    if (by_index) {
-      for (int i = lane; i < (1 << root); i += 64) tab[i] = kBadEntry;
-      wave_sync();
-    }
-    return 0;
-  }
+  if (st == 2) return 0;  // no codes: all-invalid table
   const uint32_t rmask = (1u << root) - 1;
   const uint64_t ltmask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   bool any_long = false;
@@ -387,63 +371,14 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
       L.rev_of[s] = (uint16_t)rev;
       if ((int)l <= root) {
         const uint32_t e = make_entry(mode, (uint32_t)s, l);
-        if (by_index) sub[L.offs[l] + rank] = e;  // entries in canonical order (sub[] is free until below)
-        else
-          for (uint32_t i = rev; i < (1u << root); i += (1u << l)) tab[i] = e;
+        for (uint32_t i = rev; i < (1u << root); i += (1u << l)) tab[i] = e;
       } else {
-        if (!by_index) atomicMax(&tab[rev & rmask], kLongTag | (l - (uint32_t)root));  // widest sub-table under the prefix
+        atomicMax(&tab[rev & rmask], kLongTag | (l - (uint32_t)root));  // widest sub-table under the prefix
         any_long = true;
       }
     }
   }
   wave_sync();
-  if (by_index) {
-    // Root fill by table index, the same work for every lane (the per-symbol
-    // fill loops 2^(root - l) times, and the lane of the shortest code sets
-    // the wave's pace).  Canonical codes of length l <= root cover the
-    // left-aligned values [A_l, B_l), A_l = firstc[l] << (root - l),
-    // B_l = (firstc[l] + cnt[l]) << (root - l), contiguous in l: value v
-    // belongs to the code of rank (v - A_l) >> (root - l) of its length, and
-    // values >= B_root to no code of length <= root (a sub-table prefix or,
-    // in an incomplete code, nothing).  Lane j takes values [j K, j K + K),
-    // K = 2^root / 64; table index = v bit-reversed.
-    const uint32_t K = (1u << root) >> 6, v0 = lane * K;
-    for (uint32_t v = v0; v < v0 + K; ++v) {
-      uint32_t e = kBadEntry;
-      for (int l = 1; l <= root; ++l) {
-        const uint32_t a = L.firstc[l] << (root - l), c = cnt[l] << (root - l);
-        if (v - a < c) e = sub[L.offs[l] + ((v - a) >> (root - l))];
-      }
-      tab[__brev(v) >> (32 - root)] = e;
-    }
-    wave_sync();
-    if (__ballot(any_long) != 0) {
-      for (int s2 = lane; s2 < nsym; s2 += 64) {
-        const uint32_t l = lens[s2];
-        if ((int)l > root) atomicMax(&tab[L.rev_of[s2] & rmask], kLongTag | (l - (uint32_t)root));
-      }
-      wave_sync();
-    }
-#if HBAM_FILL_CHECK
-    // check build: every entry against the per-symbol fill
-    uint32_t bad = 0;
-    for (int s2 = 0; s2 < nsym; ++s2) {
-      const uint32_t l = lens[s2];
-      if (l == 0 || (int)l > root) continue;
-      const uint32_t e = make_entry(mode, (uint32_t)s2, l);
-      for (uint32_t i = L.rev_of[s2] + (lane << l); i < (1u << root); i += (64u << l)) bad += tab[i] != e;
-    }
-    for (uint32_t i = lane; i < (1u << root); i += 64) {
-      const uint32_t v = __brev(i) >> (32 - root);
-      const uint32_t end = (L.firstc[root] + cnt[root]);
-      if (v >= end && tab[i] != kBadEntry && tab[i] < kLongTag) bad++;
-    }
-    if (__ballot(bad != 0)) {
-      if (lane == 0) printf("hbam fill check: mode %d root %d nsym %d: mismatching entries\n", mode, root, nsym);
-      return 1;
-    }
-#endif
-  }
   if (__ballot(any_long) == 0) return 0;
   // sub-table bases: exclusive scan of the sub-table sizes in root-index order
   uint32_t used = 0;
