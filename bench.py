@@ -689,10 +689,12 @@ def run_c2(D, args, steps, warmup, extras):
                     out["roofline"]["traffic_error"] = repr(e)
             if not args.no_extra:
                 extra = {}
-                for name, fn in (("c2_from_pinned_host", lambda: pinned_host_leg(path, n_all)),
-                                 ("dropin_end_to_end", lambda: dropin_leg(path, first, n_all)),
+                # (the pinned-host leg runs last of all, in main())
+                for name, fn in (("dropin_end_to_end", lambda: dropin_leg(path, first, n_all)),
                                  ("write_path", lambda: write_legs(path, size, u_file)),
                                  ("c4_long_reads", long_read_leg)):
+                    if args.extras is not None and name not in args.extras.split(","):
+                        continue
                     t = time.time()
                     try:
                         extra[name] = fn()
@@ -729,6 +731,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the in-session rocprofv3 PMC passes")
     ap.add_argument("--no-extra", action="store_true", help="skip every side leg (drop-in, C3/C5, C4, write)")
+    ap.add_argument("--extras", default=None,
+                    help="comma list of the C2 side legs to run (dropin_end_to_end, write_path, "
+                         "c4_long_reads, c2_from_pinned_host); default all")
     ap.add_argument("--serial", action="store_true",
                     help="every step in the measurement launch order (one stream, events per launch): the "
                          "command profiles/collect.sh traces, so rocprofv3's per-kernel averages are the "
@@ -761,6 +766,22 @@ def main():
             log(f"[extra] c3_c5_60GB {time.time() - t:.1f}s")
             if D.rank == 0:
                 line.setdefault("extra", {})["c3_c5_60GB"] = c3
+        if D.world == 1 and not args.no_extra and (args.extras is None or "c2_from_pinned_host" in args.extras):
+            # last of all: after hbam_gpu_run_streamed has run in a process, the
+            # drop-in loop of a later context ran at ~24 instead of ~40 GB/s U
+            # (scripts/dropin_probe2.py --steps)
+            t = time.time()
+            path = os.path.join(scratch_dir(), f"hbam_pinned_{D.tag}.bam")
+            try:
+                size, _ = build_shared_bam(path, 0, 1, args.records, D.all_gather, D.barrier)
+                ph = pinned_host_leg(path, args.records)
+            except Exception as e:
+                ph = {"error": repr(e)}
+            finally:
+                if os.path.exists(path):
+                    os.unlink(path)
+            log(f"[extra] c2_from_pinned_host {time.time() - t:.1f}s")
+            line.setdefault("extra", {})["c2_from_pinned_host"] = ph
     else:
         r = run_c3(D, args.c3_gb, args.steps, args.warmup, host_leg=False)
         if D.rank == 0:

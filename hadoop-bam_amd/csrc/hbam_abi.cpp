@@ -7,7 +7,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -195,6 +197,16 @@ int decode_device(BamFile& f, uint64_t vstart, uint64_t vend, int32_t flags, hba
   if (rc != HBAM_OK) st->status = rc;
   return rc != HBAM_OK ? rc : st->status;
 }
+// page-locked blocks handed out by hbam_host_alloc and their sizes (pinned_free needs them)
+std::mutex& host_alloc_mu() {
+  static std::mutex* m = new std::mutex();
+  return *m;
+}
+std::map<void*, size_t>& host_allocs() {
+  static std::map<void*, size_t>* m = new std::map<void*, size_t>();
+  return *m;
+}
+
 }  // namespace
 
 extern "C" {
@@ -807,13 +819,26 @@ int hbam_gpu_run_streamed(hbam_gpu* g, const void* data, uint64_t len, uint64_t 
 }
 
 void* hbam_host_alloc(uint64_t bytes) {
+  // the library's page-locked blocks: on the current device's NUMA node (hbam_mem.cpp)
   void* p = nullptr;
-  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  size_t got = 0;
+  if (hbam::pinned_alloc(&p, bytes ? bytes : 1, &got) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(host_alloc_mu());
+  host_allocs()[p] = got;
   return p;
 }
 
 void hbam_host_free(void* p) {
-  if (p) (void)hipHostFree(p);
+  if (!p) return;
+  size_t bytes = 0;
+  {
+    std::lock_guard<std::mutex> lk(host_alloc_mu());
+    auto it = host_allocs().find(p);
+    if (it == host_allocs().end()) return;
+    bytes = it->second;
+    host_allocs().erase(it);
+  }
+  hbam::pinned_free(p, bytes);
 }
 
 int hbam_gpu_reload(hbam_gpu* g, const void* data, uint64_t len, int32_t pinned, float* ms) {

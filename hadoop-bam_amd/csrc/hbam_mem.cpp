@@ -2,8 +2,15 @@
 #include "hbam_mem.h"
 
 #include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <cstdlib>
 
 #include <algorithm>
+#include <cctype>
+#include <cstdio>
+#include <string>
 #include <map>
 #include <mutex>
 #include <set>
@@ -20,6 +27,11 @@ namespace {
 // after its splits close.
 constexpr size_t kMinCached = 1ull << 20;
 constexpr size_t kDevCap = 32ull << 30;     // of 288 GB HBM per MI355X
+// Blocks below kMinCached have a cache of their own: once closed contexts'
+// window buffers fill kDevCap, a small block freed by a running decode would
+// otherwise go to hipFree (the drop-in loop after the bench's pinned-host leg
+// ran at 23 GB/s U instead of 39).
+constexpr size_t kDevSmallCap = 256ull << 20;
 constexpr size_t kPinnedCap = 8ull << 30;
 
 struct Cache {
@@ -63,6 +75,10 @@ Cache& dev_cache() {
   static Cache* c = new Cache();
   return *c;
 }
+Cache& dev_small_cache() {
+  static Cache* c = new Cache();
+  return *c;
+}
 Cache& pinned_cache() {
   static Cache* c = new Cache();
   return *c;
@@ -78,7 +94,7 @@ int current_device() {
 hipError_t dev_alloc(void** p, size_t bytes, size_t* got) {
   if (bytes == 0) bytes = 1;
   const int dev = current_device();
-  if (void* q = dev_cache().take(bytes, dev, got)) {
+  if (void* q = (bytes < kMinCached ? dev_small_cache() : dev_cache()).take(bytes, dev, got)) {
     *p = q;
     return hipSuccess;
   }
@@ -101,7 +117,9 @@ void dev_free(void* p, size_t bytes) {
     return;
   }
   // the owner has drained its streams (DevBuf::release): no device-wide wait
-  if (!dev_cache().put(p, bytes, dev, kDevCap)) (void)hipFree(p);
+  const bool kept = bytes < kMinCached ? dev_small_cache().put(p, bytes, dev, kDevSmallCap)
+                                       : dev_cache().put(p, bytes, dev, kDevCap);
+  if (!kept) (void)hipFree(p);
 }
 
 namespace {
@@ -121,10 +139,44 @@ std::set<void*>& registered() {  // blocks from the map + register path
   return *s;
 }
 
+// The NUMA node of the current device (-1: unknown).  A host has several
+// (the MI355X box: 2 sockets, its GPU on node 1), and a page-locked buffer
+// first-touched by threads on the other socket crosses the socket link on
+// every DMA: the drop-in batches' D2H ran at ~30 GB/s instead of 56 when the
+// batch slots landed there.
+int device_numa_node() {
+  static std::mutex mu;
+  static std::map<int, int> known;
+  const int dev = current_device();
+  if (dev < 0) return -1;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = known.find(dev);
+  if (it != known.end()) return it->second;
+  int node = -1;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, dev) == hipSuccess) {
+    for (char* c = bus; *c; ++c) *c = (char)tolower((unsigned char)*c);
+    const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/numa_node";
+    if (FILE* f = fopen(path.c_str(), "r")) {
+      if (fscanf(f, "%d", &node) != 1) node = -1;
+      fclose(f);
+    }
+  }
+  known[dev] = node;
+  return node;
+}
+
 void* map_and_touch(size_t bytes) {
   void* q = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
   if (q == MAP_FAILED) return nullptr;
   (void)madvise(q, bytes, MADV_HUGEPAGE);
+  // pages on the device's node whichever CPUs touch them (preferred: another
+  // node when that one is full)
+  const int node = device_numa_node();
+  if (node >= 0 && node < 64) {
+    const unsigned long mask = 1ul << node;
+    (void)syscall(SYS_mbind, q, bytes, 1 /* MPOL_PREFERRED */, &mask, 64ul, 0u);
+  }
   const size_t nt = std::min<size_t>(8, std::max<size_t>(1, bytes / (32ull << 20)));
   const size_t per = (bytes / nt + kHuge - 1) & ~(kHuge - 1);
   std::vector<std::thread> th;
@@ -193,6 +245,11 @@ void pinned_free(void* p, size_t bytes) {
 size_t release_cached() {
   std::multimap<size_t, std::pair<void*, int>> d, h;
   size_t n = dev_cache().drain(&d) + pinned_cache().drain(&h);
+  {
+    std::multimap<size_t, std::pair<void*, int>> small;
+    n += dev_small_cache().drain(&small);
+    d.insert(small.begin(), small.end());
+  }
   const int cur = current_device();
   for (auto& b : d) {
     (void)hipSetDevice(b.second.second);

@@ -1,11 +1,14 @@
 """Per-batch timing of the drop-in call (developer probe): hbam_decode_span in 1M-record
 batches from the mapped file and from a resident copy, every batch timed.
-usage: python scripts/dropin_probe2.py [records]"""
+usage: python scripts/dropin_probe2.py [records] [--torch] [--pinned]"""
 import os
 import sys
 import time
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "hadoop-bam_amd"))
+if "--torch" in sys.argv:
+    import torch  # noqa: F401,E402  (before hbam: one HIP runtime)
+import numpy as np  # noqa: E402
 import hbam  # noqa: E402
 from hbam import synth  # noqa: E402
 
@@ -48,12 +51,60 @@ def batches(f, first, nrec):
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+    if "--torch" in sys.argv:  # as bench.py: torch first, its runtime initialised
+        import torch
+        torch.cuda.init()
+        torch.empty(1, device="cuda")
     data, info = synth.make_bam(n, as_numpy=True)
     path = "/dev/shm/hbam_dropin_probe2.bam"
     data.tofile(path)
     del data
     try:
-        for rep in range(2):
+        steps = ["none", "gpu_load", "pinned_buffer", "run_streamed"] if "--pinned" in sys.argv else ["none", "none"]
+        if "--steps" in sys.argv:
+            steps = sys.argv[sys.argv.index("--steps") + 1].split(",")
+        for rep, what in enumerate(steps):
+            if what == "gpu_load":  # a device-resident context opened, loaded and closed
+                g = hbam.Gpu(0)
+                try:
+                    g.load(np.fromfile(path, np.uint8))
+                finally:
+                    g.close()
+            elif what == "pinned_buffer":  # a page-locked buffer of the file, filled and freed
+                raw = np.fromfile(path, np.uint8)
+                with hbam.PinnedBuffer(raw.nbytes) as buf:
+                    buf.array[:] = raw
+                del raw
+            elif what == "run_streamed":  # bench.py's pinned-host leg
+                g = hbam.Gpu(0)
+                try:
+                    raw = np.fromfile(path, np.uint8)
+                    with hbam.PinnedBuffer(raw.nbytes) as buf:
+                        buf.array[:] = raw
+                        g.load(raw)
+                        for _ in range(4):
+                            g.run_streamed(buf.ptr, buf.nbytes, 256 << 20)
+                finally:
+                    g.close()
+                del raw
+            elif what in ("run_resident", "reload_pinned", "streamed_one_piece"):
+                g = hbam.Gpu(0)
+                try:
+                    raw = np.fromfile(path, np.uint8)
+                    with hbam.PinnedBuffer(raw.nbytes) as buf:
+                        buf.array[:] = raw
+                        g.load(raw)
+                        for _ in range(4):
+                            if what == "run_resident":
+                                g.run()
+                            elif what == "reload_pinned":
+                                g.reload(buf.ptr, buf.nbytes, pinned=True)
+                            else:
+                                g.run_streamed(buf.ptr, buf.nbytes, buf.nbytes)
+                finally:
+                    g.close()
+                del raw
+            print("after", what, flush=True)
             with hbam.BamFile(path=path) as f:
                 first = f.header()["first_record_voff"]
                 t = time.perf_counter()
