@@ -82,6 +82,7 @@ int hip_err(hipError_t e, const char* what, std::string* err) {
 }  // namespace
 
 SpanCursor::~SpanCursor() {
+  join_prealloc();
   if (device_ < 0) return;
   (void)hipSetDevice(device_);
   (void)drain();
@@ -205,7 +206,36 @@ int SpanCursor::decode_window(BamFile& f, Carry from, bool cont, uint64_t m, Win
   return kOk;
 }
 
+// First open of a split with batches of m records: both host slots are
+// allocated on a helper thread while the first window decodes (mapping and
+// pinning 2 x ~0.45 GB for 1 M-record batches took ~35 ms of the first
+// batch).  The estimate is the columns plus 400 B of rests per record
+// (150 bp reads: ~304); a bigger batch reallocates in issue() as before.
+void SpanCursor::start_prealloc(uint64_t m) {
+  join_prealloc();
+  const size_t est = ColLayout(m, false).bytes + 400 * m + 64;
+  if (slot_[0].cap >= est && slot_[1].cap >= est) return;
+  const int dev = device_;
+  prealloc_ = std::thread([this, est, dev]() {
+    if (hipSetDevice(dev) != hipSuccess) return;  // (the NUMA node of the allocation follows the device)
+    for (auto& s : slot_) {
+      if (s.cap >= est) continue;
+      void* q = nullptr;
+      size_t got = 0;
+      if (hbam::pinned_alloc(&q, est + est / 8, &got) != hipSuccess) return;  // issue() tries again
+      if (s.mem) hbam::pinned_free(s.mem, s.cap);
+      s.mem = static_cast<uint8_t*>(q);
+      s.cap = got;
+    }
+  });
+}
+
+void SpanCursor::join_prealloc() {
+  if (prealloc_.joinable()) prealloc_.join();
+}
+
 int SpanCursor::issue(const Window& w, uint64_t k, uint64_t m, Slot* s, std::string* err) {
+  join_prealloc();
   // batch boundaries: record k's start, the batch end, the read-ahead
   // record's end (slot positions) and the next record's voff
   const uint64_t e = k + m;
@@ -286,6 +316,7 @@ int SpanCursor::next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t 
   if (!cont) {  // a seek to the split start (or anywhere in it)
     reset();
     vend_ = vend;
+    start_prealloc(max_records);
     rc = decode_window(f, Carry{vstart >> 16, vstart & 0xffff}, false, max_records, &win_[0], err);
     if (rc != kOk) return rc;
     nwin_ = 1;

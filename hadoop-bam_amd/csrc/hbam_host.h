@@ -27,6 +27,7 @@
 #include <memory>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "hbam_pipeline.h"
@@ -410,6 +411,11 @@ class SpanCursor {
   uint64_t front_ = 0, nwin_ = 0;  // window ids: front_ = the one being handed out; nwin_ decoded so far
   uint64_t k_ = 0;                 // next record of the front window
   Slot slot_[2];
+  // the first batches' page-locked slots, mapped and pinned on a helper
+  // thread while the first window decodes (joined before a slot is used)
+  std::thread prealloc_;
+  void start_prealloc(uint64_t m);
+  void join_prealloc();
   int cur_ = -1;                   // slot of the last batch handed out
   uint64_t* small_ = nullptr;      // page-locked scratch for the boundary reads
   // the last batch: where its records came from (positions / encode)
