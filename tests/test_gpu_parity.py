@@ -213,7 +213,7 @@ def test_record_errors_match_oracle(rec, off, val, code):
 
 
 def test_c2_full_size_vs_oracle():
-    """BASELINE config C2 at full size (10 M records, 0.93 GB BGZF): every key
+    """BASELINE config C2 at full size (10 M records, 1.41 GB BGZF): every key
     and voff of the device pipeline and the .splitting-bai (g = 4096) through
     the SplittingBAMIndexer entry point, bit-exact against the oracle."""
     data, info = synth.make_bam(10_000_000, as_numpy=True)
