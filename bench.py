@@ -677,6 +677,18 @@ def run_c2(D, args, steps, warmup, extras):
                                                            and full["voff_digest"] == vd)
                 except Exception as e:  # reported, never substituted for the GPU number
                     out["cpu_baseline"] = {"error": repr(e)}
+            extra = {}
+            want = (lambda name: not args.no_extra and (args.extras is None or name in args.extras.split(",")))
+            if want("dropin_end_to_end"):
+                # before the PMC child runs: after them (as after hbam_gpu_run_streamed,
+                # main()), the drop-in loop of this process ran at 24 instead of
+                # 39-40 GB/s U on first open (open issue)
+                t = time.time()
+                try:
+                    extra["dropin_end_to_end"] = dropin_leg(path, first, n_all)
+                except Exception as e:
+                    extra["dropin_end_to_end"] = {"error": repr(e)}
+                log(f"[extra] dropin_end_to_end {time.time() - t:.1f}s")
             if not args.no_pmc:
                 try:
                     tr = pmc_traffic(path, vs, ve, out["roofline"]["kernel"])
@@ -688,12 +700,10 @@ def run_c2(D, args, steps, warmup, extras):
                 except Exception as e:
                     out["roofline"]["traffic_error"] = repr(e)
             if not args.no_extra:
-                extra = {}
                 # (the pinned-host leg runs last of all, in main())
-                for name, fn in (("dropin_end_to_end", lambda: dropin_leg(path, first, n_all)),
-                                 ("write_path", lambda: write_legs(path, size, u_file)),
+                for name, fn in (("write_path", lambda: write_legs(path, size, u_file)),
                                  ("c4_long_reads", long_read_leg)):
-                    if args.extras is not None and name not in args.extras.split(","):
+                    if not want(name):
                         continue
                     t = time.time()
                     try:
