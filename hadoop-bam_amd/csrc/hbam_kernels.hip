@@ -56,23 +56,43 @@ __device__ __forceinline__ uint64_t ldu64(const uint8_t* base, uint64_t off) {
 // exact framing htsjdk writes and requires (XLEN==6), plus the BC subfield id
 // for selectivity.  Candidates are appended unordered, sorted, then the BSIZE
 // chain is verified; any break falls back to the serial walk (bgzf_walk).
-__global__ void k_bgzf_scan(const uint8_t* __restrict__ buf, uint64_t len, uint64_t base, uint64_t from,
-                            uint64_t* __restrict__ cand, uint32_t cap, uint32_t* __restrict__ count) {
+__global__ __launch_bounds__(256) void k_bgzf_scan(const uint8_t* __restrict__ buf, uint64_t len, uint64_t base,
+                                                   uint64_t from, uint64_t* __restrict__ cand, uint32_t cap,
+                                                   uint32_t* __restrict__ count) {
   // buf = first byte of the loaded range (16 B aligned, zero padded past
-  // len); 64 positions per thread from four 16 B loads + the next word.  A
-  // word without a 0x1f byte (nearly all of them) costs three VALU
-  // operations; the rare 0x1f bytes get the full header test.  Candidates
-  // are reported in file coordinates (base + offset).
-  const uint64_t nc = (len + 63) / 64;
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nc;
-       t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint4* q = reinterpret_cast<const uint4*>(buf + 64 * t);
-    const uint4 v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3];
-    const uint32_t w16 = *reinterpret_cast<const uint32_t*>(buf + 64 * t + 64);
-    const uint32_t w[17] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
-                            v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w, w16};
+  // len).  Lane i of a wave step reads 16 B chunk c = step + i: one coalesced
+  // 1 KiB load per wave (64 B per lane, as before, strided the wave's loads
+  // 64 B apart and ran at 2.2 TB/s).  The 4 bytes after a chunk, which a
+  // header starting in its last 3 bytes needs, come from the next lane's
+  // chunk (a lane shuffle; the wave's last lane loads them).  A word without
+  // a 0x1f byte (nearly all of them) costs three VALU operations; the rare
+  // 0x1f bytes get the full header test.  Candidates are reported in file
+  // coordinates (base + offset).
+  // Four such wave steps per iteration (4 KiB per wave), their loads issued
+  // together: one load in flight per wave left the scan latency-bound.
+  constexpr int kU = 4;
+  const uint64_t nc = (len + 15) / 16;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * kU;
+  const uint32_t lane = lane_id();
+  const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * kU;
+  for (uint64_t c0 = wave0; c0 < nc; c0 += stride) {
+    uint4 vv[kU];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int u = 0; u < kU; ++u) {
+      const uint64_t c = c0 + 64 * u + lane;
+      vv[u] = c < nc ? reinterpret_cast<const uint4*>(buf)[c] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+    const uint64_t c = c0 + 64 * u + lane;  // the wave stays converged through the shuffle
+    const uint4 v = vv[u];
+    uint32_t nx = (uint32_t)__shfl_down((int)v.x, 1, 64);
+    // the wave's last lane: the next step's first chunk (lane 0), or memory
+    const uint32_t next0 = u + 1 < kU ? (uint32_t)__shfl((int)vv[u + 1 < kU ? u + 1 : u].x, 0, 64) : 0u;
+    if (lane == 63) nx = u + 1 < kU ? next0 : (c < nc ? *reinterpret_cast<const uint32_t*>(buf + 16 * c + 16) : 0u);
+    const uint32_t w[5] = {v.x, v.y, v.z, v.w, nx};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
       const uint32_t x = w[k] ^ 0x1f1f1f1fu;
       uint32_t hz = (x - 0x01010101u) & ~x & 0x80808080u;  // a byte of w[k] may be 0x1f (superset)
       while (hz) {
@@ -80,7 +100,7 @@ __global__ void k_bgzf_scan(const uint8_t* __restrict__ buf, uint64_t len, uint6
         hz &= hz - 1;
         const uint32_t magic = __builtin_amdgcn_alignbyte(w[k + 1], w[k], byte);
         if (magic != 0x04088b1fu) continue;
-        const uint64_t p = 64 * t + 4 * k + byte;
+        const uint64_t p = 16 * c + 4 * k + byte;
         if (p + 18 > len || base + p < from) continue;
         const uint32_t xlen = ldu32(buf, p + 10) & 0xffffu;
         const uint32_t sub = ldu32(buf, p + 12);
@@ -88,6 +108,7 @@ __global__ void k_bgzf_scan(const uint8_t* __restrict__ buf, uint64_t len, uint6
         const uint32_t i = atomicAdd(count, 1u);
         if (i < cap) cand[i] = base + p;
       }
+    }
     }
   }
 }
@@ -514,12 +535,16 @@ struct __attribute__((packed, aligned(4))) Tok4 {
 //   LD_SYNC stops with EV_MERGE (mj = index) when it reaches one of them;
 //   LD_EMIT writes tokens to tok[0..nt) and applies the output-space rules with
 //           the output position of the first token = out0.
-template <int MODE>
+//   KEEP (LD_SPEC / LD_SYNC): also writes the tokens to tok[0..min(nt, isize))
+//           (isize = the scratch capacity; no output-space rules): emit then
+//           copies them instead of decoding the slice a third time.
+template <int MODE, bool KEEP = false>
 __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t* __restrict__ W, uint32_t a,
                                                 uint32_t stop, uint32_t E, uint32_t& x, uint32_t& nt, uint32_t& nb,
                                                 MergePts& mp, uint32_t& mj, uint32_t* __restrict__ tok,
                                                 uint32_t out0, uint32_t isize) {
   constexpr bool EMIT = MODE == LD_EMIT;
+  constexpr bool STORE = EMIT || KEEP;
   uint32_t wd, cnt, nx;
   uint64_t buf;
 #define LSEEK(p)                                                    \
@@ -532,7 +557,7 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
   } while (0)
   LSEEK(a);
   uint32_t pos = a, ev = EV_STOP;
-  uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, fill = 0;  // EMIT: pending tokens
+  uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, fill = 0;  // EMIT / KEEP: pending tokens
   nt = 0;
   nb = 0;
   if (MODE == LD_SPEC) {
@@ -556,13 +581,13 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
   } while (0)
 #define LCOMMIT(t_, len_)                                                                   \
   do {                                                                                      \
-    if (EMIT) {                                                                             \
+    if (STORE) {                                                                            \
       q0 = fill == 0 ? (t_) : q0;                                                           \
       q1 = fill == 1 ? (t_) : q1;                                                           \
       q2 = fill == 2 ? (t_) : q2;                                                           \
       q3 = (t_);                                                                            \
       if (++fill == 4) {                                                                    \
-        *reinterpret_cast<Tok4*>(tok + nt - 3) = Tok4{q0, q1, q2, q3};                      \
+        if (!KEEP || nt < isize) *reinterpret_cast<Tok4*>(tok + nt - 3) = Tok4{q0, q1, q2, q3}; \
         fill = 0;                                                                           \
       }                                                                                     \
     }                                                                                       \
@@ -697,7 +722,7 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
 #undef LREFILL
 #undef LCONSUME
 #undef LCOMMIT
-  if (EMIT && fill) {  // the 1..3 tokens not yet stored
+  if (STORE && fill && (!KEEP || nt <= isize)) {  // the 1..3 tokens not yet stored
     uint32_t* p = tok + nt - fill;
     p[0] = q0;
     if (fill > 1) p[1] = q1;
@@ -1154,14 +1179,25 @@ constexpr uint32_t kHuffCtlBytes = (sizeof(HuffCtl) + 15) & ~15u;
 constexpr uint32_t kHuffStaticBytes = kHuffLdsBytes + kHuffCtlBytes;
 
 constexpr int kHuffWavesPerSimd = 4;  // VGPR cap 128 (no spills); LDS admits 4 staged workgroups per CU
-template <bool STAGE>
+// Kept tokens (KEEP): each lane's spec and sync walks write their tokens to
+// two scratch ranges of kKeepCap tokens (HBM, by block of the launch and
+// lane), and emit copies them (plus the output-space checks) instead of
+// decoding the slice a third time; a lane whose walk overflowed a range, or
+// whose copy meets an output-space event, decodes as before.
+#ifndef HBAM_KEEP_TOKENS
+#define HBAM_KEEP_TOKENS 0
+#endif
+constexpr bool kKeepTokens = HBAM_KEEP_TOKENS != 0;
+constexpr uint32_t kKeepCap = 80;  // tokens per range (a slice holds ~39 on C2)
+template <bool STAGE, bool KEEP>
 __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huff(const uint8_t* __restrict__ file,
                                                                const BlockInfo* __restrict__ blocks, uint32_t b0,
                                                                uint64_t chunk_ustart, uint32_t* __restrict__ tokens,
                                                                HuffOut* __restrict__ hout,
                                                                const uint8_t* __restrict__ tables,
                                                                const HuffTableInfo* __restrict__ tinfo,
-                                                               uint32_t round, uint32_t defer) {
+                                                               uint32_t round, uint32_t defer,
+                                                               uint32_t* __restrict__ keep) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   HuffLds& L = *reinterpret_cast<HuffLds*>(smem);
   HuffCtl& C = *reinterpret_cast<HuffCtl*>(smem + kHuffLdsBytes);
@@ -1438,7 +1474,10 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
     const uint32_t stop = tid == kHuffThreads - 1 ? Bend : min(B0 + (tid + 1) * S, Bend);
     MergePts mp;
     uint32_t mj = 0, x, nt, nb;
-    uint32_t ev = lane_decode<LD_SPEC>(L, W, a, stop, E, x, nt, nb, mp, mj, nullptr, 0, 0);
+    uint32_t* const kspec = KEEP ? keep + ((uint64_t)blockIdx.x * kHuffThreads + tid) * (2 * kKeepCap) : nullptr;
+    uint32_t* const ksync = KEEP ? kspec + kKeepCap : nullptr;
+    uint32_t kmode = 0, kfirst = 0, ksplit = 0;  // tokens: 0 spec; 1 sync; 2 sync[0, kfirst) + spec[ksplit, snt)
+    uint32_t ev = lane_decode<LD_SPEC, KEEP>(L, W, a, stop, E, x, nt, nb, mp, mj, kspec, 0, kKeepCap);
     const uint32_t sx = x, snt = nt, snb = nb, sev = ev;
     for (;;) {  // sync: restart each slice from its predecessor's exit
       if (lane == 63) {
@@ -1456,19 +1495,23 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
       if (need) {
         a = px;
         uint32_t rx, rnt, rnb;
-        const uint32_t rev = lane_decode<LD_SYNC>(L, W, a, stop, E, rx, rnt, rnb, mp, mj, nullptr, 0, 0);
+        const uint32_t rev = lane_decode<LD_SYNC, KEEP>(L, W, a, stop, E, rx, rnt, rnb, mp, mj, ksync, 0, kKeepCap);
         if (rev == EV_MERGE) {  // shares the speculative walk from boundary mj on
           const uint32_t bj = mj == 0 ? mp.b0 : mj == 1 ? mp.b1 : mj == 2 ? mp.b2 : mp.b3;
           x = sx;
           ev = sev;
           nt = rnt + snt - (kMergeFirst << mj);
           nb = rnb + snb - bj;
+          kmode = 2;
+          ksplit = kMergeFirst << mj;
         } else {
           x = rx;
           ev = rev;
           nt = rnt;
           nb = rnb;
+          kmode = 1;
         }
+        kfirst = rnt;
       }
     }
     const uint32_t lend0 = wg_min(ev != EV_STOP ? tid : 0xffffffffu, C.red);
@@ -1477,7 +1520,36 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
     uint32_t toff, boff;
     wg_excl_scan2(valid ? nt : 0u, valid ? nb : 0u, C.red, toff, boff);
     uint32_t x3 = a, nt3 = 0, nb3 = 0, ev3 = EV_STOP;
-    if (valid)
+    bool copied = false;
+    if (KEEP && valid && (kmode == 1 || snt <= kKeepCap) && (kmode == 0 || kfirst <= kKeepCap)) {
+      // emit as a copy of the kept tokens, with emit's output-space checks:
+      // output full before a token, or a distance reaching before the block
+      // start, leaves the lane to the decoding emit (which reports the event)
+      uint32_t* const dst = tok_out + tok0 + toff;
+      const uint32_t o = out0 + boff, n1 = kmode == 0 ? 0u : kfirst;
+      const uint32_t* const tail = kspec + (kmode == 2 ? ksplit : 0u) - n1;
+      uint32_t done = 0;
+      bool ok = true;
+      for (uint32_t i = 0; i < nt; ++i) {
+        const uint32_t t = i < n1 ? ksync[i] : tail[i];
+        if (o + done >= isize) { ok = false; break; }
+        const bool m = (t >> 31) != 0;
+        if (m && ((t >> 16) & 0x7fffu) + 1 > o + done) { ok = false; break; }
+        dst[i] = t;
+        done += m ? (t & 0xffffu) : ((t >> 24) & 3u);
+      }
+      // a walk that ended on an event before `stop` tried one more symbol:
+      // emit checks the output first (a full block reports FULLX / FULLO there)
+      if (ev != EV_STOP && o + done >= isize) ok = false;
+      if (ok) {
+        copied = true;
+        x3 = x;
+        nt3 = nt;
+        nb3 = nb;
+        ev3 = ev;
+      }
+    }
+    if (valid && !copied)
       ev3 = lane_decode<LD_EMIT>(L, W, a, stop, E, x3, nt3, nb3, mp, mj, tok_out + tok0 + toff, out0 + boff, isize);
     const uint32_t m3 = wg_min((valid && ev3 != EV_STOP) ? tid : 0xffffffffu, C.red);
     const uint32_t f = m3 != 0xffffffffu ? m3 : lend;
@@ -3425,9 +3497,9 @@ hipError_t launch_bgzf_scan(const uint8_t* file, uint64_t buf_base, uint64_t lo,
   // allocated); candidates below lo are dropped
   (void)buf_base;
   const uint64_t a = lo & ~15ull;
-  const uint64_t nc = (hi - a + 63) / 64;  // 64 B per thread and step
-  hipLaunchKernelGGL(k_bgzf_scan, dim3(grid_for(nc, 256, 8192)), dim3(256), 0, s, file + a, hi - a, a, lo, cand,
-                     cap, count);
+  const uint64_t nc = (hi - a + 15) / 16;  // 16 B per lane and step, 4 steps per iteration
+  hipLaunchKernelGGL(k_bgzf_scan, dim3(grid_for((nc + 3) / 4, 256, 8192)), dim3(256), 0, s, file + a, hi - a, a, lo,
+                     cand, cap, count);
   return hipGetLastError();
 }
 hipError_t launch_bgzf_verify(const uint8_t* file, uint64_t lo, uint64_t hi, const uint64_t* cand, uint32_t n,
@@ -3472,25 +3544,27 @@ hipError_t launch_huff_tables(const uint8_t* file, const BlockInfo* blocks, uint
 }
 // phase A proper; the chunk's tables must be built (launch_huff_tables).
 // max_stage = largest staged span of the chunk's blocks (huff_stage_bytes)
+uint64_t huff_keep_words(uint32_t nb) { return kKeepTokens ? (uint64_t)nb * kHuffThreads * 2 * kKeepCap : 0; }
 hipError_t launch_inflate_huff_prebuilt(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
                                         uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
                                         const uint8_t* tables, const HuffTableInfo* tinfo, uint32_t round,
-                                        uint32_t defer, hipStream_t s) {
+                                        uint32_t defer, uint32_t* keep, hipStream_t s) {
   if (nb == 0) return hipSuccess;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_inflate_huff<true>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_inflate_huff<true, kKeepTokens>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
+  if (kKeepTokens && !keep) return hipErrorInvalidValue;  // huff_keep_words(nb) words of scratch
   const uint32_t staged_lds = kHuffStaticBytes + ((max_stage + 15) & ~15u);
   if (staged_lds <= kHuffStageMaxLds)
-    hipLaunchKernelGGL(k_inflate_huff<true>, dim3(nb), dim3(kHuffThreads), staged_lds, s, file, blocks, b0,
-                       chunk_ustart, tokens, hout, tables, tinfo, round, defer);
+    hipLaunchKernelGGL((k_inflate_huff<true, kKeepTokens>), dim3(nb), dim3(kHuffThreads), staged_lds, s, file,
+                       blocks, b0, chunk_ustart, tokens, hout, tables, tinfo, round, defer, keep);
   else
-    hipLaunchKernelGGL(k_inflate_huff<false>, dim3(nb), dim3(kHuffThreads), kHuffStaticBytes, s, file, blocks, b0,
-                       chunk_ustart, tokens, hout, tables, tinfo, round, defer);
+    hipLaunchKernelGGL((k_inflate_huff<false, kKeepTokens>), dim3(nb), dim3(kHuffThreads), kHuffStaticBytes, s,
+                       file, blocks, b0, chunk_ustart, tokens, hout, tables, tinfo, round, defer, keep);
   return hipGetLastError();
 }
 hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb, uint64_t chunk_ustart,
