@@ -535,16 +535,15 @@ struct __attribute__((packed, aligned(4))) Tok4 {
 //   LD_SYNC stops with EV_MERGE (mj = index) when it reaches one of them;
 //   LD_EMIT writes tokens to tok[0..nt) and applies the output-space rules with
 //           the output position of the first token = out0.
-//   KEEP (LD_SPEC / LD_SYNC): also writes the tokens to tok[0..min(nt, isize))
-//           (isize = the scratch capacity; no output-space rules): emit then
-//           copies them instead of decoding the slice a third time.
+//   KEEP (LD_SPEC / LD_SYNC): also writes token i to tok[i * kHuffThreads]
+//           for i < isize (= the scratch capacity; no output-space rules):
+//           emit then copies them instead of decoding the slice a third time.
 template <int MODE, bool KEEP = false>
 __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t* __restrict__ W, uint32_t a,
                                                 uint32_t stop, uint32_t E, uint32_t& x, uint32_t& nt, uint32_t& nb,
                                                 MergePts& mp, uint32_t& mj, uint32_t* __restrict__ tok,
                                                 uint32_t out0, uint32_t isize) {
   constexpr bool EMIT = MODE == LD_EMIT;
-  constexpr bool STORE = EMIT || KEEP;
   uint32_t wd, cnt, nx;
   uint64_t buf;
 #define LSEEK(p)                                                    \
@@ -581,16 +580,18 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
   } while (0)
 #define LCOMMIT(t_, len_)                                                                   \
   do {                                                                                      \
-    if (STORE) {                                                                            \
+    if (EMIT) {                                                                             \
       q0 = fill == 0 ? (t_) : q0;                                                           \
       q1 = fill == 1 ? (t_) : q1;                                                           \
       q2 = fill == 2 ? (t_) : q2;                                                           \
       q3 = (t_);                                                                            \
       if (++fill == 4) {                                                                    \
-        if (!KEEP || nt < isize) *reinterpret_cast<Tok4*>(tok + nt - 3) = Tok4{q0, q1, q2, q3}; \
+        *reinterpret_cast<Tok4*>(tok + nt - 3) = Tok4{q0, q1, q2, q3};                      \
         fill = 0;                                                                           \
       }                                                                                     \
     }                                                                                       \
+    /* KEEP: token nt of the lane's column (lanes step together: whole lines) */            \
+    if (KEEP && nt < isize) tok[(uint64_t)nt * kHuffThreads] = (t_);                        \
     ++nt;                                                                                   \
     nb += (len_);                                                                           \
     if (MODE == LD_SPEC && (nt & (nt - 1)) == 0 && nt >= kMergeFirst && nt <= 8 * kMergeFirst) { \
@@ -722,7 +723,7 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
 #undef LREFILL
 #undef LCONSUME
 #undef LCOMMIT
-  if (STORE && fill && (!KEEP || nt <= isize)) {  // the 1..3 tokens not yet stored
+  if (EMIT && fill) {  // the 1..3 tokens not yet stored
     uint32_t* p = tok + nt - fill;
     p[0] = q0;
     if (fill > 1) p[1] = q1;
@@ -1474,8 +1475,10 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
     const uint32_t stop = tid == kHuffThreads - 1 ? Bend : min(B0 + (tid + 1) * S, Bend);
     MergePts mp;
     uint32_t mj = 0, x, nt, nb;
-    uint32_t* const kspec = KEEP ? keep + ((uint64_t)blockIdx.x * kHuffThreads + tid) * (2 * kKeepCap) : nullptr;
-    uint32_t* const ksync = KEEP ? kspec + kKeepCap : nullptr;
+    // token i of lane tid at [i * kHuffThreads + tid]: the lanes of a wave
+    // step together, so each token store and load is one whole line per wave
+    uint32_t* const kspec = KEEP ? keep + (uint64_t)blockIdx.x * (2 * kKeepCap * kHuffThreads) + tid : nullptr;
+    uint32_t* const ksync = KEEP ? kspec + (uint64_t)kKeepCap * kHuffThreads : nullptr;
     uint32_t kmode = 0, kfirst = 0, ksplit = 0;  // tokens: 0 spec; 1 sync; 2 sync[0, kfirst) + spec[ksplit, snt)
     uint32_t ev = lane_decode<LD_SPEC, KEEP>(L, W, a, stop, E, x, nt, nb, mp, mj, kspec, 0, kKeepCap);
     const uint32_t sx = x, snt = nt, snb = nb, sev = ev;
@@ -1527,11 +1530,11 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
       // start, leaves the lane to the decoding emit (which reports the event)
       uint32_t* const dst = tok_out + tok0 + toff;
       const uint32_t o = out0 + boff, n1 = kmode == 0 ? 0u : kfirst;
-      const uint32_t* const tail = kspec + (kmode == 2 ? ksplit : 0u) - n1;
+      const uint32_t skip = (kmode == 2 ? ksplit : 0u) - n1;  // spec index = i + skip (mod 2^32)
       uint32_t done = 0;
       bool ok = true;
       for (uint32_t i = 0; i < nt; ++i) {
-        const uint32_t t = i < n1 ? ksync[i] : tail[i];
+        const uint32_t t = i < n1 ? ksync[(uint64_t)i * kHuffThreads] : kspec[(uint64_t)(i + skip) * kHuffThreads];
         if (o + done >= isize) { ok = false; break; }
         const bool m = (t >> 31) != 0;
         if (m && ((t >> 16) & 0x7fffu) + 1 > o + done) { ok = false; break; }
