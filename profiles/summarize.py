@@ -41,7 +41,9 @@ def short(name):
     n = name.replace("(anonymous namespace)::", "").split("(")[0]
     if "rocprim" in n:
         return "rocprim:" + ("scan" if "scan" in name else "sort" if "sort" in name else "other")
-    return n.replace("void ", "").strip()
+    # k_inflate_huff<STAGE, KEEP>: the default build (KEEP false) keeps the
+    # round-1/2 names k_inflate_huff<true> / <false>
+    return n.replace("void ", "").replace(", false>", ">").strip()
 
 
 def kernel_stats(d):
