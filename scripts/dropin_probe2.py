@@ -63,48 +63,53 @@ def main():
         steps = ["none", "gpu_load", "pinned_buffer", "run_streamed"] if "--pinned" in sys.argv else ["none", "none"]
         if "--steps" in sys.argv:
             steps = sys.argv[sys.argv.index("--steps") + 1].split(",")
-        for rep, what in enumerate(steps):
-            if what == "gpu_load":  # a device-resident context opened, loaded and closed
-                g = hbam.Gpu(0)
-                try:
-                    g.load(np.fromfile(path, np.uint8))
-                finally:
-                    g.close()
-            elif what == "pinned_buffer":  # a page-locked buffer of the file, filled and freed
-                raw = np.fromfile(path, np.uint8)
-                with hbam.PinnedBuffer(raw.nbytes) as buf:
-                    buf.array[:] = raw
-                del raw
-            elif what == "run_streamed":  # bench.py's pinned-host leg
-                g = hbam.Gpu(0)
-                try:
+        for rep, step in enumerate(steps):
+            for what in step.split("+"):  # actions before this rep's measurement
+                if what == "gpu_load":  # a device-resident context opened, loaded and closed
+                    g = hbam.Gpu(0)
+                    try:
+                        g.load(np.fromfile(path, np.uint8))
+                    finally:
+                        g.close()
+                elif what == "pinned_buffer":  # a page-locked buffer of the file, filled and freed
                     raw = np.fromfile(path, np.uint8)
                     with hbam.PinnedBuffer(raw.nbytes) as buf:
                         buf.array[:] = raw
-                        g.load(raw)
-                        for _ in range(4):
-                            g.run_streamed(buf.ptr, buf.nbytes, 256 << 20)
-                finally:
-                    g.close()
-                del raw
-            elif what in ("run_resident", "reload_pinned", "streamed_one_piece"):
-                g = hbam.Gpu(0)
-                try:
-                    raw = np.fromfile(path, np.uint8)
-                    with hbam.PinnedBuffer(raw.nbytes) as buf:
-                        buf.array[:] = raw
-                        g.load(raw)
-                        for _ in range(4):
-                            if what == "run_resident":
-                                g.run()
-                            elif what == "reload_pinned":
-                                g.reload(buf.ptr, buf.nbytes, pinned=True)
-                            else:
-                                g.run_streamed(buf.ptr, buf.nbytes, buf.nbytes)
-                finally:
-                    g.close()
-                del raw
-            print("after", what, flush=True)
+                    del raw
+                elif what == "run_streamed":  # bench.py's pinned-host leg
+                    g = hbam.Gpu(0)
+                    try:
+                        raw = np.fromfile(path, np.uint8)
+                        with hbam.PinnedBuffer(raw.nbytes) as buf:
+                            buf.array[:] = raw
+                            g.load(raw)
+                            for _ in range(4):
+                                g.run_streamed(buf.ptr, buf.nbytes, 256 << 20)
+                    finally:
+                        g.close()
+                    del raw
+                elif what == "release":  # every cached device / page-locked block back to HIP
+                    print("released", hbam.release_cached_memory(), flush=True)
+                elif what.startswith("sleep"):  # idle seconds: a transient device state would wear off
+                    time.sleep(float(what[5:] or 2))
+                elif what in ("run_resident", "reload_pinned", "streamed_one_piece"):
+                    g = hbam.Gpu(0)
+                    try:
+                        raw = np.fromfile(path, np.uint8)
+                        with hbam.PinnedBuffer(raw.nbytes) as buf:
+                            buf.array[:] = raw
+                            g.load(raw)
+                            for _ in range(4):
+                                if what == "run_resident":
+                                    g.run()
+                                elif what == "reload_pinned":
+                                    g.reload(buf.ptr, buf.nbytes, pinned=True)
+                                else:
+                                    g.run_streamed(buf.ptr, buf.nbytes, buf.nbytes)
+                    finally:
+                        g.close()
+                    del raw
+            print("after", step, flush=True)
             with hbam.BamFile(path=path) as f:
                 first = f.header()["first_record_voff"]
                 t = time.perf_counter()
