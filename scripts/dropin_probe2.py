@@ -88,6 +88,12 @@ def main():
                     finally:
                         g.close()
                     del raw
+                elif what == "dummy":  # a context opened and closed, nothing decoded
+                    with hbam.BamFile(path=path) as fd:
+                        fd.header()
+                elif what == "dummy_decode":  # a context that decodes one small batch
+                    with hbam.BamFile(path=path) as fd:
+                        batches(fd, fd.header()["first_record_voff"], 1 << 16)
                 elif what == "release":  # every cached device / page-locked block back to HIP
                     print("released", hbam.release_cached_memory(), flush=True)
                 elif what.startswith("sleep"):  # idle seconds: a transient device state would wear off
