@@ -168,12 +168,30 @@ def pmc_child(path, vstart, vend):
         f.decode_span_device(vstart, vend, digest=False)
 
 
+N_SIMD = 1024          # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
+N_CU = 256
+VALU_CYCLES = 2        # a wave64 VALU instruction holds its SIMD-32 2 cycles (MI355X_MICROARCH.md, wave scheduling)
+SALU_PER_CU_CYCLE = 1  # one scalar ALU per CU
+
+
+PMC_PASSES = (  # one rocprofv3 --pmc run each (FETCH_SIZE / WRITE_SIZE use 3 / 2 of the 4 TCC slots)
+    ("fetch", ["FETCH_SIZE"]),
+    ("write", ["WRITE_SIZE"]),
+    ("issue", ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_WAVES",
+               "GRBM_GUI_ACTIVE"]),
+)
+
+
 def pmc_traffic(path, vstart, vend, kernel):
-    """HBM bytes per launch of `kernel` (its full-size dispatches): two
-    rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: their TCC slots do not
-    fit one pass) over a child process decoding the same split once.
-    Corrections per MI355X_MICROARCH.md 'HBM [CDNA4]': both counters are KiB;
-    FETCH_SIZE counts half of a wide streaming read on gfx950 (doubled)."""
+    """Counters per launch of `kernel` (every full-size dispatch of it,
+    whatever its template instance): one rocprofv3 --pmc pass per group of
+    PMC_PASSES over a child process decoding the same split once.
+    HBM bytes: corrections per MI355X_MICROARCH.md 'HBM [CDNA4]' (both
+    counters are KiB; FETCH_SIZE counts half of a wide streaming read on
+    gfx950, so it is doubled).  Issue: wave-instructions per launch against
+    the cycles the launch held the chip (GRBM_GUI_ACTIVE is summed over the
+    8 XCDs, so / 8): VALU capacity N_SIMD / VALU_CYCLES per cycle, SALU one
+    per CU per cycle."""
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(prof):
         return None
@@ -182,9 +200,10 @@ def pmc_traffic(path, vstart, vend, kernel):
     out = {}
     base = tempfile.mkdtemp(prefix="hbam_pmc_", dir="/tmp")
     env = dict(os.environ, TMPDIR="/tmp")
-    for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
-        cmd = [prof, "--pmc", counter, "--output-format", "csv", "-d", os.path.join(base, sub), "-o", "run", "--",
-               sys.executable, os.path.abspath(__file__), "--pmc-child", path, "--pmc-span", str(vstart), str(vend)]
+    for sub, counters in PMC_PASSES:
+        cmd = [prof, "--pmc"] + counters + ["--output-format", "csv", "-d", os.path.join(base, sub), "-o", "run",
+                                            "--", sys.executable, os.path.abspath(__file__), "--pmc-child", path,
+                                            "--pmc-span", str(vstart), str(vend)]
         p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
                              start_new_session=True)
         try:
@@ -192,18 +211,38 @@ def pmc_traffic(path, vstart, vend, kernel):
         except subprocess.TimeoutExpired:
             os.killpg(p.pid, 9)
             p.wait()
-            return {"error": f"{counter} pass timed out"}
+            return {"error": f"{sub} pass timed out"}
         if p.returncode != 0:
-            return {"error": f"{counter} pass rc={p.returncode}: {err.decode(errors='replace')[-300:]}"}
-        cs = summarize.counters(base, sub)
-        e = cs.get(kernel) or cs.get(kernel + "<true>") or cs.get(kernel + "<false>")
-        if not e or ("main:" + counter) not in e:
-            return {"error": f"{counter}: no dispatch of {kernel} in the counter file"}
-        out[counter] = e["main:" + counter]
+            return {"error": f"{sub} pass rc={p.returncode}: {err.decode(errors='replace')[-300:]}"}
+        cs = summarize.counters(base, sub, merge_instances=True)
+        e = cs.get(kernel)
+        if not e:
+            return {"error": f"{sub}: no dispatch of {kernel} in the counter file"}
+        for c in counters:
+            if "main:" + c in e:
+                out[c] = e["main:" + c]
+        out.setdefault("main_dispatches", e.get("main_dispatches"))
     shutil.rmtree(base, ignore_errors=True)
+    if "FETCH_SIZE" not in out or "WRITE_SIZE" not in out:
+        return {"error": "FETCH_SIZE / WRITE_SIZE missing from the counter files"}
     fetch = out["FETCH_SIZE"] * 1024 * 2
     write = out["WRITE_SIZE"] * 1024
-    return {"bytes_per_launch": int(fetch + write), "fetch_bytes": int(fetch), "write_bytes": int(write)}
+    res = {"bytes_per_launch": int(fetch + write), "fetch_bytes": int(fetch), "write_bytes": int(write),
+           "main_dispatches": out.get("main_dispatches")}
+    cyc = out.get("GRBM_GUI_ACTIVE", 0) / 8.0
+    if cyc > 0 and "SQ_INSTS_VALU" in out:
+        valu, salu = out["SQ_INSTS_VALU"], out.get("SQ_INSTS_SALU", 0.0)
+        res["issue"] = {
+            "valu_insts_per_launch": int(valu), "salu_insts_per_launch": int(salu),
+            "lds_insts_per_launch": int(out.get("SQ_INSTS_LDS", 0)),
+            "lds_bank_conflict_per_lds_inst": round(out.get("SQ_LDS_BANK_CONFLICT", 0) /
+                                                    max(out.get("SQ_INSTS_LDS", 0), 1), 3),
+            "waves_per_launch": int(out.get("SQ_WAVES", 0)), "cycles_per_launch": int(cyc),
+            "valu_frac": round(valu * VALU_CYCLES / (N_SIMD * cyc), 4),
+            "salu_frac": round(salu / (N_CU * SALU_PER_CU_CYCLE * cyc), 4),
+            "rule": f"valu_frac = SQ_INSTS_VALU x {VALU_CYCLES} cycles / ({N_SIMD} SIMDs x cycles); salu_frac = "
+                    f"SQ_INSTS_SALU / ({N_CU} CUs x cycles); cycles = GRBM_GUI_ACTIVE / 8 (XCDs) of the launch"}
+    return res
 
 
 # ---------------------------------------------------------------------------
@@ -371,7 +410,7 @@ def roofline_of(stats, world=1):
                            "frac": round(b_alg / (st["ms_total"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}}
 
 
-def run_c3(D, target_gb, steps, warmup, host_leg=False):
+def run_c3(D, target_gb, steps, warmup, host_leg=False, solo=False):
     """C3 / C5 (strong scaling): the ranks split ONE ~60 GB BAM by BGZF byte
     ranges (hbam/shard.py: BAMInputFormat.addProbabilisticSplits on the GPU
     guesser), prefetch their split's bytes to HBM and time `steps` decodes of
@@ -433,6 +472,30 @@ def run_c3(D, target_gb, steps, warmup, host_leg=False):
             ent = np.zeros(0, np.uint64)
         gathered = D.all_gather(ent.tobytes())
         f.close()
+        solo_res = None
+        if solo and D.world > 1:
+            # the N = 1 figure of this same workload: rank 0 decodes the whole
+            # file alone (resident, same steps), the other ranks wait
+            if D.rank == 0:
+                g = hbam.BamFile(path=path, device=D.device)
+                try:
+                    whole = (first, (size << 16) | 0xFFFF)
+                    t = time.perf_counter()
+                    g.prefetch(first >> 16, size)
+                    pf1 = time.perf_counter() - t
+                    g.decode_span_device(*whole, digest=False)
+                    ns = max(1, min(steps, 5))
+                    t = time.perf_counter()
+                    for _ in range(ns):
+                        st1 = g.decode_span_device(*whole, digest=False)
+                    dt1 = time.perf_counter() - t
+                finally:
+                    g.close()
+                solo_res = {"value": meta["uncompressed_bytes"] * ns / dt1 / 1e9, "ms_per_step": dt1 / ns * 1e3,
+                            "steps": ns, "records": int(st1["records"]), "prefetch_seconds": round(pf1, 2),
+                            "note": "rank 0 alone decoding the whole C3 file (resident in its HBM) while the "
+                                    "other ranks wait: the N = 1 value of this workload"}
+            D.barrier()
         if D.rank != 0:
             return None
         sbi = shard.be64([first]) + b"".join(
@@ -472,6 +535,14 @@ def run_c3(D, target_gb, steps, warmup, host_leg=False):
         res["matches_oracle"] = bool(res["c3_parity"]["records"] and res["c3_parity"]["key_digest"] and
                                      res["c3_parity"]["voff_digest"] and
                                      res["c5_splitting_bai_g4096"]["identical_to_oracle"])
+        model = cpu_model()
+        res["cpu_baseline"] = {
+            "value": round(u / dto / 1e9, 4), "unit": "GB/s", "cores": cores, "kind": "port",
+            "host_cores_total": os.cpu_count(), "records_per_s": round(dec["records"] / dto, 1), "cpu_model": model,
+            "sample": f"whole C3 file ({u} inflated bytes, {dec['records']} records) through oracle/orc_scan.c "
+                      f"(system zlib, htsjdk reader rules, STRICT) on {cores} threads of rank 0's host "
+                      f"({model}), {dto:.1f} s"}
+        res["solo"] = solo_res
         return res
     finally:
         D.barrier()
@@ -586,7 +657,8 @@ class Dist:
         if self.world > 1:
             import torch
             import torch.distributed as dist
-            torch.cuda.set_device(self.device)
+            if not args.dry_run:
+                torch.cuda.set_device(self.device)
             dist.init_process_group(self.backend)
             self.dist = dist
         self.tag = self.all_gather(f"{os.getpid()}_{int(time.time())}")[0]
@@ -661,11 +733,30 @@ def run_c2(D, args, steps, warmup, extras):
         n_all, kd, vd = compose_digests([(p[0], p[2], p[3]) for p in parts])
         u_all = sum(p[1] for p in parts)
         assert n_all == D.world * args.records, (n_all, D.world * args.records)
+        solo = None
+        if D.world > 1 and not args.no_solo:
+            # the N = 1 figure: rank 0 decodes its own split (one C2) alone
+            if D.rank == 0 and split is not None:
+                step(timing=args.serial)
+                t = time.perf_counter()
+                for _ in range(steps):
+                    step(timing=args.serial)
+                dt = time.perf_counter() - t
+                solo = {"value": round(mine[1] * steps / dt / 1e9, 3), "ms_per_step": round(dt / steps * 1e3, 3),
+                        "note": "rank 0 alone decoding its split (one C2) while the other ranks wait"}
+            D.barrier()
         out = None
         if D.rank == 0:
             st = stats[-1] if stats and stats[-1] is not None else check
+            value = u_all * steps / elapsed / 1e9
             out = {
-                "value": u_all * steps / elapsed / 1e9, "ms_per_step": elapsed / steps * 1e3,
+                "value": value, "ms_per_step": elapsed / steps * 1e3,
+                "per_gpu_value": round(value / D.world, 3),
+                "scaling_detail": None if solo is None else {
+                    "solo_value": solo["value"], "solo": solo,
+                    "efficiency_vs_solo": round(value / (D.world * solo["value"]), 4),
+                    "rule": "value / (N x solo_value): N splits of one C2 each decoded concurrently against "
+                            "rank 0's split decoded alone"},
                 "records_per_s": n_all * steps / elapsed,
                 "config": {"workload": ("C2: synthetic 10M x 150bp paired-end coordinate-sorted BAM" if D.world == 1
                                         else f"N x C2: one BAM of {D.world} x C2 records split by BGZF ranges "
@@ -707,8 +798,23 @@ def run_c2(D, args, steps, warmup, extras):
                 try:
                     tr = pmc_traffic(path, vs, ve, out["roofline"]["kernel"])
                     if tr and "bytes_per_launch" in tr:
-                        out["roofline"]["traffic"] = tr["bytes_per_launch"]
-                        out["roofline"]["traffic_detail"] = dict(tr, source="rocprofv3 --pmc child runs, this session")
+                        rf = out["roofline"]
+                        rf["traffic"] = tr["bytes_per_launch"]
+                        rf["traffic_detail"] = {k: v for k, v in tr.items() if k != "issue"}
+                        rf["traffic_detail"]["source"] = "rocprofv3 --pmc child runs, this session, every " \
+                                                         "full-size dispatch of the kernel"
+                        rf["traffic_frac_of_alg"] = round(tr["bytes_per_launch"] / max(rf["alg_bytes_per_launch"], 1), 3)
+                        if "issue" in tr:
+                            rf["issue"] = tr["issue"]
+                            lim = {"hbm": rf["frac"], "valu_issue": tr["issue"]["valu_frac"],
+                                   "salu_issue": tr["issue"]["salu_frac"],
+                                   "hbm_traffic": tr["bytes_per_launch"] / (rf["avg_launch_ms"] * 1e-3) / 1e9
+                                   / HBM_PEAK_GBS}
+                            rf["limits"] = {k: round(v, 4) for k, v in lim.items()}
+                            rf["bound"] = max(lim, key=lim.get).replace("hbm_traffic", "hbm")
+                            rf["bound_rule"] = ("the largest of: algorithmic HBM bytes / peak (frac), measured "
+                                                "HBM traffic / peak, VALU and SALU issue fractions (issue); "
+                                                "achieved / peak / frac stay the algorithmic-bytes HBM figures")
                     elif tr:
                         out["roofline"]["traffic_error"] = tr["error"]
                 except Exception as e:
@@ -742,6 +848,89 @@ def run_c2(D, args, steps, warmup, extras):
                 pass
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` with no launcher (WORLD_SIZE unset): start N rank
+    processes of this script, one per GPU, with the env torchrun would give
+    them (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), and wait for them.  The
+    parent runs before anything imports torch or libhbam, so it never touches
+    a GPU (no exec: the ranks are children).  The ranks inherit stdout, so rank
+    0's JSON line is the one line printed.  If a rank fails, the others are
+    stopped (their own PIDs) and the parent exits with the first failing code;
+    a SIGTERM to the parent is passed on to the ranks."""
+    import signal
+    port = free_port()
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", ROLE_RANK="0", HBAM_BENCH_SPAWNED="1")
+    procs = []
+
+    def stop(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.send_signal(sig)
+                except OSError:
+                    pass
+
+    def on_term(signum, frame):
+        stop()
+        sys.exit(128 + signum)
+
+    signal.signal(signal.SIGTERM, on_term)
+    import threading
+
+    def relay(pipe):
+        # rank stdout: JSON lines (rank 0's result) to stdout, anything else
+        # (gloo / RCCL chatter) to stderr, so stdout holds the one result line
+        for line in iter(pipe.readline, b""):
+            out = sys.stdout if line.lstrip().startswith(b"{") else sys.stderr
+            out.buffer.write(line)
+            out.flush()
+        pipe.close()
+
+    relays = []
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE))
+        relays.append(threading.Thread(target=relay, args=(procs[-1].stdout,), daemon=True))
+        relays[-1].start()
+    rc = 0
+    t_fail = None
+    while True:
+        alive = [p.poll() is None for p in procs]  # poll every rank (no short-circuit)
+        if not any(alive):
+            break
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad and t_fail is None:
+            rc = bad[0]
+            log(f"[bench] a rank exited with {rc}: stopping the others")
+            stop()
+            t_fail = time.time()
+        elif t_fail is not None and time.time() - t_fail > 30:
+            stop(signal.SIGKILL)
+        time.sleep(0.2)
+    for t in relays:
+        t.join(timeout=10)
+    if rc == 0:
+        rc = next((p.returncode for p in procs if p.returncode != 0), 0)
+    return rc if rc >= 0 else 128 - rc
+
+
+def check_world(args):
+    """torchrun (or spawn_ranks) sets WORLD_SIZE: it must equal --gpus."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None and int(ws) != args.gpus:
+        log(f"[bench] --gpus {args.gpus} but WORLD_SIZE={ws}: pass --gpus equal to the number of ranks")
+        sys.exit(2)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -766,6 +955,10 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo + --one-device: rehearse the N-rank sequence on a one-GPU box")
     ap.add_argument("--one-device", action="store_true", help="every rank on device 0 (rehearsal only)")
+    ap.add_argument("--no-solo", action="store_true",
+                    help="N > 1: skip rank 0's solo pass (the N = 1 value of the same workload)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="start the ranks and rendezvous (gloo), report them, decode nothing (CPU test of the launch)")
     ap.add_argument("--pmc-child", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--pmc-span", type=int, nargs=2, default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -773,8 +966,22 @@ def main():
     if args.pmc_child:
         pmc_child(args.pmc_child, *args.pmc_span)
         return
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if os.environ.get("WORLD_SIZE") is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    check_world(args)
+    if args.dry_run and os.environ.get("HBAM_BENCH_FAIL_RANK") == os.environ.get("RANK"):
+        sys.exit(3)  # test hook: a rank that dies before the rendezvous
 
     D = Dist(args)
+    if args.dry_run:  # the launch path alone (CPU tests): every rank reports, rank 0 prints
+        ranks = D.all_gather({"rank": D.rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                              "world": D.world, "pid": os.getpid()})
+        if D.rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": D.world, "ranks": ranks}), flush=True)
+        D.close()
+        return
     workload = args.workload or ("c2" if D.world == 1 else "c3")
     line = None
     if workload == "c2":
@@ -807,9 +1014,16 @@ def main():
             log(f"[extra] c2_from_pinned_host {time.time() - t:.1f}s")
             line.setdefault("extra", {})["c2_from_pinned_host"] = ph
     else:
-        r = run_c3(D, args.c3_gb, args.steps, args.warmup, host_leg=False)
+        r = run_c3(D, args.c3_gb, args.steps, args.warmup, host_leg=False, solo=not args.no_solo)
         if D.rank == 0:
+            solo = r.get("solo")
             line = {"value": r["value"], "ms_per_step": r["ms_per_step"], "records_per_s": r["records_per_s"],
+                    "per_gpu_value": round(r["value"] / D.world, 3),
+                    "scaling_detail": None if not solo else {
+                        "solo_value": round(solo["value"], 3), "solo": solo,
+                        "efficiency_vs_solo": round(r["value"] / (D.world * solo["value"]), 4),
+                        "rule": "value / (N x solo_value): the same C3 file, its N splits decoded concurrently "
+                                "against rank 0 decoding all of it alone"},
                     "scaling": "strong", "workload_key": "c3",
                     "config": {"workload": f"C3: one {r['file']['compressed_bytes'] / 1e9:.1f} GB synthetic BAM "
                                            f"(150 bp paired-end model) split by BGZF byte ranges across "
@@ -822,7 +1036,7 @@ def main():
                     "parity": {"records": r["records"], "matches_oracle": r["matches_oracle"],
                                "c3": r["c3_parity"], "c5_splitting_bai_g4096": r["c5_splitting_bai_g4096"]},
                     "stages_ms": r["stages_ms_rank0"], "windows_rank0": r["windows_rank0"],
-                    "roofline": r["roofline"], "cpu_baseline": None}
+                    "roofline": r["roofline"], "cpu_baseline": r["cpu_baseline"]}
         if D.world > 1 and not args.no_extra:
             try:  # the weak-scaling side leg: N x C2, one C2 per rank
                 w = run_c2(D, args, steps=max(3, args.steps // 2), warmup=1, extras=False)
@@ -844,6 +1058,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "launch_order": "serial (measurement)" if args.serial else "overlapped (production)",
+            "env": {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES")},
             "data": "synthetic (tools/gen_synth_bam.c: Illumina-like qualities, zlib level 5 BGZF), "
                     "generated on the box",
         }

@@ -535,10 +535,7 @@ struct __attribute__((packed, aligned(4))) Tok4 {
 //   LD_SYNC stops with EV_MERGE (mj = index) when it reaches one of them;
 //   LD_EMIT writes tokens to tok[0..nt) and applies the output-space rules with
 //           the output position of the first token = out0.
-//   KEEP (LD_SPEC / LD_SYNC): also writes token i to tok[i * kHuffThreads]
-//           for i < isize (= the scratch capacity; no output-space rules):
-//           emit then copies them instead of decoding the slice a third time.
-template <int MODE, bool KEEP = false>
+template <int MODE>
 __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t* __restrict__ W, uint32_t a,
                                                 uint32_t stop, uint32_t E, uint32_t& x, uint32_t& nt, uint32_t& nb,
                                                 MergePts& mp, uint32_t& mj, uint32_t* __restrict__ tok,
@@ -556,7 +553,7 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
   } while (0)
   LSEEK(a);
   uint32_t pos = a, ev = EV_STOP;
-  uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, fill = 0;  // EMIT / KEEP: pending tokens
+  uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0, fill = 0;  // EMIT: pending tokens
   nt = 0;
   nb = 0;
   if (MODE == LD_SPEC) {
@@ -590,8 +587,6 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
         fill = 0;                                                                           \
       }                                                                                     \
     }                                                                                       \
-    /* KEEP: token nt of the lane's column (lanes step together: whole lines) */            \
-    if (KEEP && nt < isize) tok[(uint64_t)nt * kHuffThreads] = (t_);                        \
     ++nt;                                                                                   \
     nb += (len_);                                                                           \
     if (MODE == LD_SPEC && (nt & (nt - 1)) == 0 && nt >= kMergeFirst && nt <= 8 * kMergeFirst) { \
@@ -1180,26 +1175,14 @@ constexpr uint32_t kHuffCtlBytes = (sizeof(HuffCtl) + 15) & ~15u;
 constexpr uint32_t kHuffStaticBytes = kHuffLdsBytes + kHuffCtlBytes;
 
 constexpr int kHuffWavesPerSimd = 4;  // VGPR cap 128 (no spills); LDS admits 4 staged workgroups per CU
-// Kept tokens (KEEP): each lane's spec and sync walks write their tokens to
-// two scratch ranges of kKeepCap tokens (HBM, by block of the launch and
-// lane), and emit copies them (plus the output-space checks) instead of
-// decoding the slice a third time; a lane whose walk overflowed a range, or
-// whose copy meets an output-space event, decodes as before.
-#ifndef HBAM_KEEP_TOKENS
-#define HBAM_KEEP_TOKENS 0
-#endif
-constexpr bool kKeepTokens = HBAM_KEEP_TOKENS != 0;
-constexpr uint32_t kKeepCap = 80;  // tokens per range (a slice holds ~39 on C2)
-template <bool STAGE, bool KEEP>
-__global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huff(const uint8_t* __restrict__ file,
-                                                               const BlockInfo* __restrict__ blocks, uint32_t b0,
-                                                               uint64_t chunk_ustart, uint32_t* __restrict__ tokens,
-                                                               HuffOut* __restrict__ hout,
-                                                               const uint8_t* __restrict__ tables,
-                                                               const HuffTableInfo* __restrict__ tinfo,
-                                                               uint32_t round, uint32_t defer,
-                                                               uint32_t* __restrict__ keep) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+// One decode round of one BGZF block (the body of k_inflate_huff), reading the
+// compressed bits from an LDS copy of the block (STAGE) or from HBM/L2.
+template <bool STAGE>
+__device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restrict__ file,
+                                           const BlockInfo* __restrict__ blocks, uint32_t b0, uint64_t chunk_ustart,
+                                           uint32_t* __restrict__ tokens, HuffOut* __restrict__ hout,
+                                           const uint8_t* __restrict__ tables, const HuffTableInfo* __restrict__ tinfo,
+                                           uint32_t round, uint32_t defer) {
   HuffLds& L = *reinterpret_cast<HuffLds*>(smem);
   HuffCtl& C = *reinterpret_cast<HuffCtl*>(smem + kHuffLdsBytes);
   uint4* s_in = reinterpret_cast<uint4*>(smem + kHuffStaticBytes);
@@ -1475,12 +1458,7 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
     const uint32_t stop = tid == kHuffThreads - 1 ? Bend : min(B0 + (tid + 1) * S, Bend);
     MergePts mp;
     uint32_t mj = 0, x, nt, nb;
-    // token i of lane tid at [i * kHuffThreads + tid]: the lanes of a wave
-    // step together, so each token store and load is one whole line per wave
-    uint32_t* const kspec = KEEP ? keep + (uint64_t)blockIdx.x * (2 * kKeepCap * kHuffThreads) + tid : nullptr;
-    uint32_t* const ksync = KEEP ? kspec + (uint64_t)kKeepCap * kHuffThreads : nullptr;
-    uint32_t kmode = 0, kfirst = 0, ksplit = 0;  // tokens: 0 spec; 1 sync; 2 sync[0, kfirst) + spec[ksplit, snt)
-    uint32_t ev = lane_decode<LD_SPEC, KEEP>(L, W, a, stop, E, x, nt, nb, mp, mj, kspec, 0, kKeepCap);
+    uint32_t ev = lane_decode<LD_SPEC>(L, W, a, stop, E, x, nt, nb, mp, mj, nullptr, 0, 0);
     const uint32_t sx = x, snt = nt, snb = nb, sev = ev;
     for (;;) {  // sync: restart each slice from its predecessor's exit
       if (lane == 63) {
@@ -1498,23 +1476,19 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
       if (need) {
         a = px;
         uint32_t rx, rnt, rnb;
-        const uint32_t rev = lane_decode<LD_SYNC, KEEP>(L, W, a, stop, E, rx, rnt, rnb, mp, mj, ksync, 0, kKeepCap);
+        const uint32_t rev = lane_decode<LD_SYNC>(L, W, a, stop, E, rx, rnt, rnb, mp, mj, nullptr, 0, 0);
         if (rev == EV_MERGE) {  // shares the speculative walk from boundary mj on
           const uint32_t bj = mj == 0 ? mp.b0 : mj == 1 ? mp.b1 : mj == 2 ? mp.b2 : mp.b3;
           x = sx;
           ev = sev;
           nt = rnt + snt - (kMergeFirst << mj);
           nb = rnb + snb - bj;
-          kmode = 2;
-          ksplit = kMergeFirst << mj;
         } else {
           x = rx;
           ev = rev;
           nt = rnt;
           nb = rnb;
-          kmode = 1;
         }
-        kfirst = rnt;
       }
     }
     const uint32_t lend0 = wg_min(ev != EV_STOP ? tid : 0xffffffffu, C.red);
@@ -1523,36 +1497,7 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
     uint32_t toff, boff;
     wg_excl_scan2(valid ? nt : 0u, valid ? nb : 0u, C.red, toff, boff);
     uint32_t x3 = a, nt3 = 0, nb3 = 0, ev3 = EV_STOP;
-    bool copied = false;
-    if (KEEP && valid && (kmode == 1 || snt <= kKeepCap) && (kmode == 0 || kfirst <= kKeepCap)) {
-      // emit as a copy of the kept tokens, with emit's output-space checks:
-      // output full before a token, or a distance reaching before the block
-      // start, leaves the lane to the decoding emit (which reports the event)
-      uint32_t* const dst = tok_out + tok0 + toff;
-      const uint32_t o = out0 + boff, n1 = kmode == 0 ? 0u : kfirst;
-      const uint32_t skip = (kmode == 2 ? ksplit : 0u) - n1;  // spec index = i + skip (mod 2^32)
-      uint32_t done = 0;
-      bool ok = true;
-      for (uint32_t i = 0; i < nt; ++i) {
-        const uint32_t t = i < n1 ? ksync[(uint64_t)i * kHuffThreads] : kspec[(uint64_t)(i + skip) * kHuffThreads];
-        if (o + done >= isize) { ok = false; break; }
-        const bool m = (t >> 31) != 0;
-        if (m && ((t >> 16) & 0x7fffu) + 1 > o + done) { ok = false; break; }
-        dst[i] = t;
-        done += m ? (t & 0xffffu) : ((t >> 24) & 3u);
-      }
-      // a walk that ended on an event before `stop` tried one more symbol:
-      // emit checks the output first (a full block reports FULLX / FULLO there)
-      if (ev != EV_STOP && o + done >= isize) ok = false;
-      if (ok) {
-        copied = true;
-        x3 = x;
-        nt3 = nt;
-        nb3 = nb;
-        ev3 = ev;
-      }
-    }
-    if (valid && !copied)
+    if (valid)
       ev3 = lane_decode<LD_EMIT>(L, W, a, stop, E, x3, nt3, nb3, mp, mj, tok_out + tok0 + toff, out0 + boff, isize);
     const uint32_t m3 = wg_min((valid && ev3 != EV_STOP) ? tid : 0xffffffffu, C.red);
     const uint32_t f = m3 != 0xffffffffu ? m3 : lend;
@@ -1573,6 +1518,25 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
       hout[bi] = HuffOut{ntok, err, 0u, outpos};
     }
   }
+}
+
+// Phase A: one 256-thread workgroup per BGZF block of the chunk.  Each
+// workgroup stages its compressed block in LDS when the block fits the
+// launch's dynamic LDS (stage_cap bytes after the tables), else it reads the
+// bits from HBM/L2: one launch per round whatever the block sizes (a launch
+// used to run unstaged as a whole when one block of the chunk was too big).
+__global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huff(
+    const uint8_t* __restrict__ file, const BlockInfo* __restrict__ blocks, uint32_t b0, uint64_t chunk_ustart,
+    uint32_t* __restrict__ tokens, HuffOut* __restrict__ hout, const uint8_t* __restrict__ tables,
+    const HuffTableInfo* __restrict__ tinfo, uint32_t round, uint32_t defer, uint32_t stage_cap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const BlockInfo& b = blocks[b0 + blockIdx.x];
+  const uint64_t abase = (b.coff + 18) & ~15ull;
+  const uint32_t need = (uint32_t)(((b.coff + b.csize - abase + 15) >> 4) + 1) * 16u;  // huff_stage_bytes
+  if (need <= stage_cap)
+    huff_block<true>(smem, file, blocks, b0, chunk_ustart, tokens, hout, tables, tinfo, round, defer);
+  else
+    huff_block<false>(smem, file, blocks, b0, chunk_ustart, tokens, hout, tables, tinfo, round, defer);
 }
 
 // ---------------------------------------------------------------------------
@@ -3546,28 +3510,24 @@ hipError_t launch_huff_tables(const uint8_t* file, const BlockInfo* blocks, uint
   return hipGetLastError();
 }
 // phase A proper; the chunk's tables must be built (launch_huff_tables).
-// max_stage = largest staged span of the chunk's blocks (huff_stage_bytes)
-uint64_t huff_keep_words(uint32_t nb) { return kKeepTokens ? (uint64_t)nb * kHuffThreads * 2 * kKeepCap : 0; }
+// max_stage = largest staged span of the chunk's blocks (huff_stage_bytes):
+// the dynamic LDS covers the largest span that still leaves room for 4
+// workgroups per CU; a block over it reads its bits from HBM.
 hipError_t launch_inflate_huff_prebuilt(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
                                         uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
                                         const uint8_t* tables, const HuffTableInfo* tinfo, uint32_t round,
-                                        uint32_t defer, uint32_t* keep, hipStream_t s) {
+                                        uint32_t defer, hipStream_t s) {
   if (nb == 0) return hipSuccess;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_inflate_huff<true, kKeepTokens>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_inflate_huff),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  if (kKeepTokens && !keep) return hipErrorInvalidValue;  // huff_keep_words(nb) words of scratch
-  const uint32_t staged_lds = kHuffStaticBytes + ((max_stage + 15) & ~15u);
-  if (staged_lds <= kHuffStageMaxLds)
-    hipLaunchKernelGGL((k_inflate_huff<true, kKeepTokens>), dim3(nb), dim3(kHuffThreads), staged_lds, s, file,
-                       blocks, b0, chunk_ustart, tokens, hout, tables, tinfo, round, defer, keep);
-  else
-    hipLaunchKernelGGL((k_inflate_huff<false, kKeepTokens>), dim3(nb), dim3(kHuffThreads), kHuffStaticBytes, s,
-                       file, blocks, b0, chunk_ustart, tokens, hout, tables, tinfo, round, defer, keep);
+  const uint32_t cap = std::min<uint32_t>((max_stage + 15) & ~15u, kHuffStageMaxLds - kHuffStaticBytes);
+  hipLaunchKernelGGL(k_inflate_huff, dim3(nb), dim3(kHuffThreads), kHuffStaticBytes + cap, s, file, blocks, b0,
+                     chunk_ustart, tokens, hout, tables, tinfo, round, defer, cap);
   return hipGetLastError();
 }
 hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb, uint64_t chunk_ustart,

@@ -76,13 +76,10 @@ hipError_t launch_huff_tables(const uint8_t* file, const BlockInfo* blocks, uint
                               hipStream_t s);
 // (defer: stop a block before its next DEFLATE header, kHuffPending, for
 // the next round; the last round decodes every remaining header inline)
-// keep: huff_keep_words(nb) words of scratch when the build keeps tokens
-// (HBAM_KEEP_TOKENS; 0 words otherwise, keep may be nullptr)
-uint64_t huff_keep_words(uint32_t nb);
 hipError_t launch_inflate_huff_prebuilt(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
                                         uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
                                         const uint8_t* tables, const HuffTableInfo* tinfo, uint32_t round,
-                                        uint32_t defer, uint32_t* keep, hipStream_t s);
+                                        uint32_t defer, hipStream_t s);
 // LDS bytes phase A stages for a block: its cdata from the 16 B-aligned start,
 // footer included, plus one 16 B pad (must match k_inflate_huff).
 inline uint32_t huff_stage_bytes(const BlockInfo& b) {

@@ -56,7 +56,7 @@ Pipeline::Pipeline(int device) : device_(device) {
   stage_owner_.s[1] = stream_;
   stage_owner_.n = 2;
   stage_.owner = &stage_owner_;
-  own(own_file_, own_spare_, dblocks_, ref_len_, du_, tokens_[0], tokens_[1], keep_, hout_, tables_[0], tables_[1],
+  own(own_file_, own_spare_, dblocks_, ref_len_, du_, tokens_[0], tokens_[1], hout_, tables_[0], tables_[1],
       tinfo_[0], tinfo_[1], g_, x_, x2_, entry_, base_arr_, summary_, dead_, cand_, sorted_, isz_, ust_, cnt_, flags_,
       errv_, need_, rec_pos_, rec_voff_, rcand_, force_, wcnt_, counters_, list_, hlong_, scan_tmp_, cols_, long_rec_,
       long_n_, wbuf_, woffs_, wbad_, scalars_);
@@ -561,7 +561,6 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
       HIPCHK(tables_[i].reserve(max_nb * kHuffTableImage));
       HIPCHK(tinfo_[i].reserve(max_nb));
     }
-    if (const uint64_t kw = huff_keep_words((uint32_t)max_nb)) HIPCHK(keep_.reserve(kw));  // phase A only: one stream
     if (!serial) {  // phase B and the table builds see everything queued on stream_ before this call
       HIPCHK(hipEventRecord(sync_ev_[0], stream_));
       HIPCHK(hipStreamWaitEvent(stream_b_, sync_ev_[0], 0));
@@ -594,7 +593,7 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
       HIPCHK(mark());
       HIPCHK(launch_inflate_huff_prebuilt(fbase, dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, max_stage,
                                           tables_[par].p, tinfo_[par].p, r, r + 1 < kInflateRounds ? 1u : 0u,
-                                          keep_.p, stream_));
+                                          stream_));
       HIPCHK(mark());
     }
     if (!serial) {

@@ -302,7 +302,6 @@ class Pipeline {
   DevBuf<uint8_t> du_;
   std::vector<uint8_t> inflated_;  // per block flag
   DevBuf<uint32_t> tokens_[2];  // LZ77 token streams, by chunk parity (overlapped inflate)
-  DevBuf<uint32_t> keep_;       // phase A's kept spec / sync tokens (HBAM_KEEP_TOKENS builds)
   DevBuf<HuffOut> hout_;
   DevBuf<uint8_t> tables_[2];     // phase-A prebuilt table images (per chunk, by chunk parity)
   hipStream_t stream_b_ = nullptr;  // inflate phase B (overlaps phase A of the next chunk)

@@ -116,7 +116,15 @@ def inflate_stage_spans(d):
             "lz77_launches_per_pass": sum(1 for _, _, n, _ in main[0] if n == "hbam::k_inflate_lz77")}
 
 
-def counters(d, sub):
+def base_name(k):
+    """A kernel's name without its template arguments (k_inflate_huff<true>)."""
+    return k.split("<")[0]
+
+
+def counters(d, sub, merge_instances=False):
+    """Per kernel: each counter averaged over its dispatches, and over its
+    full-size ("main:") dispatches; main_dispatches = how many those are.
+    merge_instances: template instances of a kernel count as one kernel."""
     p = _find(os.path.join(d, sub), "*counter_collection.csv")
     agg = defaultdict(lambda: defaultdict(list))
     if not p:
@@ -126,6 +134,8 @@ def counters(d, sub):
     grid = {}
     for r in csv.DictReader(open(p)):
         k = short(_col(r, "Kernel_Name", "KernelName"))
+        if merge_instances:
+            k = base_name(k)
         cn = _col(r, "Counter_Name", "CounterName")
         v = float(_col(r, "Counter_Value", "CounterValue"))
         disp = _col(r, "Dispatch_Id", "DispatchId", "Correlation_Id")
@@ -135,12 +145,17 @@ def counters(d, sub):
     gmax = defaultdict(int)
     for key, g in grid.items():
         gmax[names[key][0]] = max(gmax[names[key][0]], g)
+    main_disp = defaultdict(set)
     for key, v in per_dispatch.items():
         k, cn = names[key]
         agg[k][cn].append(v)
         if 2 * grid[key] >= gmax[k]:
             agg[k]["main:" + cn].append(v)
-    return {k: {cn: sum(vs) / len(vs) for cn, vs in cs.items()} for k, cs in agg.items()}
+            main_disp[k].add(key[2])
+    out = {k: {cn: sum(vs) / len(vs) for cn, vs in cs.items()} for k, cs in agg.items()}
+    for k, ds in main_disp.items():
+        out[k]["main_dispatches"] = len(ds)
+    return out
 
 
 def main():

@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU-box check of the tree: -m gpu tests, the C2 bench line (with the
+# in-session PMC passes), and the N-rank launch rehearsed on one GPU.
+# Usage (on the box, from the repo root): bash scripts/gpu_round.sh <tag> [steps...]
+# steps: tests bench rehearsal (default: all three)
+set -o pipefail
+TAG=${1:-x}; shift
+STEPS=${*:-tests bench rehearsal}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
+cd $R
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+        > $OUT/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+      tail -2 $OUT/pytest_gpu.log ;;
+    bench)
+      timeout -k 10 420 python -u bench.py --steps 10 --warmup 3 --no-extra > $OUT/bench.json 2> $OUT/bench.err \
+        || { echo "bench failed"; tail -30 $OUT/bench.err; exit 2; }
+      cat $OUT/bench.json ;;
+    benchfull)
+      timeout -k 10 900 python -u bench.py --steps 20 --warmup 5 > $OUT/bench_full.json 2> $OUT/bench_full.err \
+        || { echo "bench failed"; tail -30 $OUT/bench_full.err; exit 2; }
+      cat $OUT/bench_full.json ;;
+    rehearsal)
+      timeout -k 10 600 python -u bench.py --gpus 2 --dist-backend gloo --one-device --c3-gb 7 --steps 3 --warmup 1 \
+        > $OUT/rehearsal.json 2> $OUT/rehearsal.err || { echo "rehearsal failed"; tail -30 $OUT/rehearsal.err; exit 3; }
+      cat $OUT/rehearsal.json ;;
+  esac
+done

@@ -1,0 +1,47 @@
+"""bench.py's launch path on CPU: `--gpus N` with no launcher starts N rank
+processes itself (the driver may run `python bench.py --gpus 8` directly),
+and under a launcher --gpus must match WORLD_SIZE.  --dry-run stops after the
+gloo rendezvous, so nothing here touches a GPU."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    env.update(kw)
+    return env
+
+
+def test_gpus_n_spawns_n_ranks():
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "3", "--dist-backend", "gloo", "--dry-run"],
+                       capture_output=True, text=True, timeout=180, env=_env())
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, lines  # rank 0's line only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 3
+    assert [r["rank"] for r in d["ranks"]] == [0, 1, 2]
+    assert [r["local_rank"] for r in d["ranks"]] == [0, 1, 2]
+    assert len({r["pid"] for r in d["ranks"]}) == 3
+
+
+def test_world_size_must_match_gpus():
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "1", "--dry-run"], capture_output=True, text=True,
+                       timeout=60, env=_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
+    assert p.returncode == 2
+    assert "WORLD_SIZE" in p.stderr
+
+
+def test_failing_rank_fails_the_run():
+    # a bad backend name makes every rank fail at rendezvous: the parent must
+    # not hang and must exit non-zero
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dist-backend", "gloo", "--dry-run"],
+                       capture_output=True, text=True, timeout=180,
+                       env=_env(MASTER_ADDR="127.0.0.1", HBAM_BENCH_FAIL_RANK="1"))
+    assert p.returncode != 0
