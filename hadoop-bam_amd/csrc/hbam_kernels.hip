@@ -611,42 +611,106 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
   const uint32_t fast_end = E >= 48 ? min(stop, E - 47) : 0u;
   for (;;) {
     bool merged = false;
-    while (pos < fast_end && (!EMIT || out0 + nb < isize)) {
-      if (MODE == LD_SYNC) {
-        const bool h0 = pos == mp.p0, h1 = pos == mp.p1, h2 = pos == mp.p2, h3 = pos == mp.p3;
-        if (h0 | h1 | h2 | h3) {
-          mj = h0 ? 0u : h1 ? 1u : h2 ? 2u : 3u;
-          merged = true;
-          break;
+    // Every lane peeks the 64 bits at `pos` from three words (no bit-buffer
+    // refills).  The loop runs with the wave's exec mask unchanged until no
+    // lane is active (one scalar branch per symbol): a lane that has left
+    // (act = 0) or meets a symbol the fast path does not take (ok = 0) only
+    // computes, every update is a select.  The branchy form paid an exec-mask
+    // update per branch on the scalar unit that the CU's 16 waves share
+    // (SQ_INSTS_SALU ~ 0.8 x SQ_INSTS_VALU, the issue limit of the kernel).
+    // go(p): inside the fast region; SYNC: hit = p is a boundary of the lane's
+    // speculative walk (the walks share every symbol from there on; the min
+    // of the xors is 0 iff one matches).  & rather than &&: no branches.
+    auto fast_go = [&](uint32_t p, uint32_t bytes, bool& hit) -> bool {
+      hit = false;
+      if (MODE == LD_SYNC) hit = min(min(p ^ mp.p0, p ^ mp.p1), min(p ^ mp.p2, p ^ mp.p3)) == 0;
+      return (p < fast_end) & (!EMIT | (out0 + bytes < isize));
+    };
+    bool hit0;
+    const bool g0 = fast_go(pos, nb, hit0);
+    merged = g0 & hit0;
+    bool act = g0 & !hit0;
+    // SPEC: the next checkpoint count (the slow path may have passed some)
+    uint32_t ncp = nt < kMergeFirst ? kMergeFirst : nt < 2 * kMergeFirst ? 2 * kMergeFirst
+                 : nt < 4 * kMergeFirst ? 4 * kMergeFirst : nt < 8 * kMergeFirst ? 8 * kMergeFirst : ~0u;
+    if (__builtin_amdgcn_ballot_w64(act)) do {
+      const uint32_t wd = pos >> 5, sh = pos & 31;
+      const uint32_t w0 = W[wd], w1 = W[wd + 1], w2 = W[wd + 2];
+      const uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, sh);
+      const uint32_t hi = __builtin_amdgcn_alignbit(w2, w1, sh);
+      uint32_t e = L.lit[lo & ((1u << kLitRoot) - 1)];
+      {  // a code longer than the root (rare): every lane reads, long ones keep it
+        const bool lg = (e >> 26) == K_LONG;
+        if (__builtin_amdgcn_ballot_w64(lg)) {
+          const uint32_t es = L.litsub[((e & 0xffffu) + __builtin_amdgcn_ubfe(lo, kLitRoot, (e >> 16) & 15u)) &
+                                       (kLitSubCap - 1)];
+          e = lg ? es : e;
         }
       }
-      LREFILL();
-      uint32_t e = L.lit[(uint32_t)buf & ((1u << kLitRoot) - 1)];
-      if ((e >> 26) == K_LONG)
-        e = L.litsub[(e & 0xffffu) + ((uint32_t)(buf >> kLitRoot) & ((1u << ((e >> 16) & 15u)) - 1))];
-      const uint32_t kind = e >> 26;
-      if (kind > K_LEN) break;  // EOB, invalid or canonical-decode entry
+      // kind 0 literal, 1 length: isl = bit 26; kind > 1 leaves the fast path
+      const uint32_t isl = (e >> 26) & 1u;
       const uint32_t n1 = (e >> 16) & 31;
-      const bool isl = kind == K_LEN;
-      const uint32_t ex = isl ? (e >> 9) & 15 : 0u;
-      const uint32_t len = isl ? (e & 511) + ((uint32_t)(buf >> n1) & ((1u << ex) - 1)) : (e >> 24);
-      const uint32_t c1 = n1 + ex;
-      buf >>= c1;
-      cnt -= c1;
-      LREFILL();
-      uint32_t d = L.dist[(uint32_t)buf & ((1u << kDistRoot) - 1)];
-      if ((d >> 26) == K_LONG)
-        d = L.distsub[(d & 0xffffu) + ((uint32_t)(buf >> kDistRoot) & ((1u << ((d >> 16) & 15u)) - 1))];
-      if (isl && d >= kKindLit) break;  // invalid distance code
+      const uint32_t ex = __builtin_amdgcn_ubfe(e, 9, 4 * isl);
+      // literal: e >> 24 bytes; length: base + ex extra bits (ubfe of 0 bits is 0)
+      const uint32_t len = (isl ? (e & 511) : (e >> 24)) + __builtin_amdgcn_ubfe(lo, n1, ex);
+      const uint32_t c1 = n1 + ex;  // <= 20: the distance code starts inside lo
+      const uint32_t b2 = __builtin_amdgcn_alignbit(hi, lo, c1);
+      uint32_t d = L.dist[b2 & ((1u << kDistRoot) - 1)];
+      {
+        const bool lg = (d >> 26) == K_LONG;
+        if (__builtin_amdgcn_ballot_w64(lg)) {
+          const uint32_t ds = L.distsub[((d & 0xffffu) + __builtin_amdgcn_ubfe(b2, kDistRoot, (d >> 16) & 15u)) &
+                                        (kDistSubCap - 1)];
+          d = lg ? ds : d;
+        }
+      }
       const uint32_t dn = (d >> 16) & 31, dx = (d >> 21) & 15;
-      const uint32_t dist = (d & 0x7fff) + ((uint32_t)(buf >> dn) & ((1u << dx) - 1));
-      if (EMIT && isl && dist > out0 + nb) break;  // too far back: the slow path reports it
-      const uint32_t c2 = isl ? dn + dx : 0u;
-      buf >>= c2;
-      cnt -= c2;
-      pos += c1 + c2;
-      const uint32_t t = isl ? (0x80000000u | ((dist - 1) << 16) | len) : (e & 0x0300ffffu);
-      LCOMMIT(t, len);
+      const uint32_t dist = (d & 0x7fff) + __builtin_amdgcn_ubfe(b2, dn, dx);
+      // not taken here (the slow path decodes that symbol): an EOB / invalid /
+      // canonical-decode entry (e >= 2 << 26), an invalid distance code for a
+      // length (d >= 1 << 26), (EMIT) a distance before the block start
+      uint32_t bad = (e >> 27) | (isl & (d >> 26));
+      if (EMIT) bad |= isl & ((out0 + nb - dist) >> 31);
+      const bool upd = act & (bad == 0);
+      const uint32_t tm = 0x80000000u | ((dist - 1) << 16) | len, tl = e & 0x0300ffffu;
+      const uint32_t t = tl ^ ((tm ^ tl) & (0u - isl));
+      const uint32_t npos = pos + c1 + ((dn + dx) & (0u - isl));
+      pos = upd ? npos : pos;
+      nb += upd ? len : 0u;
+      if (EMIT) {
+        const uint32_t fs = upd ? fill : 7u;  // the queue slot this token takes (7: none)
+        q0 = fs == 0 ? t : q0;
+        q1 = fs == 1 ? t : q1;
+        q2 = fs == 2 ? t : q2;
+        q3 = upd ? t : q3;
+        if (fs == 3) *reinterpret_cast<Tok4*>(tok + nt - 3) = Tok4{q0, q1, q2, q3};
+        fill = upd ? (fill + 1) & 3u : fill;
+      }
+      nt += upd ? 1u : 0u;
+      if (MODE == LD_SPEC) {
+        // boundaries after symbols F, 2F, 4F, 8F (nt grows by one per symbol,
+        // so the lanes of a wave reach them in the same few iterations)
+        const bool cp = upd & (nt == ncp);
+        if (__builtin_amdgcn_ballot_w64(cp)) {
+          mp.p0 = cp && nt == kMergeFirst ? pos : mp.p0;
+          mp.b0 = cp && nt == kMergeFirst ? nb : mp.b0;
+          mp.p1 = cp && nt == 2 * kMergeFirst ? pos : mp.p1;
+          mp.b1 = cp && nt == 2 * kMergeFirst ? nb : mp.b1;
+          mp.p2 = cp && nt == 4 * kMergeFirst ? pos : mp.p2;
+          mp.b2 = cp && nt == 4 * kMergeFirst ? nb : mp.b2;
+          mp.p3 = cp && nt == 8 * kMergeFirst ? pos : mp.p3;
+          mp.b3 = cp && nt == 8 * kMergeFirst ? nb : mp.b3;
+          ncp = cp ? (ncp == 8 * kMergeFirst ? ~0u : 2 * ncp) : ncp;
+        }
+      }
+      bool hit;
+      const bool g = fast_go(pos, nb, hit);
+      merged = merged | (upd & g & hit);
+      act = upd & g & !hit;
+    } while (__builtin_amdgcn_ballot_w64(act));
+    if (MODE == LD_SYNC && merged) {
+      const bool h0 = pos == mp.p0, h1 = pos == mp.p1, h2 = pos == mp.p2;
+      mj = h0 ? 0u : h1 ? 1u : h2 ? 2u : 3u;
     }
     if (MODE == LD_SYNC && merged) {
       ev = EV_MERGE;
