@@ -630,9 +630,7 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
     const bool g0 = fast_go(pos, nb, hit0);
     merged = g0 & hit0;
     bool act = g0 & !hit0;
-    // SPEC: the next checkpoint count (the slow path may have passed some)
-    uint32_t ncp = nt < kMergeFirst ? kMergeFirst : nt < 2 * kMergeFirst ? 2 * kMergeFirst
-                 : nt < 4 * kMergeFirst ? 4 * kMergeFirst : nt < 8 * kMergeFirst ? 8 * kMergeFirst : ~0u;
+    uint32_t it = 0, ucp = kMergeFirst;  // iterations of this loop, next checkpoint iteration (wave-uniform)
     if (__builtin_amdgcn_ballot_w64(act)) do {
       const uint32_t wd = pos >> 5, sh = pos & 31;
       const uint32_t w0 = W[wd], w1 = W[wd + 1], w2 = W[wd + 2];
@@ -687,21 +685,19 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
         fill = upd ? (fill + 1) & 3u : fill;
       }
       nt += upd ? 1u : 0u;
-      if (MODE == LD_SPEC) {
-        // boundaries after symbols F, 2F, 4F, 8F (nt grows by one per symbol,
-        // so the lanes of a wave reach them in the same few iterations)
-        const bool cp = upd & (nt == ncp);
-        if (__builtin_amdgcn_ballot_w64(cp)) {
-          mp.p0 = cp && nt == kMergeFirst ? pos : mp.p0;
-          mp.b0 = cp && nt == kMergeFirst ? nb : mp.b0;
-          mp.p1 = cp && nt == 2 * kMergeFirst ? pos : mp.p1;
-          mp.b1 = cp && nt == 2 * kMergeFirst ? nb : mp.b1;
-          mp.p2 = cp && nt == 4 * kMergeFirst ? pos : mp.p2;
-          mp.b2 = cp && nt == 4 * kMergeFirst ? nb : mp.b2;
-          mp.p3 = cp && nt == 8 * kMergeFirst ? pos : mp.p3;
-          mp.b3 = cp && nt == 8 * kMergeFirst ? nb : mp.b3;
-          ncp = cp ? (ncp == 8 * kMergeFirst ? ~0u : 2 * ncp) : ncp;
-        }
+      ++it;
+      if (MODE == LD_SPEC && it == ucp) {
+        // boundaries after symbols F, 2F, 4F, 8F, tested at the iteration of
+        // that number (uniform): a lane that entered this loop with nt = 0 and
+        // decoded a symbol in every iteration has nt == it.  A lane that
+        // re-entered after the slow path records only where the counts
+        // agree; a missing boundary costs its sync walk time, not a result.
+        const bool cp = upd & (nt == it);
+        if (it == kMergeFirst) { mp.p0 = cp ? pos : mp.p0; mp.b0 = cp ? nb : mp.b0; }
+        if (it == 2 * kMergeFirst) { mp.p1 = cp ? pos : mp.p1; mp.b1 = cp ? nb : mp.b1; }
+        if (it == 4 * kMergeFirst) { mp.p2 = cp ? pos : mp.p2; mp.b2 = cp ? nb : mp.b2; }
+        if (it == 8 * kMergeFirst) { mp.p3 = cp ? pos : mp.p3; mp.b3 = cp ? nb : mp.b3; }
+        ucp = it == 8 * kMergeFirst ? 0u : 2 * it;
       }
       bool hit;
       const bool g = fast_go(pos, nb, hit);
@@ -1237,6 +1233,11 @@ enum : uint32_t { kActDecode = 1, kActDone = 2 };
 constexpr uint32_t kHuffLdsBytes = (sizeof(HuffLds) + 15) & ~15u;
 constexpr uint32_t kHuffCtlBytes = (sizeof(HuffCtl) + 15) & ~15u;
 constexpr uint32_t kHuffStaticBytes = kHuffLdsBytes + kHuffCtlBytes;
+// LDS of a phase-A workgroup (static, kHuffStageMaxLds): the staged block at
+// offset 0 (its word addresses need no base add, and the three-word peek fits
+// the ds_read2 offsets), then the tables and the control block.
+constexpr uint32_t kHuffStageCap = kHuffStageMaxLds - kHuffStaticBytes;
+static_assert(kHuffStageCap % 16 == 0 && kHuffStageCap >= 16 * 1024, "phase-A LDS budget");
 
 constexpr int kHuffWavesPerSimd = 4;  // VGPR cap 128 (no spills); LDS admits 4 staged workgroups per CU
 // One decode round of one BGZF block (the body of k_inflate_huff), reading the
@@ -1247,9 +1248,9 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
                                            uint32_t* __restrict__ tokens, HuffOut* __restrict__ hout,
                                            const uint8_t* __restrict__ tables, const HuffTableInfo* __restrict__ tinfo,
                                            uint32_t round, uint32_t defer) {
-  HuffLds& L = *reinterpret_cast<HuffLds*>(smem);
-  HuffCtl& C = *reinterpret_cast<HuffCtl*>(smem + kHuffLdsBytes);
-  uint4* s_in = reinterpret_cast<uint4*>(smem + kHuffStaticBytes);
+  HuffLds& L = *reinterpret_cast<HuffLds*>(smem + kHuffStageCap);
+  HuffCtl& C = *reinterpret_cast<HuffCtl*>(smem + kHuffStageCap + kHuffLdsBytes);
+  uint4* s_in = reinterpret_cast<uint4*>(smem);
   const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const uint32_t bi = b0 + blockIdx.x;
   const BlockInfo blk = blocks[bi];
@@ -1585,19 +1586,19 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
 }
 
 // Phase A: one 256-thread workgroup per BGZF block of the chunk.  Each
-// workgroup stages its compressed block in LDS when the block fits the
-// launch's dynamic LDS (stage_cap bytes after the tables), else it reads the
-// bits from HBM/L2: one launch per round whatever the block sizes (a launch
-// used to run unstaged as a whole when one block of the chunk was too big).
+// workgroup stages its compressed block in LDS when it fits kHuffStageCap,
+// else it reads the bits from HBM/L2: one launch per round whatever the block
+// sizes (a launch used to run unstaged as a whole when one block of the chunk
+// was too big).
 __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huff(
     const uint8_t* __restrict__ file, const BlockInfo* __restrict__ blocks, uint32_t b0, uint64_t chunk_ustart,
     uint32_t* __restrict__ tokens, HuffOut* __restrict__ hout, const uint8_t* __restrict__ tables,
-    const HuffTableInfo* __restrict__ tinfo, uint32_t round, uint32_t defer, uint32_t stage_cap) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const HuffTableInfo* __restrict__ tinfo, uint32_t round, uint32_t defer) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kHuffStageMaxLds];
   const BlockInfo& b = blocks[b0 + blockIdx.x];
   const uint64_t abase = (b.coff + 18) & ~15ull;
   const uint32_t need = (uint32_t)(((b.coff + b.csize - abase + 15) >> 4) + 1) * 16u;  // huff_stage_bytes
-  if (need <= stage_cap)
+  if (need <= kHuffStageCap)
     huff_block<true>(smem, file, blocks, b0, chunk_ustart, tokens, hout, tables, tinfo, round, defer);
   else
     huff_block<false>(smem, file, blocks, b0, chunk_ustart, tokens, hout, tables, tinfo, round, defer);
@@ -3574,24 +3575,14 @@ hipError_t launch_huff_tables(const uint8_t* file, const BlockInfo* blocks, uint
   return hipGetLastError();
 }
 // phase A proper; the chunk's tables must be built (launch_huff_tables).
-// max_stage = largest staged span of the chunk's blocks (huff_stage_bytes):
-// the dynamic LDS covers the largest span that still leaves room for 4
-// workgroups per CU; a block over it reads its bits from HBM.
 hipError_t launch_inflate_huff_prebuilt(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
                                         uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
                                         const uint8_t* tables, const HuffTableInfo* tinfo, uint32_t round,
                                         uint32_t defer, hipStream_t s) {
+  (void)max_stage;  // every workgroup decides for its own block (k_inflate_huff)
   if (nb == 0) return hipSuccess;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_inflate_huff),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  const uint32_t cap = std::min<uint32_t>((max_stage + 15) & ~15u, kHuffStageMaxLds - kHuffStaticBytes);
-  hipLaunchKernelGGL(k_inflate_huff, dim3(nb), dim3(kHuffThreads), kHuffStaticBytes + cap, s, file, blocks, b0,
-                     chunk_ustart, tokens, hout, tables, tinfo, round, defer, cap);
+  hipLaunchKernelGGL(k_inflate_huff, dim3(nb), dim3(kHuffThreads), 0, s, file, blocks, b0, chunk_ustart, tokens,
+                     hout, tables, tinfo, round, defer);
   return hipGetLastError();
 }
 hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb, uint64_t chunk_ustart,
