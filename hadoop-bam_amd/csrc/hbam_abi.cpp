@@ -236,6 +236,15 @@ int hbam_open(const char* path, const hbam_opts* opts, hbam_ctx** out) {
   return finish_open(rc, std::move(f), err, out);
 }
 
+int hbam_open_reader(uint64_t size, hbam_read_fn read, void* user, const hbam_opts* opts, hbam_ctx** out) {
+  if (!valid_stringency(opts)) return finish_open(HBAM_E_ARG, nullptr, "unknown validation stringency", out);
+  if (!read) return finish_open(HBAM_E_ARG, nullptr, "no reader", out);
+  std::unique_ptr<BamFile> f;
+  std::string err;
+  int rc = BamFile::open_reader(size, read, user, options_of(opts, true), &f, &err);
+  return finish_open(rc, std::move(f), err, out);
+}
+
 void hbam_close(hbam_ctx* ctx) { delete ctx; }
 
 const char* hbam_last_error(hbam_ctx* ctx) { return ctx ? ctx->err.c_str() : g_open_err.c_str(); }

@@ -13,9 +13,69 @@
 #include <thread>
 #include <vector>
 
+#include <errno.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include "hbam_device.h"
 #include "hbam_mem.h"
 
 namespace hbam {
+
+int HostSource::read(uint8_t* dst, uint64_t off, uint64_t len, std::string* err) const {
+  if (len == 0) return kOk;
+  if (off > size || len > size - off) {
+    *err = "read of [" + std::to_string(off) + ", " + std::to_string(off + len) + ") past the end of the " +
+           std::to_string(size) + "-byte file";
+    return kErrTrunc;
+  }
+  if (mem) {
+    // a mapped path: a page past a shortened file's end would raise SIGBUS,
+    // so the length is checked first (a truncation racing this copy can
+    // still fault; HDFS block files and finished outputs are never cut)
+    struct stat st;
+    if (fd >= 0 && fstat(fd, &st) == 0 && (uint64_t)st.st_size < off + len) {
+      *err = "file truncated: " + std::to_string((uint64_t)st.st_size) + " bytes now, " + std::to_string(size) +
+             " when opened; read of [" + std::to_string(off) + ", " + std::to_string(off + len) + ")";
+      return kErrTrunc;
+    }
+    memcpy(dst, mem + off, len);
+    return kOk;
+  }
+  uint64_t done = 0;
+  if (fd >= 0) {
+    while (done < len) {
+      const ssize_t r = pread(fd, dst + done, len - done, (off_t)(off + done));
+      if (r < 0) {
+        if (errno == EINTR) continue;
+        *err = std::string("read error: ") + strerror(errno) + " at offset " + std::to_string(off + done);
+        return kErrIO;
+      }
+      if (r == 0) break;
+      done += (uint64_t)r;
+    }
+  } else if (read_fn) {
+    std::lock_guard<std::mutex> g(mu);
+    while (done < len) {
+      const int64_t r = read_fn(user, off + done, dst + done, len - done);
+      if (r < 0) {
+        *err = "read error (reader callback returned " + std::to_string(r) + ") at offset " + std::to_string(off + done);
+        return kErrIO;
+      }
+      if (r == 0) break;
+      done += (uint64_t)r;
+    }
+  } else {
+    *err = "no host source";
+    return kErrState;
+  }
+  if (done < len) {  // the file is shorter than when it was opened
+    *err = "file truncated: " + std::to_string(done) + " of " + std::to_string(len) + " bytes at offset " +
+           std::to_string(off) + " (the file was " + std::to_string(size) + " bytes when opened)";
+    return kErrTrunc;
+  }
+  return kOk;
+}
 
 namespace {
 
@@ -36,16 +96,26 @@ class CopyPool {
   }
   // dst[0, len) <- src[0, len), split over every thread of the pool (the
   // caller copies a part too); concurrent callers take turns
-  void copy(uint8_t* dst, const uint8_t* src, size_t len) {
+  void copy(uint8_t* dst, const uint8_t* src, size_t len) { (void)run(dst, src, nullptr, 0, len, nullptr); }
+  // dst[0, len) <- bytes [off, off + len) of hs (status of the first failing part)
+  int copy(uint8_t* dst, const HostSource& hs, uint64_t off, size_t len, std::string* err) {
+    if (!hs.parallel()) return hs.read(dst, off, len, err);
+    return run(dst, nullptr, &hs, off, len, err);
+  }
+
+ private:
+  int run(uint8_t* dst, const uint8_t* src, const HostSource* hs, uint64_t off, size_t len, std::string* err) {
     std::lock_guard<std::mutex> turn(job_m_);
     if (workers_.empty() || len < (1u << 20)) {
+      if (hs) return hs->read(dst, off, len, err);
       memcpy(dst, src, len);
-      return;
+      return kOk;
     }
     Job j;
     {
       std::lock_guard<std::mutex> g(m_);
-      j = Job{dst, src, len, ++gen_};
+      status_ = kOk;
+      j = Job{dst, src, hs, off, len, ++gen_};
       job_ = j;
       left_ = parts_;
       ticket_.store(j.gen << 32);  // (job, next part)
@@ -54,12 +124,15 @@ class CopyPool {
     run_parts(j);
     std::unique_lock<std::mutex> g(m_);
     done_.wait(g, [this] { return left_ == 0; });
+    if (status_ != kOk && err) *err = status_msg_;
+    return status_;
   }
 
- private:
   struct Job {
     uint8_t* dst;
     const uint8_t* src;
+    const HostSource* hs;  // non-null: read [off, off + len) of it instead of src
+    uint64_t off;
     size_t len;
     uint64_t gen;
   };
@@ -72,8 +145,17 @@ class CopyPool {
       if ((t >> 32) != j.gen || (int)(t & 0xffffffffu) >= parts_) return;
       if (!ticket_.compare_exchange_weak(t, t + 1)) continue;
       const size_t lo = (size_t)(t & 0xffffffffu) * per, hi = lo + per < j.len ? lo + per : j.len;
-      if (lo < hi) memcpy(j.dst + lo, j.src + lo, hi - lo);
+      int rc = kOk;
+      std::string e;
+      if (lo < hi) {
+        if (j.hs) rc = j.hs->read(j.dst + lo, j.off + lo, hi - lo, &e);
+        else memcpy(j.dst + lo, j.src + lo, hi - lo);
+      }
       std::lock_guard<std::mutex> g(m_);
+      if (rc != kOk && status_ == kOk) {
+        status_ = rc;
+        status_msg_ = e;
+      }
       if (--left_ == 0) done_.notify_all();
     }
   }
@@ -100,6 +182,8 @@ class CopyPool {
   uint64_t gen_ = 0;
   int parts_ = 1;
   int left_ = 0;
+  int status_ = kOk;  // the current job's first failing part
+  std::string status_msg_;
   Job job_{};
   std::atomic<uint64_t> ticket_{0};
 };
@@ -141,11 +225,40 @@ hipError_t HostFeed::drain() {
 hipError_t HostFeed::copy(uint8_t* dst, const uint8_t* src, size_t len, hipStream_t s) {
   if (len == 0) return hipSuccess;
   if (len < kDirectBytes) return hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, s);
+  HostSource m;
+  m.mem = src;
+  m.size = len;
+  std::string err;
+  const int rc = copy(dst, m, 0, len, s, &err);
+  return rc == kOk ? hipSuccess : rc == kErrDevice ? last_hip_ : hipErrorUnknown;
+}
+
+int HostFeed::copy(uint8_t* dst, const HostSource& src, uint64_t off, size_t len, hipStream_t s, std::string* err) {
+  if (len == 0) return kOk;
+  if (src.mem && src.fd < 0 && len < kDirectBytes) {  // (a mapped path: read() checks its length first)
+    if (off > src.size || len > src.size - off) return src.read(nullptr, off, len, err);  // kErrTrunc
+    last_hip_ = hipMemcpyAsync(dst, src.mem + off, len, hipMemcpyHostToDevice, s);
+    if (last_hip_ != hipSuccess) *err = std::string("host->HBM copy: ") + hipGetErrorString(last_hip_);
+    return last_hip_ == hipSuccess ? kOk : kErrDevice;
+  }
+  const int rc = pieces(dst, src, off, len, s, err);
+  if (rc == kErrDevice && err->empty()) *err = std::string("host->HBM copy: ") + hipGetErrorString(last_hip_);
+  return rc;
+}
+
+int HostFeed::pieces(uint8_t* dst, const HostSource& src, uint64_t off, size_t len, hipStream_t s, std::string* err) {
   hipError_t e;
+#define FEEDCHK(x)                          \
+  do {                                      \
+    if ((e = (x)) != hipSuccess) {          \
+      last_hip_ = e;                        \
+      return kErrDevice;                    \
+    }                                       \
+  } while (0)
   int dev = 0;
-  if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+  FEEDCHK(hipGetDevice(&dev));
   if (dev_ != dev) {  // events and buffers of another device: start afresh
-    if ((e = drain()) != hipSuccess) return e;
+    FEEDCHK(drain());
     for (int i = 0; i < 2; ++i)
       if (ev_[i]) {
         (void)hipEventDestroy(ev_[i]);
@@ -157,11 +270,11 @@ hipError_t HostFeed::copy(uint8_t* dst, const uint8_t* src, size_t len, hipStrea
     if (!buf_[i]) {
       void* p = nullptr;
       size_t got = 0;
-      if ((e = pinned_alloc(&p, kPiece, &got)) != hipSuccess) return e;
+      FEEDCHK(pinned_alloc(&p, kPiece, &got));
       buf_[i] = static_cast<uint8_t*>(p);
       cap_[i] = got;
     }
-    if (!ev_[i] && (e = hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming)) != hipSuccess) return e;
+    if (!ev_[i]) FEEDCHK(hipEventCreateWithFlags(&ev_[i], hipEventDisableTiming));
   }
   CopyPool& cp = pool();
   static const bool trace = getenv("HBAM_FEED_TRACE") != nullptr;  // developer timing lines on stderr
@@ -170,21 +283,23 @@ hipError_t HostFeed::copy(uint8_t* dst, const uint8_t* src, size_t len, hipStrea
     const int j = (int)(k & 1);
     const auto t0 = clk::now();
     if (busy_[j]) {  // this buffer's previous piece has crossed
-      if ((e = hipEventSynchronize(ev_[j])) != hipSuccess) return e;
+      FEEDCHK(hipEventSynchronize(ev_[j]));
       busy_[j] = false;
     }
     const auto t1 = clk::now();
     const size_t n = len - o < kPiece ? len - o : kPiece;
-    cp.copy(buf_[j], src + o, n);
+    const int rc = cp.copy(buf_[j], src, off + o, n, err);
+    if (rc != kOk) return rc;
     if (trace)
       fprintf(stderr, "[feed %p] piece %zu: wait %.3f ms, fill %.3f ms (%zu B)\n", (void*)this, k,
               std::chrono::duration<double, std::milli>(t1 - t0).count(),
               std::chrono::duration<double, std::milli>(clk::now() - t1).count(), n);
-    if ((e = hipMemcpyAsync(dst + o, buf_[j], n, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    if ((e = hipEventRecord(ev_[j], s)) != hipSuccess) return e;
+    FEEDCHK(hipMemcpyAsync(dst + o, buf_[j], n, hipMemcpyHostToDevice, s));
+    FEEDCHK(hipEventRecord(ev_[j], s));
     busy_[j] = true;
   }
-  return hipSuccess;
+  return kOk;
+#undef FEEDCHK
 }
 
 }  // namespace hbam

@@ -15,7 +15,36 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <mutex>
+#include <string>
+
 namespace hbam {
+
+// Where a file's host bytes come from, the way BAMRecordReader reads through
+// WrapSeekable (util/WrapSeekable.java:56-87): memory (an in-memory copy, or
+// hbam_open's read-only mapping of the path, with fd set: each read first
+// checks the file's length, so a file truncated under an open ctx fails with
+// HBAM_E_TRUNC instead of a SIGBUS), a file descriptor read with pread (fd
+// without mem), or a positioned-read callback (hbam_open_reader: a Hadoop
+// FSDataInputStream, PositionedReadable.read(position, buf, off, len),
+// through JNI).  The mapping stays: memcpy from it by the feed threads moved
+// C3 at 108 GB/s U, pread into the bounce buffers at 47 (r04d).
+struct HostSource {
+  typedef int64_t (*ReadFn)(void* user, uint64_t offset, void* dst, uint64_t len);
+  const uint8_t* mem = nullptr;
+  int fd = -1;
+  ReadFn read_fn = nullptr;
+  void* user = nullptr;
+  uint64_t size = 0;
+  bool valid() const { return mem || fd >= 0 || read_fn; }
+  // pieces of one copy may be read by several threads at once (memory, pread);
+  // a callback is called by one thread at a time (mu)
+  bool parallel() const { return read_fn == nullptr; }
+  // dst[0, len) <- file bytes [off, off + len): kOk, kErrTrunc (the file ends
+  // before off + len) or kErrIO (a read error), with *err set
+  int read(uint8_t* dst, uint64_t off, uint64_t len, std::string* err) const;
+  mutable std::mutex mu;
+};
 
 // Copy threads of the process (the caller + workers): HBAM_FEED_THREADS, else
 // 8.  Jobs of concurrent contexts take turns.
@@ -33,6 +62,11 @@ class HostFeed {
   // may still run: order later work after it on s, or synchronize s).
   // Copies below kDirectBytes go straight through hipMemcpyAsync.
   hipError_t copy(uint8_t* dst, const uint8_t* src, size_t len, hipStream_t s);
+  // dst (device) <- file bytes [off, off + len) of src, the same way (a
+  // source that is not memory always goes through the bounce buffers).
+  // Returns kOk, kErrTrunc / kErrIO (src's read failed; *err says why) or
+  // kErrDevice.
+  int copy(uint8_t* dst, const HostSource& src, uint64_t off, size_t len, hipStream_t s, std::string* err);
   // wait for every queued piece (before the caller frees dst or unmaps src)
   hipError_t drain();
 
@@ -40,6 +74,8 @@ class HostFeed {
   static constexpr size_t kDirectBytes = 4ull << 20;
 
  private:
+  int pieces(uint8_t* dst, const HostSource& src, uint64_t off, size_t len, hipStream_t s, std::string* err);
+  hipError_t last_hip_ = hipSuccess;
   uint8_t* buf_[2] = {nullptr, nullptr};
   size_t cap_[2] = {0, 0};
   hipEvent_t ev_[2] = {nullptr, nullptr};

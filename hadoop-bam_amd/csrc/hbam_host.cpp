@@ -62,6 +62,7 @@ template class PinnedVec<uint32_t>;
 
 Source::~Source() {
   if (map) munmap(map, map_len);
+  if (fd >= 0) ::close(fd);
 }
 
 // ---------------------------------------------------------------------------
@@ -71,7 +72,9 @@ int BamFile::open_memory(const uint8_t* data, uint64_t len, const OpenOptions& o
                          std::string* err) {
   std::unique_ptr<BamFile> f(new BamFile());
   f->src_.owned.assign(data, data + len);
-  f->src_.host = f->src_.owned.data();
+  static const uint8_t empty = 0;
+  f->src_.host.mem = len ? f->src_.owned.data() : &empty;
+  f->src_.host.size = len;
   f->src_.size = len;
   int rc = f->init(o, err);
   if (rc == kOk) *out = std::move(f);
@@ -92,22 +95,40 @@ int BamFile::open_path(const char* path, const OpenOptions& o, std::unique_ptr<B
     return kErrIO;
   }
   f->src_.size = (uint64_t)st.st_size;
+  // pages are read only when a window copies them (WrapSeekable seeks); the
+  // fd stays open for the length check before each read (HostSource)
+  f->src_.fd = fd;
+  f->src_.host.fd = fd;
+  f->src_.host.size = (uint64_t)st.st_size;
   if (st.st_size > 0) {
-    // pages are read only when a window copies them (WrapSeekable seeks)
     void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_PRIVATE, fd, 0);
     if (m == MAP_FAILED) {
-      ::close(fd);
       *err = std::string("cannot map ") + path;
-      return kErrIO;
+      return kErrIO;  // (f closes fd)
     }
     f->src_.map = m;
     f->src_.map_len = (size_t)st.st_size;
-    f->src_.host = static_cast<const uint8_t*>(m);
+    f->src_.host.mem = static_cast<const uint8_t*>(m);
   } else {
     static const uint8_t empty = 0;
-    f->src_.host = &empty;
+    f->src_.host.mem = &empty;
   }
-  ::close(fd);
+  int rc = f->init(o, err);
+  if (rc == kOk) *out = std::move(f);
+  return rc;
+}
+
+int BamFile::open_reader(uint64_t size, hbam::HostSource::ReadFn fn, void* user, const OpenOptions& o,
+                         std::unique_ptr<BamFile>* out, std::string* err) {
+  if (!fn) {
+    *err = "no reader";
+    return kErrArg;
+  }
+  std::unique_ptr<BamFile> f(new BamFile());
+  f->src_.size = size;
+  f->src_.host.read_fn = fn;
+  f->src_.host.user = user;
+  f->src_.host.size = size;
   int rc = f->init(o, err);
   if (rc == kOk) *out = std::move(f);
   return rc;
@@ -164,16 +185,24 @@ int BamFile::init(const OpenOptions& o, std::string* err) {
 int BamFile::prefetch(uint64_t lo, uint64_t hi) {
   hi = std::min(hi, src_.size);
   if (lo >= hi) return kOk;
-  if (!src_.host) {
+  if (!src_.host.valid()) {
     err_ = "prefetch needs a host copy of the file";
     return kErrState;
   }
   // byte lo lands at dev.p + lo % 16: file offsets keep their 16 B alignment
   // on the device, which the kernels' aligned loads assume
-  uint8_t* at;
-  if (hipSetDevice(pipe_->device()) != hipSuccess || src_.dev.reserve(hi - lo + 16 + hbam::kFilePad) != hipSuccess ||
-      pipe_->copy_from_host(at = src_.dev.p + (lo & 15), src_.host + lo, hi - lo) != kOk ||
-      hipMemset(at + (hi - lo), 0, hbam::kFilePad) != hipSuccess) {
+  if (hipSetDevice(pipe_->device()) != hipSuccess || src_.dev.reserve(hi - lo + 16 + hbam::kFilePad) != hipSuccess) {
+    err_ = "prefetch: HBM allocation failed";
+    return kErrDevice;
+  }
+  uint8_t* at = src_.dev.p + (lo & 15);
+  src_.dev_lo = src_.dev_hi = 0;  // nothing resident until the copy succeeds
+  win_lo_ = ~0ull;
+  if (int rc = pipe_->copy_from_host(at, src_.host, lo, hi - lo)) {
+    err_ = "prefetch: " + pipe_->error();
+    return rc;
+  }
+  if (hipMemset(at + (hi - lo), 0, hbam::kFilePad) != hipSuccess) {
     err_ = "prefetch: HIP copy failed";
     return kErrDevice;
   }
@@ -195,12 +224,12 @@ int BamFile::load_window(uint64_t lo, uint64_t hi, bool free_start, bool host_on
   if (dev) {
     rc = pipe_->attach_device(src_.dev.p + (src_.dev_lo & 15) + (lo - src_.dev_lo), hi - lo, lo, hi == src_.size);
   } else {
-    if (!src_.host) {
+    if (!src_.host.valid()) {
       err_ = "file bytes [" + std::to_string(lo) + ", " + std::to_string(hi) + ") are not resident in HBM";
       return kErrState;
     }
     uint64_t copied = 0;
-    rc = pipe_->load(src_.host + lo, hi - lo, lo, hi == src_.size, &copied);
+    rc = pipe_->load(src_.host, hi - lo, lo, hi == src_.size, &copied);
     src_.bytes_read += copied;
   }
   if (rc == kOk) rc = pipe_->locate(free_start);
@@ -384,7 +413,7 @@ int BamFile::decode_step(Carry from, uint64_t vend, hbam::ChainMode mode, bool d
     hbam::Pipeline& p = *pipe_;
     // the split goes on past this window: start the next window's new bytes
     // on their way to HBM while this one decodes (Pipeline::stage)
-    if (src_.host && win_hi_ < src_.size && (!clamp || win_hi_ < (vend >> 16) + 0x20000)) {
+    if (src_.host.valid() && win_hi_ < src_.size && (!clamp || win_hi_ < (vend >> 16) + 0x20000)) {
       // the next window starts at the record this one cannot finish (a few
       // blocks before win_hi_), so it ends up to that tail short of
       // win_hi_ + span_w: stage that much less, or the bytes past its end

@@ -63,9 +63,10 @@ class PinnedVec {
 
 // Where a BamFile's compressed bytes come from.
 struct Source {
-  const uint8_t* host = nullptr;  // the whole file in host address space (copy or mmap); nullptr: device only
+  hbam::HostSource host;          // the file's host bytes (copy, pread of the path, reader callback); invalid: device only
   uint64_t size = 0;              // file length
   std::vector<uint8_t> owned;     // hbam_open_mem copy
+  int fd = -1;                    // hbam_open: the path (mapped; its length checked before each read)
   void* map = nullptr;            // hbam_open: read-only mmap of the path
   size_t map_len = 0;
   hbam::DevBuf<uint8_t> dev;      // device-resident bytes [dev_lo, dev_hi) (+ kFilePad zeros)
@@ -107,6 +108,10 @@ class BamFile {
   static int open_memory(const uint8_t* data, uint64_t len, const OpenOptions& o, std::unique_ptr<BamFile>* out,
                          std::string* err);
   static int open_path(const char* path, const OpenOptions& o, std::unique_ptr<BamFile>* out, std::string* err);
+  // a file of `size` bytes read through a positioned-read callback
+  // (hbam_open_reader: a Hadoop FSDataInputStream through JNI)
+  static int open_reader(uint64_t size, hbam::HostSource::ReadFn fn, void* user, const OpenOptions& o,
+                         std::unique_ptr<BamFile>* out, std::string* err);
   static int open_device_copy(const uint8_t* data, uint64_t len, const OpenOptions& o, std::unique_ptr<BamFile>* out,
                               std::string* err);
 

@@ -103,7 +103,26 @@ int Pipeline::hip_check(hipError_t e, const char* what) {
   } while (0)
 
 int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof, uint64_t* host_bytes) {
+  HostSource m;
+  m.mem = data;
+  m.size = len;
+  return load_from(m, 0, len, base, at_eof, host_bytes);
+}
+
+int Pipeline::load(const HostSource& src, uint64_t len, uint64_t base, bool at_eof, uint64_t* host_bytes) {
+  return load_from(src, base, len, base, at_eof, host_bytes);
+}
+
+int Pipeline::load_from(const HostSource& src, uint64_t src_off, uint64_t len, uint64_t base, bool at_eof,
+                        uint64_t* host_bytes) {
   HIPCHK(hipSetDevice(device_));
+  // dst <- file bytes [base + a, base + a + n) (src offset src_off + a)
+  auto feed = [&](uint64_t a, uint64_t n) -> int {
+    std::string e;
+    const int rc = feed_load_.copy(dfile_ + a, src, src_off + a, n, stream_, &e);
+    if (rc != kOk) err_ = e;
+    return rc;
+  };
   static const bool tr = getenv("HBAM_CURSOR_TRACE") != nullptr;
   const auto t0 = std::chrono::steady_clock::now();
   // the prefix of [base, base + len) that the window in place already holds
@@ -123,12 +142,14 @@ int Pipeline::load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof
     const uint64_t a = std::max(base + keep, stage_lo_), b = std::min(base + len, stage_hi_);
     if (stage_hi_ > stage_lo_ && a < b) {
       if (int rc = stage_wait()) return rc;
-      if (a > base + keep) HIPCHK(feed_load_.copy(dfile_ + keep, data + keep, a - base - keep, stream_));
+      if (a > base + keep)
+        if (int rc = feed(keep, a - base - keep)) return rc;
       HIPCHK(hipMemcpyAsync(dfile_ + (a - base), stage_.p + (a - stage_lo_), b - a, hipMemcpyDeviceToDevice, stream_));
-      if (base + len > b) HIPCHK(feed_load_.copy(dfile_ + (b - base), data + (b - base), base + len - b, stream_));
+      if (base + len > b)
+        if (int rc = feed(b - base, base + len - b)) return rc;
       host = len - keep - (b - a);
     } else {
-      HIPCHK(feed_load_.copy(dfile_ + keep, data + keep, len - keep, stream_));
+      if (int rc = feed(keep, len - keep)) return rc;
       host = len - keep;
     }
   }
@@ -188,25 +209,30 @@ hipError_t Pipeline::rb_sync(hipStream_t s) {
   return hipSuccess;
 }
 
-int Pipeline::copy_from_host(uint8_t* dst, const uint8_t* src, uint64_t len) {
+int Pipeline::copy_from_host(uint8_t* dst, const HostSource& src, uint64_t off, uint64_t len) {
   HIPCHK(hipSetDevice(device_));
-  HIPCHK(feed_load_.copy(dst, src, len, stream_));
+  std::string e;
+  const int rc = feed_load_.copy(dst, src, off, len, stream_, &e);
+  if (rc != kOk) {
+    HIPCHK(rb_sync(stream_));  // pieces already queued land before the caller moves on
+    return fail(rc, e);
+  }
   HIPCHK(rb_sync(stream_));
   return kOk;
 }
 
 int Pipeline::stage_wait() {
   if (stage_thr_.joinable()) stage_thr_.join();
-  const hipError_t e = stage_err_;
-  stage_err_ = hipSuccess;
-  if (e != hipSuccess) {
+  const int rc = stage_rc_;
+  stage_rc_ = kOk;
+  if (rc != kOk) {
     stage_lo_ = stage_hi_ = 0;
-    return hip_check(e, "staged host->HBM copy");
+    return fail(rc, "staged host->HBM copy: " + stage_msg_);
   }
   return kOk;
 }
 
-int Pipeline::stage(const uint8_t* host, uint64_t lo, uint64_t hi) {
+int Pipeline::stage(const HostSource& src, uint64_t lo, uint64_t hi) {
   HIPCHK(hipSetDevice(device_));
   if (hi <= lo || (lo == stage_lo_ && hi == stage_hi_)) return kOk;  // nothing new to stage
   if (int rc = stage_wait()) return rc;
@@ -217,11 +243,16 @@ int Pipeline::stage(const uint8_t* host, uint64_t lo, uint64_t hi) {
   uint8_t* dst = stage_.p;
   const int dev = device_;
   hipStream_t cs = stream_stage_;
-  stage_thr_ = std::thread([this, dst, host, lo, hi, dev, cs]() {
+  const HostSource* hs = &src;
+  stage_thr_ = std::thread([this, dst, hs, lo, hi, dev, cs]() {
+    std::string msg;
     hipError_t e = hipSetDevice(dev);
-    if (e == hipSuccess) e = feed_stage_.copy(dst, host + lo, hi - lo, cs);
-    if (e == hipSuccess) e = hipStreamSynchronize(cs);
-    stage_err_ = e;
+    int rc = e == hipSuccess ? feed_stage_.copy(dst, *hs, lo, hi - lo, cs, &msg) : (int)kErrDevice;
+    if (rc == kOk && (e = hipStreamSynchronize(cs)) != hipSuccess) rc = kErrDevice;
+    if (rc == kErrDevice && msg.empty()) msg = hipGetErrorString(e);
+    if (rc != kOk) (void)hipStreamSynchronize(cs);  // pieces already queued land first
+    stage_msg_ = msg;
+    stage_rc_ = rc;
   });
   stage_lo_ = lo;
   stage_hi_ = hi;

@@ -147,21 +147,24 @@ class Pipeline {
   // synchronizes s in any case.
   hipError_t rb(void* dst, const void* src, size_t bytes, hipStream_t s);
   hipError_t rb_sync(hipStream_t s);
-  // dst (device) <- host bytes src [len) through the copy threads and bounce
-  // buffers (HostFeed), synchronously on the pipeline's stream
-  int copy_from_host(uint8_t* dst, const uint8_t* src, uint64_t len);
+  // dst (device) <- file bytes [off, off + len) of src through the copy
+  // threads and bounce buffers (HostFeed), synchronously on the pipeline's
+  // stream (a short read of src: kErrTrunc)
+  int copy_from_host(uint8_t* dst, const HostSource& src, uint64_t off, uint64_t len);
 
   // Copy file bytes [base, base + len) into the window buffer.  at_eof: the
   // range ends at the end of the file (else the window is open).
   // When the window in place was loaded from the host too and holds a prefix
   // of the new range, that prefix moves device to device and only the rest
   // crosses PCIe; *host_bytes (optional) = the bytes copied from `data`.
+  // (src: the file, read from offset base; data: its bytes [base, base + len) in memory)
+  int load(const HostSource& src, uint64_t len, uint64_t base, bool at_eof, uint64_t* host_bytes = nullptr);
   int load(const uint8_t* data, uint64_t len, uint64_t base, bool at_eof, uint64_t* host_bytes = nullptr);
-  // Start copying file bytes [lo, hi) (host pointer `host` = file offset 0)
-  // into a staging buffer on the copy stream; a later load() takes the part
-  // of its window inside [lo, hi) from there (device-to-device) instead of
-  // the host, so a window's H2D overlaps the previous window's decode.
-  int stage(const uint8_t* host, uint64_t lo, uint64_t hi);
+  // Start copying file bytes [lo, hi) of src into a staging buffer on the
+  // copy stream; a later load() takes the part of its window inside [lo, hi)
+  // from there (device-to-device) instead of the host, so a window's H2D
+  // overlaps the previous window's decode.  src must outlive the copy.
+  int stage(const HostSource& src, uint64_t lo, uint64_t hi);
   // Use device-resident file bytes [base, base + len) (readable for kFilePad
   // bytes past len).
   int attach_device(const uint8_t* dptr, uint64_t len, uint64_t base, bool at_eof);
@@ -281,8 +284,12 @@ class Pipeline {
   uint64_t stage_lo_ = 0, stage_hi_ = 0;
   std::thread stage_thr_;      // issues the staged copy (pageable copies block their caller)
   HostFeed feed_load_, feed_stage_;  // host -> HBM copies of load() and of the stage thread
-  hipError_t stage_err_ = hipSuccess;
+  int stage_rc_ = 0;           // the staged copy's status (kOk = 0) and message
+  std::string stage_msg_;
   int stage_wait();            // the staged copy done (its error, if any)
+  // load() of file bytes [base, base + len) read from src at src_off + (x - base)
+  int load_from(const HostSource& src, uint64_t src_off, uint64_t len, uint64_t base, bool at_eof,
+                uint64_t* host_bytes);
   uint64_t flen_ = 0, base_ = 0;
   bool at_eof_ = true;
   uint64_t window_end_ = 0;

@@ -78,6 +78,9 @@ _sig("hbam_release_cached_memory", u64, [])
 _sig("hbam_open", C.c_int, [C.c_char_p, C.POINTER(Opts), C.POINTER(P)])
 _sig("hbam_open_mem", C.c_int, [P, u64, C.POINTER(Opts), C.POINTER(P)])
 _sig("hbam_open_bgzf", C.c_int, [P, u64, C.POINTER(Opts), C.POINTER(P)])
+# hbam_read_fn: int64 (*)(void *user, uint64 offset, void *dst, uint64 len)
+READ_FN = C.CFUNCTYPE(C.c_int64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64)
+_sig("hbam_open_reader", C.c_int, [u64, READ_FN, P, C.POINTER(Opts), C.POINTER(P)])
 _sig("hbam_close", None, [P])
 _sig("hbam_last_error", C.c_char_p, [P])
 _sig("hbam_free", None, [P])
@@ -289,16 +292,37 @@ class Codec:
         self.close()
 
 
+def reader_callback(read):
+    """hbam_read_fn over a Python positioned read: read(offset, n) -> bytes
+    (fewer than n only at the end of the file); an exception is an I/O error
+    (-1).  Keep the returned object alive as long as the ctx."""
+    def cb(user, off, dst, n):
+        try:
+            b = read(int(off), int(n))
+        except Exception:
+            return -1
+        if b:
+            C.memmove(dst, b, len(b))
+        return len(b)
+    return READ_FN(cb)
+
+
 class BamFile:
     """An opened BAM (or plain BGZF with bam=False) on one GPU.  path= opens
-    a file split-locally (only the windows a decode needs are read);
-    window_bytes = compressed bytes per HBM window (0: 4 GiB)."""
+    a file split-locally (only the windows a decode needs are read, with
+    pread); reader= + size= reads through a positioned-read callback
+    (hbam_open_reader: read(offset, n) -> bytes, as a Hadoop FSDataInputStream
+    does through JNI); window_bytes = compressed bytes per HBM window (0: 4 GiB)."""
 
     def __init__(self, data: bytes = None, path: str = None, device=0, bam=True, check_crc=False,
-                 stringency=STRICT, window_bytes=0):
+                 stringency=STRICT, window_bytes=0, reader=None, size=None):
         self._h = P()
         o = _opts(device, check_crc, stringency, window_bytes)
-        if path is not None:
+        if reader is not None:
+            self._cb = reader_callback(reader)
+            rc = _L.hbam_open_reader(size, self._cb, None, C.byref(o), C.byref(self._h))
+            self.size = size
+        elif path is not None:
             rc = _L.hbam_open(path.encode(), C.byref(o), C.byref(self._h))
             self.size = os.path.getsize(path)
         else:

@@ -19,10 +19,13 @@
  * a decode copies into HBM just the window of compressed bytes it works on
  * (opts.window_bytes at a time, the next record's position carried from one
  * window to the next).  Device memory is bounded by the window, whatever the
- * file size.  hbam_open maps the file read-only: the file must not be
- * truncated or replaced while a ctx is open (a copy from a page past the new
- * end raises SIGBUS in the process, where the reference's stream read would
- * throw an IOException); HDFS block files and completed outputs never are.
+ * file size.  hbam_open maps the path read-only and checks the file's
+ * length before each read of it; hbam_open_reader reads through a caller's
+ * positioned-read callback (a Hadoop FileSystem stream).  A file that turns
+ * out shorter than its length at open (truncated while a ctx is open) fails
+ * the call that reads there with HBAM_E_TRUNC, and a read error with
+ * HBAM_E_IO, as the reference's stream reads throw (only a truncation that
+ * races a copy of a mapped path can still raise SIGBUS).
  *
  * Threading: a ctx is single-threaded (RecordReader contract); the library is
  * re-entrant across ctxs.  Each ctx owns one HIP stream on its device.
@@ -48,7 +51,7 @@ extern "C" {
 #define HBAM_E_STATE 6
 #define HBAM_E_NOMEM 7
 
-#define HBAM_ABI_VERSION 3
+#define HBAM_ABI_VERSION 4
 
 /* htsjdk ValidationStringency, as util/SAMHeaderReader.java:45-46 reads it */
 #define HBAM_STRICT 0  /* htsjdk's default: SAMRecord.isValid errors -> SAMFormatException */
@@ -105,6 +108,19 @@ typedef struct hbam_batch {
 int hbam_open(const char *path, const hbam_opts *opts, hbam_ctx **out);
 int hbam_open_mem(const void *data, uint64_t len, const hbam_opts *opts, hbam_ctx **out);
 int hbam_open_bgzf(const void *data, uint64_t len, const hbam_opts *opts, hbam_ctx **out);
+/* Positioned read of a file of a known length: copy file bytes
+ * [offset, offset + len) into dst and return the bytes copied (fewer only at
+ * the end of the file, 0 there) or a negative value on an I/O error.  This is
+ * PositionedReadable.read(position, buffer, offset, length) of the
+ * FSDataInputStream that WrapSeekable.openPath wraps (util/WrapSeekable.java:
+ * 56-87; BAMRecordReader.java:147, BAMInputFormat.java:476).  dst is
+ * page-locked host memory the library owns.  The library calls read from its
+ * own threads, never two calls at once for one ctx: a JNI binding attaches
+ * the calling thread to the JVM.  user is passed through. */
+typedef int64_t (*hbam_read_fn)(void *user, uint64_t offset, void *dst, uint64_t len);
+/* hbam_open for a file read through `read` (HDFS or any Hadoop FileSystem):
+ * size = FileStatus.getLen().  user must stay valid until hbam_close. */
+int hbam_open_reader(uint64_t size, hbam_read_fn read, void *user, const hbam_opts *opts, hbam_ctx **out);
 void hbam_close(hbam_ctx *ctx);
 const char *hbam_last_error(hbam_ctx *ctx);
 void hbam_free(void *p);

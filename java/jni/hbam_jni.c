@@ -10,6 +10,7 @@
  * calls is exercised through ctypes by tests/.
  */
 #include <jni.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -88,7 +89,94 @@ JNIEXPORT jlong FN(open)(JNIEnv *env, jclass c, jstring path, jint device, jbool
   return (jlong)(intptr_t)ctx;
 }
 
-JNIEXPORT void FN(close)(JNIEnv *env, jclass c, jlong h) { hbam_close(CTX(h)); }
+/* ---- hbam_open_reader: a HbamNative.PositionedReader behind hbam_read_fn ---- */
+struct jreader {
+  JavaVM *vm;
+  jobject reader;     /* global ref */
+  jmethodID read;     /* int read(long, ByteBuffer) */
+  hbam_ctx *ctx;
+  struct jreader *next;
+};
+static struct jreader *g_readers = NULL; /* the readers of open ctxs, freed by close */
+static pthread_mutex_t g_readers_mu = PTHREAD_MUTEX_INITIALIZER;
+
+/* hbam_read_fn: called from library threads, attached here as daemons (a
+ * thread the library keeps, e.g. its staging thread, stays attached) */
+static int64_t jreader_read(void *user, uint64_t off, void *dst, uint64_t len) {
+  struct jreader *r = (struct jreader *)user;
+  JNIEnv *env = NULL;
+  if ((*r->vm)->GetEnv(r->vm, (void **)&env, JNI_VERSION_1_6) != JNI_OK &&
+      (*r->vm)->AttachCurrentThreadAsDaemon(r->vm, (void **)&env, NULL) != JNI_OK)
+    return -1;
+  uint64_t done = 0;
+  while (done < len) { /* direct buffers hold < 2 GiB */
+    const uint64_t n = len - done < (1u << 30) ? len - done : (1u << 30);
+    jobject buf = (*env)->NewDirectByteBuffer(env, (uint8_t *)dst + done, (jlong)n);
+    if (!buf) {
+      (*env)->ExceptionClear(env);
+      return -1;
+    }
+    const jint got = (*env)->CallIntMethod(env, r->reader, r->read, (jlong)(off + done), buf);
+    (*env)->DeleteLocalRef(env, buf);
+    if ((*env)->ExceptionCheck(env)) { /* the reader's IOException: HBAM_E_IO */
+      (*env)->ExceptionClear(env);
+      return -1;
+    }
+    if (got <= 0) break; /* end of file */
+    done += (uint64_t)got;
+    if ((uint64_t)got < n) break;
+  }
+  return (int64_t)done;
+}
+
+JNIEXPORT jlong FN(openReader)(JNIEnv *env, jclass c, jlong size, jobject reader, jint device, jboolean crc,
+                               jint stringency, jlong window) {
+  struct jreader *r = (struct jreader *)calloc(1, sizeof *r);
+  jclass rc_cls = reader ? (*env)->GetObjectClass(env, reader) : NULL;
+  if (!r || !rc_cls || (*env)->GetJavaVM(env, &r->vm) != 0) {
+    free(r);
+    throw_for(env, reader ? HBAM_E_NOMEM : HBAM_E_ARG, reader ? "out of memory" : "null reader");
+    return 0;
+  }
+  r->read = (*env)->GetMethodID(env, rc_cls, "read", "(JLjava/nio/ByteBuffer;)I");
+  if (!r->read) {
+    free(r);
+    return 0; /* NoSuchMethodError pending */
+  }
+  r->reader = (*env)->NewGlobalRef(env, reader);
+  hbam_opts o = {device, crc ? 1 : 0, stringency, 0, (uint64_t)window};
+  hbam_ctx *ctx = NULL;
+  int rc = hbam_open_reader((uint64_t)size, jreader_read, r, &o, &ctx);
+  if (rc != HBAM_OK) {
+    throw_for(env, rc, hbam_last_error(ctx));
+    if (ctx) hbam_close(ctx);
+    (*env)->DeleteGlobalRef(env, r->reader);
+    free(r);
+    return 0;
+  }
+  r->ctx = ctx;
+  pthread_mutex_lock(&g_readers_mu);
+  r->next = g_readers;
+  g_readers = r;
+  pthread_mutex_unlock(&g_readers_mu);
+  return (jlong)(intptr_t)ctx;
+}
+
+JNIEXPORT void FN(close)(JNIEnv *env, jclass c, jlong h) {
+  hbam_close(CTX(h)); /* joins the ctx's threads: no read after this */
+  pthread_mutex_lock(&g_readers_mu);
+  struct jreader **pp = &g_readers, *r = NULL;
+  while (*pp && (*pp)->ctx != CTX(h)) pp = &(*pp)->next;
+  if (*pp) {
+    r = *pp;
+    *pp = r->next;
+  }
+  pthread_mutex_unlock(&g_readers_mu);
+  if (r) {
+    (*env)->DeleteGlobalRef(env, r->reader);
+    free(r);
+  }
+}
 
 JNIEXPORT jlongArray FN(header)(JNIEnv *env, jclass c, jlong h) {
   hbam_header_info hi;

@@ -32,14 +32,24 @@ import org.apache.hadoop.mapreduce.InputSplit;
 import org.apache.hadoop.mapreduce.RecordReader;
 import org.apache.hadoop.mapreduce.TaskAttemptContext;
 import org.apache.hadoop.mapreduce.lib.input.FileSplit;
+import org.seqdoop.hadoop_bam.gpu.HbamFiles;
 import org.seqdoop.hadoop_bam.gpu.HbamNative;
-import org.seqdoop.hadoop_bam.util.SAMHeaderReader;
 
 public class GpuBAMInputFormat extends BAMInputFormat {
   public static final String GPU_ENABLE_PROPERTY = "hadoopbam.gpu.enable";
 
   static boolean gpuEnabled(Configuration conf) {
-    return conf.getBoolean(GPU_ENABLE_PROPERTY, false) && !isBoundedTraversal(conf);
+    return conf.getBoolean(GPU_ENABLE_PROPERTY, false) && !isBoundedTraversal(conf) && nativeAvailable();
+  }
+
+  /** libhbam and its JNI glue load (else the stock classes serve every file). */
+  static boolean nativeAvailable() {
+    try {
+      HbamNative.getKey0(0, 0);
+      return true;
+    } catch (UnsatisfiedLinkError | NoClassDefFoundError e) {
+      return false;
+    }
   }
 
   @Override
@@ -90,15 +100,19 @@ public class GpuBAMInputFormat extends BAMInputFormat {
       lengths[k] = f.getLength();
     }
     final byte[] sbi = readAll(fs, getIdxPath(file));
-    final byte[] bai = cfg.getBoolean(ENABLE_BAI_SPLIT_CALCULATOR, false) ? readAll(fs, getBAIPath(file)) : null;
-    final ValidationStringency vs = SAMHeaderReader.getValidationStringency(cfg);
-    final long ctx = HbamNative.open(GpuBAMRecordReader.localPath(file, cfg), GpuBAMRecordReader.device(cfg), false,
-                                     GpuBAMRecordReader.stringencyCode(vs), 0L);
+    byte[] bai = null;
+    if (cfg.getBoolean(ENABLE_BAI_SPLIT_CALCULATOR, false)) {
+      // as addBAISplits (:339-344): <file>.bai, else <name>.bai in place of .bam
+      bai = readAll(fs, getBAIPath(file));
+      if (bai == null) bai = readAll(fs, new Path(file.toString().replaceFirst("\\.bam$", ".bai")));
+    }
+    final ValidationStringency vs = GpuBAMRecordReader.stringencyOf(cfg);
+    // the guesser reads the file through its own file system, as
+    // WrapSeekable.openPath in addProbabilisticSplits (:476)
     final long[] v;
-    try {
-      v = HbamNative.getSplits(ctx, starts, lengths, sbi, bai);
-    } finally {
-      HbamNative.close(ctx);
+    try (HbamFiles.Handle h = HbamFiles.open(file, cfg, GpuBAMRecordReader.device(cfg),
+                                             GpuBAMRecordReader.stringencyCode(vs), 0L)) {
+      v = HbamNative.getSplits(h.ctx, starts, lengths, sbi, bai);
     }
     final int m = v.length / 2;
     for (int k = 0; k < m; ++k) {

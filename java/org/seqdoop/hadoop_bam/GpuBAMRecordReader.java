@@ -29,13 +29,12 @@ import java.io.IOException;
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
 import org.apache.hadoop.conf.Configuration;
-import org.apache.hadoop.fs.FileSystem;
-import org.apache.hadoop.fs.LocalFileSystem;
 import org.apache.hadoop.fs.Path;
 import org.apache.hadoop.io.LongWritable;
 import org.apache.hadoop.mapreduce.InputSplit;
 import org.apache.hadoop.mapreduce.RecordReader;
 import org.apache.hadoop.mapreduce.TaskAttemptContext;
+import org.seqdoop.hadoop_bam.gpu.HbamFiles;
 import org.seqdoop.hadoop_bam.gpu.HbamNative;
 import org.seqdoop.hadoop_bam.util.SAMHeaderReader;
 
@@ -49,7 +48,8 @@ public class GpuBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
   private final SAMRecordWritable record = new SAMRecordWritable();
   private final LazyBAMRecordFactory factory = new LazyBAMRecordFactory();
 
-  private long ctx;  // hbam_ctx*, 0 when closed
+  private HbamFiles.Handle file;  // the open ctx (and its stream on a non-local file system)
+  private long ctx;  // file.ctx, 0 when closed
   private SAMFileHeader header;
   private ValidationStringency stringency;
   private boolean isInitialized = false;
@@ -75,12 +75,10 @@ public class GpuBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     return HbamNative.STRICT;  // htsjdk's default
   }
 
-  /** The local file the library maps (hbam_open takes a path). */
-  static String localPath(Path file, Configuration conf) throws IOException {
-    final FileSystem fs = file.getFileSystem(conf);
-    if (!(fs instanceof LocalFileSystem) && !"file".equals(fs.getUri().getScheme()))
-      throw new IOException("hadoopbam.gpu: " + file + " is not on a local (or locally mounted) file system");
-    return fs.makeQualified(file).toUri().getPath();
+  /** The property's stringency, htsjdk's default (STRICT) when unset, as the SamReader applies it. */
+  static ValidationStringency stringencyOf(Configuration conf) {
+    final ValidationStringency s = SAMHeaderReader.getValidationStringency(conf);
+    return s == null ? ValidationStringency.DEFAULT_STRINGENCY : s;
   }
 
   @Override
@@ -92,10 +90,10 @@ public class GpuBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
 
     final Configuration conf = tctx.getConfiguration();
     final FileVirtualSplit split = (FileVirtualSplit) spl;
-    final Path file = split.getPath();
+    final Path path = split.getPath();
 
-    stringency = SAMHeaderReader.getValidationStringency(conf);
-    header = SAMHeaderReader.readSAMHeaderFrom(file, conf);
+    stringency = stringencyOf(conf);
+    header = SAMHeaderReader.readSAMHeaderFrom(path, conf);
 
     if (conf.getBoolean("hadoopbam.bam.keep-paired-reads-together", false))
       throw new IllegalArgumentException("Property hadoopbam.bam.keep-paired-reads-together is no longer honored.");
@@ -105,8 +103,12 @@ public class GpuBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     virtualEnd = split.getEndVirtualOffset();
     batchRecords = conf.getLong(BATCH_RECORDS_PROPERTY, 1L << 20);
 
-    ctx = HbamNative.open(localPath(file, conf), device(conf), false, stringencyCode(stringency),
+    // the file through its own file system, as WrapSeekable.openPath (:147):
+    // a local path is read with pread, HDFS and the rest through positioned
+    // reads of the FSDataInputStream (hbam_open_reader)
+    file = HbamFiles.open(path, conf, device(conf), stringencyCode(stringency),
                           conf.getLong(WINDOW_BYTES_PROPERTY, 0L));
+    ctx = file.ctx;
     cursor[0] = virtualStart;
     cols = null;
     n = i = 0;
@@ -126,8 +128,9 @@ public class GpuBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
 
   @Override
   public void close() throws IOException {
-    if (ctx != 0) {
-      HbamNative.close(ctx);
+    if (file != null) {
+      file.close();
+      file = null;
       ctx = 0;
     }
     cols = null;

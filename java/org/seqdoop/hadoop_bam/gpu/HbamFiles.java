@@ -1,0 +1,135 @@
+// Copyright (c) the hadoop-bam_amd authors.  MIT license (as Hadoop-BAM).
+//
+// Opening a BAM on the GPU path the way the reference opens it: a path on a
+// local file system goes to hbam_open (pread of the path), any other Hadoop
+// FileSystem (HDFS, S3A, ...) to hbam_open_reader over the FSDataInputStream
+// that WrapSeekable.openPath would wrap (util/WrapSeekable.java:56-87,
+// BAMRecordReader.java:147, BAMInputFormat.java:476), and a plain InputStream
+// (SplittingBAMIndexer.index(InputStream, ...)) to hbam_open_reader over a
+// forward-only reader.
+//
+// Not compiled in this repository (no JDK in the build image).
+package org.seqdoop.hadoop_bam.gpu;
+
+import java.io.Closeable;
+import java.io.IOException;
+import java.io.InputStream;
+import java.nio.ByteBuffer;
+import org.apache.hadoop.conf.Configuration;
+import org.apache.hadoop.fs.FSDataInputStream;
+import org.apache.hadoop.fs.FileSystem;
+import org.apache.hadoop.fs.LocalFileSystem;
+import org.apache.hadoop.fs.Path;
+
+public final class HbamFiles {
+  private HbamFiles() {}
+
+  /** Bytes copied per Java read (a bounce array between the stream and the direct buffer). */
+  static final int CHUNK = 1 << 20;
+
+  /** An open ctx and the stream (if any) its reader reads; close() closes both. */
+  public static final class Handle implements Closeable {
+    public final long ctx;
+    private final Closeable stream;
+
+    Handle(long ctx, Closeable stream) {
+      this.ctx = ctx;
+      this.stream = stream;
+    }
+
+    @Override
+    public void close() throws IOException {
+      HbamNative.close(ctx);
+      if (stream != null) stream.close();
+    }
+  }
+
+  /** PositionedReadable.read over an FSDataInputStream (thread-safe positioned reads). */
+  static final class FsReader implements HbamNative.PositionedReader {
+    private final FSDataInputStream in;
+    private final byte[] buf = new byte[CHUNK];
+
+    FsReader(FSDataInputStream in) {
+      this.in = in;
+    }
+
+    @Override
+    public int read(long position, ByteBuffer dst) throws IOException {
+      int done = 0;
+      final int want = dst.capacity();
+      while (done < want) {
+        final int r = in.read(position + done, buf, 0, Math.min(CHUNK, want - done));
+        if (r <= 0) break;  // end of file
+        dst.put(buf, 0, r);
+        done += r;
+      }
+      return done == 0 && want > 0 ? -1 : done;
+    }
+  }
+
+  /**
+   * A forward-only InputStream as positioned reads: a read ahead of the
+   * stream's position skips to it; a read behind it is an IOException (the
+   * library reads a file front to back when it indexes it).
+   */
+  static final class StreamReader implements HbamNative.PositionedReader {
+    private final InputStream in;
+    private final byte[] buf = new byte[CHUNK];
+    private long pos;
+
+    StreamReader(InputStream in) {
+      this.in = in;
+    }
+
+    @Override
+    public int read(long position, ByteBuffer dst) throws IOException {
+      if (position < pos) throw new IOException("backward read at " + position + " of a stream at " + pos);
+      while (pos < position) {
+        final long k = in.skip(position - pos);
+        if (k <= 0) {
+          if (in.read() < 0) return -1;
+          pos += 1;
+        } else {
+          pos += k;
+        }
+      }
+      int done = 0;
+      final int want = dst.capacity();
+      while (done < want) {
+        final int r = in.read(buf, 0, Math.min(CHUNK, want - done));
+        if (r < 0) break;
+        dst.put(buf, 0, r);
+        done += r;
+        pos += r;
+      }
+      return done == 0 && want > 0 ? -1 : done;
+    }
+  }
+
+  static boolean isLocal(FileSystem fs) {
+    return fs instanceof LocalFileSystem || "file".equals(fs.getUri().getScheme());
+  }
+
+  /** Open file of conf's file system on the GPU path (hbam_open or hbam_open_reader). */
+  public static Handle open(Path file, Configuration conf, int device, int stringency, long windowBytes)
+      throws IOException {
+    final FileSystem fs = file.getFileSystem(conf);
+    if (isLocal(fs)) {
+      final String p = fs.makeQualified(file).toUri().getPath();
+      return new Handle(HbamNative.open(p, device, false, stringency, windowBytes), null);
+    }
+    final long size = fs.getFileStatus(file).getLen();
+    final FSDataInputStream in = fs.open(file);
+    try {
+      return new Handle(HbamNative.openReader(size, new FsReader(in), device, false, stringency, windowBytes), in);
+    } catch (IOException | RuntimeException e) {
+      in.close();
+      throw e;
+    }
+  }
+
+  /** Open a stream of inputSize bytes read front to back (SplittingBAMIndexer.index(InputStream, ...)). */
+  public static Handle open(InputStream in, long inputSize, int device, int stringency) throws IOException {
+    return new Handle(HbamNative.openReader(inputSize, new StreamReader(in), device, false, stringency, 0L), in);
+  }
+}

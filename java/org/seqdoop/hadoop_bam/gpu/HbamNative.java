@@ -58,6 +58,27 @@ public final class HbamNative {
   public static native long open(String path, int device, boolean checkCrc, int stringency, long windowBytes)
       throws IOException;
 
+  /**
+   * Positioned reads of a file, as PositionedReadable.read(position, buf,
+   * off, len) of the FSDataInputStream WrapSeekable.openPath wraps
+   * (util/WrapSeekable.java:56-87).  dst is a direct buffer over the
+   * library's page-locked memory, valid for this call only; return the bytes
+   * put into it (from its position 0; fewer only at the end of the file) or
+   * -1 at the end of the file.  Called from library threads (attached by the
+   * glue), never twice at once for one ctx.
+   */
+  public interface PositionedReader {
+    int read(long position, ByteBuffer dst) throws IOException;
+  }
+
+  /**
+   * hbam_open_reader: the file of length size read through reader (HDFS or
+   * any Hadoop FileSystem); otherwise as {@link #open}.  The ctx holds a
+   * global reference to reader until {@link #close}.
+   */
+  public static native long openReader(long size, PositionedReader reader, int device, boolean checkCrc,
+                                       int stringency, long windowBytes) throws IOException;
+
   public static native void close(long ctx);
 
   /** hbam_header: {n_ref, l_text, first_record_voff, file_size}. */

@@ -24,6 +24,14 @@ for s in $STEPS; do
       timeout -k 10 900 python -u bench.py --steps 20 --warmup 5 > $OUT/bench_full.json 2> $OUT/bench_full.err \
         || { echo "bench failed"; tail -30 $OUT/bench_full.err; exit 2; }
       cat $OUT/bench_full.json ;;
+    reader)
+      timeout -k 10 300 python -u -m pytest tests/test_gpu_reader.py -x -q --timeout 120 --timeout-method thread \
+        > $OUT/pytest_reader.log 2>&1 || { echo "reader tests failed"; tail -40 $OUT/pytest_reader.log; exit 1; }
+      tail -2 $OUT/pytest_reader.log ;;
+    hostlegs)
+      timeout -k 10 600 python -u bench.py --steps 5 --warmup 2 --no-pmc --extras dropin_end_to_end --c3-gb 20 \
+        > $OUT/bench_host.json 2> $OUT/bench_host.err || { echo "bench failed"; tail -30 $OUT/bench_host.err; exit 2; }
+      python3 -c "import json,sys; d=json.load(open('$OUT/bench_host.json')); e=d['extra']; print(json.dumps(e['dropin_end_to_end'])); c=e['c3_c5_60GB']; print(json.dumps({k: c.get(k) for k in ('c3_streamed_from_host','value','matches_oracle')}))" ;;
     rehearsal)
       timeout -k 10 600 python -u bench.py --gpus 2 --dist-backend gloo --one-device --c3-gb 7 --steps 3 --warmup 1 \
         > $OUT/rehearsal.json 2> $OUT/rehearsal.err || { echo "rehearsal failed"; tail -30 $OUT/rehearsal.err; exit 3; }

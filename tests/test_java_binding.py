@@ -31,8 +31,8 @@ def _natives():
 
 def test_every_native_method_has_its_jni_function():
     natives = _natives()
-    assert {"open", "decodeSpan", "readerPosition", "splittingIndex", "splittingIndexForRecords", "getSplits",
-            "getKey", "getKey0", "murmurhash3"} <= set(natives)
+    assert {"open", "openReader", "decodeSpan", "readerPosition", "splittingIndex", "splittingIndexForRecords",
+            "getSplits", "getKey", "getKey0", "murmurhash3"} <= set(natives)
     jni = _strip_comments(open(JNI).read())
     fns = {}
     for m in re.finditer(r"JNIEXPORT [\w\s\*]+ FN\((\w+)\)\(([^)]*)\)", jni):
@@ -52,9 +52,10 @@ def test_jni_calls_only_declared_entry_points():
 def test_delegating_classes_call_existing_natives():
     natives = _natives()
     seen = set()
-    for cls in ("GpuBAMRecordReader.java", "GpuBAMInputFormat.java", "GpuSplittingBAMIndexer.java"):
+    for cls in ("GpuBAMRecordReader.java", "GpuBAMInputFormat.java", "GpuSplittingBAMIndexer.java",
+                os.path.join("gpu", "HbamFiles.java")):
         src = _strip_comments(open(os.path.join(JAVA, cls)).read())
-        assert "package org.seqdoop.hadoop_bam;" in src
+        assert "package org.seqdoop.hadoop_bam" in src
         for m in re.finditer(r"HbamNative\.(\w+)\(", src):
             name = m.group(1)
             assert name in natives, (cls, name)
@@ -72,8 +73,7 @@ def test_delegating_classes_call_existing_natives():
             assert nargs == natives[name], (cls, name, nargs, natives[name])
             seen.add(name)
     # the reader path, the indexer and the planner all go through the boundary
-    assert {"open", "close", "decodeSpan", "readerPosition", "getSplits", "splittingIndex",
-            "splittingIndexForRecords"} <= seen
+    assert {"open", "openReader", "close", "decodeSpan", "readerPosition", "getSplits", "splittingIndex"} <= seen
 
 
 def test_reader_mirrors_the_reference_reader_surface():
@@ -85,3 +85,43 @@ def test_reader_mirrors_the_reference_reader_surface():
         assert meth in src, meth
     # the record is built with the codec's argument order (LazyBAMRecordFactory.java:37-50)
     assert "factory.createBAMRecord(" in src
+
+
+REF_INDEXER = "/root/reference/src/main/java/org/seqdoop/hadoop_bam/SplittingBAMIndexer.java"
+
+
+def _public_signatures(src):
+    """(name, parameter types) of public methods and constructors."""
+    out = set()
+    for m in re.finditer(r"public\s+(?:static\s+)?(?:final\s+)?(?:[\w<>\[\]]+\s+)?(\w+)\s*\(([^)]*)\)", src):
+        types = tuple(re.sub(r"\bfinal\s+", "", a).split()[0] for a in m.group(2).split(",") if a.strip())
+        out.add((m.group(1), types))
+    return out
+
+
+def test_gpu_indexer_has_the_reference_indexer_api():
+    """GpuSplittingBAMIndexer offers every public entry point of
+    SplittingBAMIndexer (SplittingBAMIndexer.java:72-290) with the same
+    parameter types (the deprecated granularity-only constructor aside)."""
+    gpu = _strip_comments(open(os.path.join(JAVA, "GpuSplittingBAMIndexer.java")).read())
+    if os.path.exists(REF_INDEXER):
+        ref = _public_signatures(_strip_comments(open(REF_INDEXER).read()))
+        ref = {("GpuSplittingBAMIndexer" if n == "SplittingBAMIndexer" else n, t) for n, t in ref
+               if (n, t) != ("SplittingBAMIndexer", ("int",)) and n != "PtrSkipPair"}  # (a private helper class)
+    else:  # the reference's list, as read from the file above when it was present
+        ref = {("main", ("String[]",)), ("run", ("Configuration",)),
+               ("index", ("InputStream", "OutputStream", "long", "int")),
+               ("GpuSplittingBAMIndexer", ("OutputStream",)), ("GpuSplittingBAMIndexer", ("OutputStream", "int")),
+               ("processAlignment", ("SAMRecord",)), ("writeVirtualOffset", ("long",)), ("finish", ("long",))}
+    have = _public_signatures(gpu)
+    assert ref <= have, ref - have
+
+
+def test_write_time_indexer_keeps_o1_state():
+    """processAlignment writes record 0 and every granularity-th record as it
+    arrives (SplittingBAMIndexer.java:186-202), with a long counter: no voff
+    buffer that grows with the file."""
+    src = _strip_comments(open(os.path.join(JAVA, "GpuSplittingBAMIndexer.java")).read())
+    assert "private long count;" in src
+    assert src.count("count == 0 || (count + 1) % granularity == 0") == 2
+    assert "long[] voffs" not in src and "Arrays.copyOf" not in src
