@@ -270,6 +270,27 @@ def dropin_leg(path, first, records):
             res.setdefault(label, {})[run] = {
                 "records": n, "batches": k, "rest_bytes_to_host": nbytes, "seconds": round(dt, 3),
                 "uncompressed_GBps": round(u / dt / 1e9, 3), "records_per_s": round(n / dt, 1)}
+    # the same 1 M-record loop with the file read through hbam_open_reader (a
+    # positioned-read callback, as a Hadoop FSDataInputStream through JNI):
+    # here os.pread in Python, one call at a time
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        size = os.fstat(fd).st_size
+        for run in ("first_open", "second_open"):
+            with hbam.BamFile(reader=lambda off, n: os.pread(fd, n, off), size=size, parallel_reads=True) as f:
+                t = time.perf_counter()
+                n, k, nbytes = f.scan_batches(first, ALL, 1 << 20)
+                dt = time.perf_counter() - t
+                u = f.file_stats()[1]
+            assert n == records, (n, records)
+            res.setdefault("batches_1M_reader_callback", {})[run] = {
+                "records": n, "batches": k, "seconds": round(dt, 3), "uncompressed_GBps": round(u / dt / 1e9, 3),
+                "records_per_s": round(n / dt, 1)}
+        res["batches_1M_reader_callback"]["note"] = ("hbam_open_reader over os.pread (a Python callback, "
+                                                     "parallel_reads: the copy threads call it at once) instead "
+                                                     "of hbam_open's mapped path")
+    finally:
+        os.close(fd)
     return res
 
 

@@ -65,6 +65,7 @@ OpenOptions options_of(const hbam_opts* opts, bool header) {
   r.check_crc = o.check_crc != 0;
   r.stringency = o.stringency;
   r.window_bytes = o.window_bytes;
+  r.parallel_reads = o.parallel_reads != 0;
   r.parse_header = header;
   return r;
 }

@@ -55,7 +55,8 @@ int HostSource::read(uint8_t* dst, uint64_t off, uint64_t len, std::string* err)
       done += (uint64_t)r;
     }
   } else if (read_fn) {
-    std::lock_guard<std::mutex> g(mu);
+    std::unique_lock<std::mutex> g(mu, std::defer_lock);
+    if (!concurrent) g.lock();
     while (done < len) {
       const int64_t r = read_fn(user, off + done, dst + done, len - done);
       if (r < 0) {

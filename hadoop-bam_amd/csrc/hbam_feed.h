@@ -36,10 +36,11 @@ struct HostSource {
   ReadFn read_fn = nullptr;
   void* user = nullptr;
   uint64_t size = 0;
+  bool concurrent = false;  // read_fn may run on several threads at once (hbam_opts.parallel_reads)
   bool valid() const { return mem || fd >= 0 || read_fn; }
-  // pieces of one copy may be read by several threads at once (memory, pread);
-  // a callback is called by one thread at a time (mu)
-  bool parallel() const { return read_fn == nullptr; }
+  // pieces of one copy may be read by several threads at once (memory, pread,
+  // a concurrent callback); another callback is called by one thread at a time (mu)
+  bool parallel() const { return read_fn == nullptr || concurrent; }
   // dst[0, len) <- file bytes [off, off + len): kOk, kErrTrunc (the file ends
   // before off + len) or kErrIO (a read error), with *err set
   int read(uint8_t* dst, uint64_t off, uint64_t len, std::string* err) const;

@@ -129,6 +129,7 @@ int BamFile::open_reader(uint64_t size, hbam::HostSource::ReadFn fn, void* user,
   f->src_.host.read_fn = fn;
   f->src_.host.user = user;
   f->src_.host.size = size;
+  f->src_.host.concurrent = o.parallel_reads;
   int rc = f->init(o, err);
   if (rc == kOk) *out = std::move(f);
   return rc;

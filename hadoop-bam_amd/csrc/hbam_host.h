@@ -98,6 +98,7 @@ struct OpenOptions {
   bool check_crc = false;
   int stringency = hbam::kStrict;
   uint64_t window_bytes = kDefaultWindowBytes;
+  bool parallel_reads = false;  // a reader callback may run on several threads at once
 };
 
 // One opened BAM (or BGZF) file on one GPU.

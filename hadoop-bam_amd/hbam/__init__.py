@@ -31,12 +31,12 @@ STRICT, LENIENT, SILENT = 0, 1, 2  # hadoopbam.samheaderreader.validation-string
 
 
 class Opts(C.Structure):
-    _fields_ = [("device", i32), ("check_crc", i32), ("stringency", i32), ("reserved", i32),
+    _fields_ = [("device", i32), ("check_crc", i32), ("stringency", i32), ("parallel_reads", i32),
                 ("window_bytes", u64)]
 
 
-def _opts(device=0, check_crc=False, stringency=STRICT, window_bytes=0):
-    return Opts(device, int(check_crc), stringency, 0, window_bytes)
+def _opts(device=0, check_crc=False, stringency=STRICT, window_bytes=0, parallel_reads=False):
+    return Opts(device, int(check_crc), stringency, int(parallel_reads), window_bytes)
 
 
 class HeaderInfo(C.Structure):
@@ -312,12 +312,13 @@ class BamFile:
     a file split-locally (only the windows a decode needs are read, with
     pread); reader= + size= reads through a positioned-read callback
     (hbam_open_reader: read(offset, n) -> bytes, as a Hadoop FSDataInputStream
-    does through JNI); window_bytes = compressed bytes per HBM window (0: 4 GiB)."""
+    does through JNI; parallel_reads: it may be called from several library
+    threads at once); window_bytes = compressed bytes per HBM window (0: 4 GiB)."""
 
     def __init__(self, data: bytes = None, path: str = None, device=0, bam=True, check_crc=False,
-                 stringency=STRICT, window_bytes=0, reader=None, size=None):
+                 stringency=STRICT, window_bytes=0, reader=None, size=None, parallel_reads=False):
         self._h = P()
-        o = _opts(device, check_crc, stringency, window_bytes)
+        o = _opts(device, check_crc, stringency, window_bytes, parallel_reads)
         if reader is not None:
             self._cb = reader_callback(reader)
             rc = _L.hbam_open_reader(size, self._cb, None, C.byref(o), C.byref(self._h))

@@ -65,7 +65,8 @@ typedef struct hbam_opts {
   int32_t device;        /* hadoopbam.gpu.device: HIP device ordinal (default 0) */
   int32_t check_crc;     /* BlockCompressedInputStream.setCheckCrcs (default 0) */
   int32_t stringency;    /* hadoopbam.samheaderreader.validation-stringency (HBAM_STRICT when unset) */
-  int32_t reserved;
+  int32_t parallel_reads; /* hbam_open_reader: nonzero = the read callback may run on several library
+                             threads at once (PositionedReadable positioned reads are thread-safe) */
   uint64_t window_bytes; /* hadoopbam.gpu.window-bytes: compressed bytes per HBM window (0 = 4 GiB) */
 } hbam_opts;
 
@@ -115,8 +116,10 @@ int hbam_open_bgzf(const void *data, uint64_t len, const hbam_opts *opts, hbam_c
  * FSDataInputStream that WrapSeekable.openPath wraps (util/WrapSeekable.java:
  * 56-87; BAMRecordReader.java:147, BAMInputFormat.java:476).  dst is
  * page-locked host memory the library owns.  The library calls read from its
- * own threads, never two calls at once for one ctx: a JNI binding attaches
- * the calling thread to the JVM.  user is passed through. */
+ * own threads, one call at a time for one ctx (unless opts->parallel_reads): a JNI binding attaches
+ * the calling thread to the JVM.  user is passed through.  With
+ * opts->parallel_reads set, the library's copy threads call read at once for
+ * disjoint ranges (HDFS DFSInputStream positioned reads are thread-safe). */
 typedef int64_t (*hbam_read_fn)(void *user, uint64_t offset, void *dst, uint64_t len);
 /* hbam_open for a file read through `read` (HDFS or any Hadoop FileSystem):
  * size = FileStatus.getLen().  user must stay valid until hbam_close. */

@@ -129,8 +129,8 @@ static int64_t jreader_read(void *user, uint64_t off, void *dst, uint64_t len) {
   return (int64_t)done;
 }
 
-JNIEXPORT jlong FN(openReader)(JNIEnv *env, jclass c, jlong size, jobject reader, jint device, jboolean crc,
-                               jint stringency, jlong window) {
+JNIEXPORT jlong FN(openReader)(JNIEnv *env, jclass c, jlong size, jobject reader, jboolean parallel, jint device,
+                               jboolean crc, jint stringency, jlong window) {
   struct jreader *r = (struct jreader *)calloc(1, sizeof *r);
   jclass rc_cls = reader ? (*env)->GetObjectClass(env, reader) : NULL;
   if (!r || !rc_cls || (*env)->GetJavaVM(env, &r->vm) != 0) {
@@ -144,7 +144,7 @@ JNIEXPORT jlong FN(openReader)(JNIEnv *env, jclass c, jlong size, jobject reader
     return 0; /* NoSuchMethodError pending */
   }
   r->reader = (*env)->NewGlobalRef(env, reader);
-  hbam_opts o = {device, crc ? 1 : 0, stringency, 0, (uint64_t)window};
+  hbam_opts o = {device, crc ? 1 : 0, stringency, parallel ? 1 : 0, (uint64_t)window};
   hbam_ctx *ctx = NULL;
   int rc = hbam_open_reader((uint64_t)size, jreader_read, r, &o, &ctx);
   if (rc != HBAM_OK) {

@@ -44,10 +44,14 @@ public final class HbamFiles {
     }
   }
 
-  /** PositionedReadable.read over an FSDataInputStream (thread-safe positioned reads). */
+  /**
+   * PositionedReadable.read over an FSDataInputStream: positioned reads are
+   * thread-safe, so the library's copy threads read disjoint ranges at once
+   * (a bounce array per thread).
+   */
   static final class FsReader implements HbamNative.PositionedReader {
     private final FSDataInputStream in;
-    private final byte[] buf = new byte[CHUNK];
+    private final ThreadLocal<byte[]> bufs = ThreadLocal.withInitial(() -> new byte[CHUNK]);
 
     FsReader(FSDataInputStream in) {
       this.in = in;
@@ -55,6 +59,7 @@ public final class HbamFiles {
 
     @Override
     public int read(long position, ByteBuffer dst) throws IOException {
+      final byte[] buf = bufs.get();
       int done = 0;
       final int want = dst.capacity();
       while (done < want) {
@@ -121,7 +126,8 @@ public final class HbamFiles {
     final long size = fs.getFileStatus(file).getLen();
     final FSDataInputStream in = fs.open(file);
     try {
-      return new Handle(HbamNative.openReader(size, new FsReader(in), device, false, stringency, windowBytes), in);
+      return new Handle(HbamNative.openReader(size, new FsReader(in), true, device, false, stringency, windowBytes),
+                        in);
     } catch (IOException | RuntimeException e) {
       in.close();
       throw e;
@@ -130,6 +136,7 @@ public final class HbamFiles {
 
   /** Open a stream of inputSize bytes read front to back (SplittingBAMIndexer.index(InputStream, ...)). */
   public static Handle open(InputStream in, long inputSize, int device, int stringency) throws IOException {
-    return new Handle(HbamNative.openReader(inputSize, new StreamReader(in), device, false, stringency, 0L), in);
+    return new Handle(HbamNative.openReader(inputSize, new StreamReader(in), false, device, false, stringency, 0L),
+                      in);
   }
 }

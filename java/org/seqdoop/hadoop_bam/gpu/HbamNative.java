@@ -65,7 +65,7 @@ public final class HbamNative {
    * library's page-locked memory, valid for this call only; return the bytes
    * put into it (from its position 0; fewer only at the end of the file) or
    * -1 at the end of the file.  Called from library threads (attached by the
-   * glue), never twice at once for one ctx.
+   * glue); never twice at once for one ctx unless opened with parallelReads.
    */
   public interface PositionedReader {
     int read(long position, ByteBuffer dst) throws IOException;
@@ -73,11 +73,13 @@ public final class HbamNative {
 
   /**
    * hbam_open_reader: the file of length size read through reader (HDFS or
-   * any Hadoop FileSystem); otherwise as {@link #open}.  The ctx holds a
-   * global reference to reader until {@link #close}.
+   * any Hadoop FileSystem); otherwise as {@link #open}.  parallelReads: the
+   * reader may be called from several library threads at once (positioned
+   * reads of an FSDataInputStream are thread-safe).  The ctx holds a global
+   * reference to reader until {@link #close}.
    */
-  public static native long openReader(long size, PositionedReader reader, int device, boolean checkCrc,
-                                       int stringency, long windowBytes) throws IOException;
+  public static native long openReader(long size, PositionedReader reader, boolean parallelReads, int device,
+                                       boolean checkCrc, int stringency, long windowBytes) throws IOException;
 
   public static native void close(long ctx);
 

@@ -178,3 +178,18 @@ def test_prefetch_through_a_reader():
         st = f.decode_span_device(f.header()["first_record_voff"], ALL)
         assert st["records"] == len(s.decode_all()[1]["key"])
         assert len(r.calls) == n  # decoded from HBM, no more reads
+
+
+def test_parallel_reads_match_the_oracle():
+    """parallel_reads: the copy threads call the reader at once (disjoint
+    ranges, as HDFS positioned reads allow); same records."""
+    data, _ = synth.make_bam(60000, block_payload=65280)
+    s = orc.Stream(data)
+    r = Reader(data)
+    with hbam.BamFile(reader=r, size=len(data), parallel_reads=True) as f:
+        got = f.decode_all()
+    assert got["status"] == 0
+    assert_same_records(got, s.decode_all()[1], s.data)
+    # the ranges read cover the file, none twice
+    spans = sorted(r.calls)
+    assert all(a + n <= b for (a, n), (b, _) in zip(spans, spans[1:]))
