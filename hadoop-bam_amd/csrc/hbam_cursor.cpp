@@ -163,6 +163,12 @@ uint64_t SpanCursor::block_end(const std::vector<BlockInfo>& B, uint64_t pos) co
 }
 
 int SpanCursor::decode_window(BamFile& f, Carry from, bool cont, uint64_t m, Window* w, std::string* err) {
+  // w's buffers are reused (reserve may hand a block back to the process
+  // cache, dev_free does not wait for the device): no batch of the window
+  // they hold may still be crossing PCIe.  next_batch re-decodes a window slot
+  // only after its batches landed; this makes that explicit.
+  for (const Slot& s : slot_)
+    if (s.busy && s.win == w->id) CCHK(hipEventSynchronize(s.done));
   Step st;
   ctrace("decode_window start", nwin_);
   int rc = f.decode_step(from, vend_, hbam::kReader, true, cont, &st, f.dropin_window_bytes());
@@ -232,6 +238,41 @@ void SpanCursor::start_prealloc(uint64_t m) {
 
 void SpanCursor::join_prealloc() {
   if (prealloc_.joinable()) prealloc_.join();
+}
+
+// Rest bytes a bounded batch may hand out: below 2 GiB, the largest direct
+// ByteBuffer (HBAM_MAX_BATCH_BYTES lowers it, for tests).
+static uint64_t batch_data_cap() {
+  const char* e = getenv("HBAM_MAX_BATCH_BYTES");
+  const uint64_t hard = (1ull << 31) - 1024;
+  const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+  return v && v < hard ? v : hard;
+}
+
+int SpanCursor::capped(const Window& w, uint64_t k, uint64_t m, uint64_t* out, std::string* err) {
+  *out = m;
+  const uint64_t cap = batch_data_cap();
+  if (m <= 1 || w.nbytes - 36 * w.n <= cap) return kOk;  // the whole window fits: no reads
+  // rests of records [k, e): (rec_pos[e] - rec_pos[k]) - 36 (e - k)
+  auto rests = [&](uint64_t e, uint64_t* r) -> int {
+    CCHK(hipStreamWaitEvent(meta_, w.ready, 0));
+    const uint64_t* src[2] = {w.rec_pos + k, w.rec_pos + e};
+    CCHK(hbam::launch_gather_u64(small_ + 6, src, 2, meta_));
+    CCHK(hipStreamSynchronize(meta_));
+    *r = (small_[7] - small_[6]) - 36 * (e - k);
+    return kOk;
+  };
+  uint64_t r = 0;
+  if (int rc = rests(k + m, &r)) return rc;
+  if (r <= cap) return kOk;
+  uint64_t lo = 1, hi = m;  // rests(k + lo) fits (one record always goes), rests(k + hi) does not
+  while (hi - lo > 1) {
+    const uint64_t mid = lo + (hi - lo) / 2;
+    if (int rc = rests(k + mid, &r)) return rc;
+    if (r <= cap) lo = mid; else hi = mid;
+  }
+  *out = lo;
+  return kOk;
 }
 
 int SpanCursor::issue(const Window& w, uint64_t k, uint64_t m, Slot* s, std::string* err) {
@@ -348,7 +389,8 @@ int SpanCursor::next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t 
     k_ = 0;
   }
   Window& W = win_[front_ % 2];
-  const uint64_t m = std::min(max_records, W.n - k_);
+  uint64_t m = 0;
+  if ((rc = capped(W, k_, std::min(max_records, W.n - k_), &m, err)) != kOk) return rc;
   int s = -1;
   for (int j = 0; j < 2; ++j)
     if (slot_[j].busy && slot_[j].win == W.id && slot_[j].k == k_ && slot_[j].m == m) s = j;
@@ -362,10 +404,15 @@ int SpanCursor::next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t 
   // the next batch on the wire behind this one; the next window decoded
   // while this window's batches cross PCIe
   const bool in_window = k_ + m < W.n;
-  if (in_window && (rc = issue(W, k_ + m, std::min(max_records, W.n - k_ - m), &O, err)) != kOk) return rc;
+  uint64_t m2 = 0;
+  if (in_window && ((rc = capped(W, k_ + m, std::min(max_records, W.n - k_ - m), &m2, err)) != kOk ||
+                    (rc = issue(W, k_ + m, m2, &O, err)) != kOk))
+    return rc;
   if (!W.ended && nwin_ == front_ + 1 && (rc = decode_next(W)) != kOk) return rc;
   const Window* N = nwin_ > front_ + 1 ? &win_[(front_ + 1) % 2] : nullptr;
-  if (!in_window && N && N->n && (rc = issue(*N, 0, std::min(max_records, N->n), &O, err)) != kOk) return rc;
+  if (!in_window && N && N->n &&
+      ((rc = capped(*N, 0, std::min(max_records, N->n), &m2, err)) != kOk || (rc = issue(*N, 0, m2, &O, err)) != kOk))
+    return rc;
   // the read-ahead record past the window: the next window's first record
   uint64_t ahead = ~0ull;
   if (in_window) {

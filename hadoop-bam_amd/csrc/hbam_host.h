@@ -398,6 +398,11 @@ class SpanCursor {
   int ensure_streams(hbam::Pipeline& p, std::string* err);
   int decode_window(BamFile& f, Carry from, bool cont, uint64_t m, Window* w, std::string* err);
   int issue(const Window& w, uint64_t k, uint64_t m, Slot* s, std::string* err);
+  // m capped so that the batch's rest bytes fit a Java direct buffer (an int
+  // capacity and int positions: GpuBAMRecordReader.recordAt): the largest
+  // m' <= m whose rests [k, k + m') take at most batch_data_cap() bytes
+  // (at least one record)
+  int capped(const Window& w, uint64_t k, uint64_t m, uint64_t* out, std::string* err);
   int drain();
   int next_batch_all(BamFile& f, uint64_t vstart, uint64_t vend, BatchView* out, uint64_t* next_voff,
                      std::string* err);

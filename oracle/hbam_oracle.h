@@ -158,7 +158,15 @@ typedef struct {
    * or voff (both modes); dmix = MurmurHash3 fmix64.  Composable:
    * D(A ++ B) = D(A) * P^|B| + D(B). */
   uint64_t key_digest, voff_digest;
+  /* mode 0: the same digest of each fixed field, in the order refID, pos,
+   * l_read_name, mapq, bin, n_cigar, flag, l_seq, next_refID, next_pos, tlen
+   * (signed fields sign-extended to 64 bits), and the zlib crc32 of every
+   * record's rest ([36, 4 + block_size)) back to back, with its length */
+  uint64_t field_digest[11];
+  uint32_t rest_crc, pad;
+  uint64_t rest_bytes;
 } orc_scan_result;
+#define ORC_N_FIELDS 11
 #define ORC_DIGEST_P 0x100000001b3ull
 int orc_scan(const uint8_t *file, uint64_t len, int threads, int mode, int stringency, int32_t g,
              uint64_t max_blocks, uint8_t **sbi, uint64_t *sbi_len, orc_scan_result *res);

@@ -290,7 +290,10 @@ def record_invalid(rec: bytes, n_ref, ref_len=None, strict=True):
 class _ScanResult(C.Structure):
     _fields_ = [("records", C.c_uint64), ("key_xor", C.c_uint64), ("voff_sum", C.c_uint64),
                 ("blocks", C.c_uint64), ("u_bytes", C.c_uint64), ("status", C.c_int32), ("rewalks", C.c_int32),
-                ("key_digest", C.c_uint64), ("voff_digest", C.c_uint64)]
+                ("key_digest", C.c_uint64), ("voff_digest", C.c_uint64), ("field_digest", C.c_uint64 * 11),
+                ("rest_crc", C.c_uint32), ("pad", C.c_uint32), ("rest_bytes", C.c_uint64)]
+    FIELDS = ("ref_id", "pos", "l_read_name", "mapq", "bin", "n_cigar", "flag", "l_seq", "next_ref_id", "next_pos",
+              "tlen")
 
 
 DIGEST_P = 0x100000001B3  # ORC_DIGEST_P (hbam_oracle.h)
@@ -315,6 +318,27 @@ def digest(values):
     for v in values:
         d = (d * DIGEST_P + dmix(int(v))) & M64
     return d
+
+
+def digest_np(values):
+    """digest() of a numpy integer column (signed columns sign-extended to
+    64 bits, as orc_scan_result.field_digest), vectorized: (n, digest)."""
+    x = np.asarray(values)
+    x = (x.astype(np.int64) if x.dtype.kind == "i" else x.astype(np.uint64)).view(np.uint64)
+    n = len(x)
+    if n == 0:
+        return 0, 0
+    with np.errstate(over="ignore"):
+        x = x ^ (x >> np.uint64(33))
+        x = x * np.uint64(0xFF51AFD7ED558CCD)
+        x = x ^ (x >> np.uint64(33))
+        x = x * np.uint64(0xC4CEB9FE1A85EC53)
+        x = x ^ (x >> np.uint64(33))
+        pw = np.empty(n, np.uint64)
+        pw[0] = 1
+        if n > 1:
+            pw[1:] = np.cumprod(np.full(n - 1, DIGEST_P, np.uint64))
+        return n, int((x * pw[::-1]).sum(dtype=np.uint64))
 
 
 def digest_concat(parts):
@@ -347,6 +371,7 @@ def scan(data, threads=1, mode="decode", stringency=STRICT, granularity=4096, ma
         sbi = C.string_at(out, olen.value)
         L.orc_free(out)
     d = {f: getattr(r, f) for f, _ in _ScanResult._fields_}
+    d["field_digest"] = dict(zip(_ScanResult.FIELDS, list(r.field_digest)))
     d["rc"] = rc
     return d, sbi
 
@@ -361,6 +386,7 @@ def scan_records(data, cap, threads=1, stringency=STRICT):
     r = _ScanResult()
     rc = L.orc_scan_records(ptr, n, threads, stringency, cap, keys.ctypes.data, voffs.ctypes.data, C.byref(r))
     d = {f: getattr(r, f) for f, _ in _ScanResult._fields_}
+    d["field_digest"] = dict(zip(_ScanResult.FIELDS, list(r.field_digest)))
     d["rc"] = rc
     k = int(r.records)
     return d, keys[:k], voffs[:k]

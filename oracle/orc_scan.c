@@ -145,6 +145,9 @@ typedef struct {
   int status;
   uint64_t n, key_xor, voff_sum;
   uint64_t kdig, vdig;      /* order-sensitive digests of this range (Horner) */
+  uint64_t fdig[ORC_N_FIELDS]; /* the same of each fixed field (orc_scan_result.field_digest order) */
+  uint32_t rcrc;            /* zlib crc32 of the records' rests, back to back */
+  uint64_t rlen;            /* their bytes */
   uint64_t *voffs, vcap;    /* index mode (and keep): every record voff */
   int64_t *keys;            /* decode mode with keep: every record key (capacity vcap) */
   int keep;                 /* decode mode: keep every voff and key */
@@ -197,6 +200,9 @@ static void s_walk(stask *t, sreader *r) {
   uint64_t q = t->entry;
   t->n = t->key_xor = t->voff_sum = 0;
   t->kdig = t->vdig = 0;
+  memset(t->fdig, 0, sizeof t->fdig);
+  t->rcrc = (uint32_t)crc32(0L, Z_NULL, 0);
+  t->rlen = 0;
   t->stopped = 0;
   t->status = ORC_OK;
   int first = 1;  /* reader: the split start follows a seek (no dead check) */
@@ -238,6 +244,15 @@ static void s_walk(stask *t, sreader *r) {
       t->voff_sum += v;
       t->kdig = t->kdig * ORC_DIGEST_P + s_dmix(key);
       t->vdig = t->vdig * ORC_DIGEST_P + s_dmix(v);
+      /* the fixed fields (signed ones sign-extended to 64 bits) and the rest
+       * (LazyBAMRecordFactory.createBAMRecord's arguments) */
+      const uint64_t fv[ORC_N_FIELDS] = {
+          (uint64_t)(int64_t)ref, (uint64_t)(int64_t)s_rdi32(x + 8), x[12], x[13], (uint64_t)(x[14] | (x[15] << 8)),
+          (uint64_t)(x[16] | (x[17] << 8)), flag, (uint64_t)(int64_t)s_rdi32(x + 20), (uint64_t)(int64_t)nref,
+          (uint64_t)(int64_t)s_rdi32(x + 28), (uint64_t)(int64_t)s_rdi32(x + 32)};
+      for (int f = 0; f < ORC_N_FIELDS; f++) t->fdig[f] = t->fdig[f] * ORC_DIGEST_P + s_dmix(fv[f]);
+      t->rcrc = (uint32_t)crc32(t->rcrc, x + 36, (uInt)(bs - 32));
+      t->rlen += (uint64_t)(bs - 32);
       if (t->keep) {
         if (t->n == t->vcap) {
           t->vcap = t->vcap ? 2 * t->vcap : 1 << 16;
@@ -428,6 +443,9 @@ static int scan_impl(const uint8_t *file, uint64_t len, int threads, int mode, i
           t->n = 0;
           t->key_xor = t->voff_sum = 0;
           t->kdig = t->vdig = 0;
+          memset(t->fdig, 0, sizeof t->fdig);
+          t->rcrc = (uint32_t)crc32(0L, Z_NULL, 0);
+          t->rlen = 0;
           t->exit = t->entry;
           t->stopped = 0;
           t->status = ORC_OK;
@@ -448,6 +466,9 @@ static int scan_impl(const uint8_t *file, uint64_t len, int threads, int mode, i
     const uint64_t w = s_pow(ORC_DIGEST_P, t->n);
     res->key_digest = res->key_digest * w + t->kdig;
     res->voff_digest = res->voff_digest * w + t->vdig;
+    for (int f = 0; f < ORC_N_FIELDS; f++) res->field_digest[f] = res->field_digest[f] * w + t->fdig[f];
+    res->rest_crc = res->rest_bytes ? (uint32_t)crc32_combine(res->rest_crc, t->rcrc, (z_off_t)t->rlen) : t->rcrc;
+    res->rest_bytes += t->rlen;
     if (mode == 1 && sbi) {
       for (uint64_t j = 0; j < t->n; j++) {
         if ((ordinal + j + 1) % (uint64_t)g == 0) {

@@ -396,3 +396,31 @@ def test_long_cigar_validation_matches_oracle(case):
             got = f.decode_all(raise_on_error=False)
         assert got["status"] == want_rc, (case, stringency)
         assert_same_records(got, want)
+
+
+@pytest.mark.parametrize("cap", [150_000, 1])
+def test_bounded_batches_cap_their_rest_bytes(monkeypatch, cap):
+    """A bounded batch hands its rests to Java as one direct ByteBuffer (int
+    capacity, int positions: GpuBAMRecordReader.recordAt): the cursor ends a
+    batch before its rests pass the cap (2 GiB; HBAM_MAX_BATCH_BYTES lowers
+    it here), one record at least, and the batches still cover the split in
+    order.  Long reads (10-50 kb) reach a 150 KB cap every few records."""
+    data, _ = synth.make_bam(80, mode="long")
+    s = orc.Stream(data)
+    rc, want = s.decode_all()
+    assert rc == 0
+    monkeypatch.setenv("HBAM_MAX_BATCH_BYTES", str(cap))
+    with hbam.BamFile(data) as f:
+        first = f.header()["first_record_voff"]
+        got = list(f.iter_batches(first, ALL, max_records=1 << 20))
+    assert len(got) > 4
+    for b in got:
+        assert b["status"] == 0
+        assert len(b["data"]) <= cap or len(b["key"]) == 1
+    keys = np.concatenate([b["key"] for b in got])
+    voffs = np.concatenate([b["voff"] for b in got])
+    np.testing.assert_array_equal(keys, want["key"])
+    np.testing.assert_array_equal(voffs, want["voff"])
+    u = s.data
+    rests = b"".join(u[o + 36:o + 36 + n] for o, n in zip(want["offset"].tolist(), want["rest_len"].tolist()))
+    assert b"".join(b["data"] for b in got) == rests

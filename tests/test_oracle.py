@@ -152,3 +152,26 @@ def test_scan_digests_are_order_sensitive_and_compose():
     assert d["rc"] == 0
     np.testing.assert_array_equal(k, want["key"])
     np.testing.assert_array_equal(v, want["voff"])
+
+
+def test_scan_field_and_rest_digests():
+    """orc_scan's per-field digests and rest crc32 (the at-scale parity of
+    tests/test_gpu_large.py): equal, at any thread count, to the digests of
+    the single-threaded oracle's columns and to the crc32 of its rests in
+    record order; the vectorized digest equals the scalar one."""
+    import zlib
+    from hbam import synth
+    data, _ = synth.make_bam(5000, as_numpy=True, block_payload=8192)
+    s = orc.Stream(data.tobytes())
+    rc, want = s.decode_all()
+    assert rc == 0
+    u = s.data
+    rests = b"".join(u[o + 36:o + 36 + n] for o, n in zip(want["offset"].tolist(), want["rest_len"].tolist()))
+    for threads in (1, 4):
+        r, _ = orc.scan(data, threads=threads)
+        assert r["rc"] == 0
+        for f in orc._ScanResult.FIELDS:
+            assert r["field_digest"][f] == orc.digest_np(want[f])[1], f
+        assert r["rest_bytes"] == len(rests) and r["rest_crc"] == zlib.crc32(rests)
+    v = want["tlen"]
+    assert orc.digest_np(v)[1] == orc.digest([int(x) & ((1 << 64) - 1) for x in v.astype(np.int64)])
