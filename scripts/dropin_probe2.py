@@ -15,6 +15,11 @@ from hbam import synth  # noqa: E402
 ALL = (1 << 64) - 1
 
 
+def mark(what):
+    """A phase marker in both clocks a profiler trace may use (qtrace_summary.py)."""
+    print(f"MARK {what} mono={time.monotonic_ns()} boot={time.clock_gettime_ns(time.CLOCK_BOOTTIME)}", flush=True)
+
+
 def link_rates():
     import torch
     n = 1 << 32
@@ -118,9 +123,11 @@ def main():
             print("after", step, flush=True)
             with hbam.BamFile(path=path) as f:
                 first = f.header()["first_record_voff"]
+                mark(f"mapped{rep}_begin")
                 t = time.perf_counter()
                 m, ts = batches(f, first, 1 << 20)
                 dt = time.perf_counter() - t
+                mark(f"mapped{rep}_end")
                 print(f"mapped rep {rep}: {m} records {dt:.3f}s {info['uncompressed'] / dt / 1e9:.1f} GB/s batches ms {ts}",
                       flush=True)
                 f.prefetch(0, f.size)

@@ -32,6 +32,24 @@ for s in $STEPS; do
       timeout -k 10 600 python -u bench.py --steps 5 --warmup 2 --no-pmc --extras dropin_end_to_end --c3-gb 20 \
         > $OUT/bench_host.json 2> $OUT/bench_host.err || { echo "bench failed"; tail -30 $OUT/bench_host.err; exit 2; }
       python3 -c "import json,sys; d=json.load(open('$OUT/bench_host.json')); e=d['extra']; print(json.dumps(e['dropin_end_to_end'])); c=e['c3_c5_60GB']; print(json.dumps({k: c.get(k) for k in ('c3_streamed_from_host','value','matches_oracle')}))" ;;
+    large)
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_large.py tests/test_gpu_windows.py -x -q -s --timeout 500 \
+        --timeout-method thread > $OUT/pytest_large.log 2>&1 || { echo "large tests failed"; tail -40 $OUT/pytest_large.log; exit 1; }
+      tail -3 $OUT/pytest_large.log ;;
+    qtrace)
+      # which hardware queue each drop-in kernel and copy lands on, before and
+      # after hbam_gpu_run_streamed (the slowed next context)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace \
+        --output-format csv -d $OUT/qtrace -- python3 $R/scripts/dropin_probe2.py 10000000 --torch \
+        --steps none,run_streamed,none,none > $OUT/qtrace.log 2>&1) \
+        || { echo "qtrace failed"; tail -30 $OUT/qtrace.log; exit 4; }
+      grep -E "^(mapped|resident)" $OUT/qtrace.log | cut -c1-90 ;;
+    variants)
+      # stage times + overlapped wall time per pass of the in-tree experiment builds
+      timeout -k 10 400 python -u scripts/probe_inflate.py 10000000 hadoop-bam_amd/lib/libhbam.so \
+        hadoop-bam_amd/lib/variants/*.so > $OUT/variants.log 2>&1 \
+        || { echo "variants failed"; tail -30 $OUT/variants.log; exit 5; }
+      cat $OUT/variants.log ;;
     rehearsal)
       timeout -k 10 600 python -u bench.py --gpus 2 --dist-backend gloo --one-device --c3-gb 7 --steps 3 --warmup 1 \
         > $OUT/rehearsal.json 2> $OUT/rehearsal.err || { echo "rehearsal failed"; tail -30 $OUT/rehearsal.err; exit 3; }
