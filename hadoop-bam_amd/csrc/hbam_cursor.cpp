@@ -162,6 +162,21 @@ uint64_t SpanCursor::block_end(const std::vector<BlockInfo>& B, uint64_t pos) co
   return B[lo].coff + B[lo].csize;
 }
 
+// Window sizes of a bounded split: the first batch cannot leave before the
+// first window is copied and decoded, and nothing else overlaps that wait, so
+// the windows ramp up -- 1/8, 1/4, 1/2 of the drop-in window, then the whole
+// -- and the first batches cross PCIe while the larger windows decode
+// (HBAM_DROPIN_RAMP=0: every window full size).
+uint64_t SpanCursor::ramp_window(uint64_t full, uint64_t id) {
+  static const bool ramp = [] {
+    const char* e = getenv("HBAM_DROPIN_RAMP");
+    return !(e && e[0] == '0');
+  }();
+  constexpr uint64_t kMinRamp = 16ull << 20;
+  if (!ramp || id >= 3 || full < 2 * kMinRamp) return full;
+  return std::max(kMinRamp, full >> (3 - id));
+}
+
 int SpanCursor::decode_window(BamFile& f, Carry from, bool cont, uint64_t m, Window* w, std::string* err) {
   // w's buffers are reused (reserve may hand a block back to the process
   // cache, dev_free does not wait for the device): no batch of the window
@@ -171,7 +186,9 @@ int SpanCursor::decode_window(BamFile& f, Carry from, bool cont, uint64_t m, Win
     if (s.busy && s.win == w->id) CCHK(hipEventSynchronize(s.done));
   Step st;
   ctrace("decode_window start", nwin_);
-  int rc = f.decode_step(from, vend_, hbam::kReader, true, cont, &st, f.dropin_window_bytes());
+  const uint64_t full = f.dropin_window_bytes();
+  int rc = f.decode_step(from, vend_, hbam::kReader, true, cont, &st, ramp_window(full, nwin_),
+                         ramp_window(full, nwin_ + 1));
   ctrace("decode_step done", st.span.n);
   if (rc != kOk) {
     *err = f.error();

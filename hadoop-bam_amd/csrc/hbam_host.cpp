@@ -214,6 +214,8 @@ int BamFile::prefetch(uint64_t lo, uint64_t hi) {
   return kOk;
 }
 
+namespace { void htrace(const char* what); }
+
 int BamFile::load_window(uint64_t lo, uint64_t hi, bool free_start, bool host_only) {
   hi = std::min(hi, src_.size);
   if (hi < lo) hi = lo;
@@ -232,6 +234,7 @@ int BamFile::load_window(uint64_t lo, uint64_t hi, bool free_start, bool host_on
     uint64_t copied = 0;
     rc = pipe_->load(src_.host, hi - lo, lo, hi == src_.size, &copied);
     src_.bytes_read += copied;
+    htrace(copied ? "window bytes copied to HBM" : "window bytes already in HBM");
   }
   if (rc == kOk) rc = pipe_->locate(free_start);
   if (rc != kOk) {
@@ -394,7 +397,7 @@ void htrace(const char* what) {  // HBAM_CURSOR_TRACE: developer timing lines on
 }  // namespace
 
 int BamFile::decode_step(Carry from, uint64_t vend, hbam::ChainMode mode, bool decode, bool continuation,
-                         Step* out, uint64_t window) {
+                         Step* out, uint64_t window, uint64_t next_window) {
   htrace("decode_step");
   *out = Step();
   Carry c = from;
@@ -419,9 +422,11 @@ int BamFile::decode_step(Carry from, uint64_t vend, hbam::ChainMode mode, bool d
       // blocks before win_hi_), so it ends up to that tail short of
       // win_hi_ + span_w: stage that much less, or the bytes past its end
       // would be copied again by the window after it
+      // (next_window: the caller's next window is a different size)
+      const uint64_t nw = next_window ? std::max<uint64_t>(next_window, 1ull << 16) : span_w;
       const uint64_t s_lo = win_hi_;
-      const uint64_t tail = std::min<uint64_t>(span_w / 2, 4 * 65536);
-      uint64_t s_hi = std::min(src_.size, s_lo + span_w - tail);
+      const uint64_t tail = std::min<uint64_t>(nw / 2, 4 * 65536);
+      uint64_t s_hi = std::min(src_.size, s_lo + nw - tail);
       if (clamp) s_hi = std::min(s_hi, std::max((vend >> 16) + 0x20000, s_lo));
       const bool resident = src_.dev.p && s_lo >= src_.dev_lo && s_hi <= src_.dev_hi;
       if (s_hi > s_lo && !resident) {

@@ -144,9 +144,11 @@ class BamFile {
   // Decode the part of FileVirtualSplit [.., vend) that starts at `from`
   // and lies in one window.  continuation: `from` is the carry of the
   // previous step (not a reader seek).
-  // window: compressed bytes per window (0 = window_bytes())
+  // window: compressed bytes per window (0 = window_bytes()); next_window:
+  // the size of the caller's next window, staged while this one decodes
+  // (0 = window)
   int decode_step(Carry from, uint64_t vend, hbam::ChainMode mode, bool decode, bool continuation,
-                  Step* out, uint64_t window = 0);
+                  Step* out, uint64_t window = 0, uint64_t next_window = 0);
   // window of the drop-in batch path (hbam_decode_span): hadoopbam.gpu.window-bytes
   // when set, else kDropinWindowBytes -- several windows per split, so that
   // one window's batches cross PCIe while the next decodes
@@ -397,6 +399,7 @@ class SpanCursor {
   };
   int ensure_streams(hbam::Pipeline& p, std::string* err);
   int decode_window(BamFile& f, Carry from, bool cont, uint64_t m, Window* w, std::string* err);
+  static uint64_t ramp_window(uint64_t full, uint64_t id);
   int issue(const Window& w, uint64_t k, uint64_t m, Slot* s, std::string* err);
   // m capped so that the batch's rest bytes fit a Java direct buffer (an int
   // capacity and int positions: GpuBAMRecordReader.recordAt): the largest

@@ -1239,7 +1239,10 @@ constexpr uint32_t kHuffStaticBytes = kHuffLdsBytes + kHuffCtlBytes;
 constexpr uint32_t kHuffStageCap = kHuffStageMaxLds - kHuffStaticBytes;
 static_assert(kHuffStageCap % 16 == 0 && kHuffStageCap >= 16 * 1024, "phase-A LDS budget");
 
-constexpr int kHuffWavesPerSimd = 4;  // VGPR cap 128 (no spills); LDS admits 4 staged workgroups per CU
+#ifndef HBAM_HUFF_WAVES_PER_SIMD
+#define HBAM_HUFF_WAVES_PER_SIMD 4
+#endif
+constexpr int kHuffWavesPerSimd = HBAM_HUFF_WAVES_PER_SIMD;  // VGPR cap 128 (no spills); LDS admits 4 staged workgroups per CU
 // One decode round of one BGZF block (the body of k_inflate_huff), reading the
 // compressed bits from an LDS copy of the block (STAGE) or from HBM/L2.
 template <bool STAGE>
@@ -3041,6 +3044,114 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, uint32_t src) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// The k_rec_count rules for the listed record at q (one lane): *stop = the
+// block's count ends at this record (*counted: the record itself counts),
+// *s = its status, *nd = bytes past the inflated range the record needs,
+// *long_cigar = its cigar was left to record_invalid_wave.
+template <int MODE>
+__device__ __forceinline__ void check_listed(const ChainEnv& E, uint64_t q, uint64_t lim, bool first, bool light,
+                                             bool* stop, bool* counted, int* s, uint64_t* nd, bool* long_cigar) {
+  const uint64_t avail = E.e_true - q;
+  if (q >= lim) {
+    *stop = true;  // outside the span
+  } else if (light && !dead_near(E, q)) {
+    // all rules pass without reading the record
+  } else if (MODE == kReader) {
+    if (!first && is_dead(E, q)) {
+      *stop = true;  // readInt at an exhausted block + empty block: EOF
+    } else if (avail < 4) {
+      *stop = true;
+    } else if (q + 4 > E.e_inf) {
+      *stop = true;
+      *nd = q + 4;
+    } else {
+      const int32_t bs = (int32_t)ldu32(E.u, q);
+      if (bs < 32) {
+        *stop = true;
+        *s = kErrFormat;
+      } else if (dead_in_record(E, q, bs) || avail - 4 < (uint64_t)bs) {
+        *stop = true;
+        *s = kErrTrunc;
+      } else if (q + 4 + (uint64_t)bs > E.e_inf) {
+        *stop = true;
+        *nd = q + 4 + (uint64_t)bs;
+      } else {
+        const int32_t ref = (int32_t)ldu32(E.u, q + 4), nref = (int32_t)ldu32(E.u, q + 24);
+        if (ref < -1 || ref >= E.n_ref || nref < -1 || nref >= E.n_ref) {
+          *stop = true;
+          *s = kErrArg;
+        } else if (E.validate && record_invalid(E, q, bs, E.validate == 2, long_cigar)) {
+          *stop = true;
+          *s = kErrFormat;
+        }
+      }
+    }
+  } else {
+    if (is_dead(E, q)) {
+      *stop = true;
+    } else if (avail < 4) {
+      *stop = true;
+      if (avail > 0) *s = kErrIO;  // "less than 4 bytes long"
+    } else if (q + 4 > E.e_inf) {
+      *stop = true;
+      *nd = q + 4;
+    } else {
+      const int32_t bs = (int32_t)ldu32(E.u, q);
+      if (bs > 0 && ((uint64_t)bs > avail - 4 || is_dead(E, q + 4))) {
+        *stop = true;
+        *counted = true;
+        *s = kErrIO;  // "Skip failed"
+      }
+    }
+  }
+}
+
+// One block's listed records checked by its wave: *count = the records before
+// the first stop (plus that record when it counts), *st = the stop's status,
+// *need = the largest position a stopped record needs past the inflated range
+// (0: none); returns whether records before the stop left long cigars to
+// record_invalid_wave.
+template <int MODE>
+__device__ __forceinline__ bool check_block(const ChainEnv& E, uint32_t i, uint64_t e, const uint32_t* __restrict__ wcnt,
+                                            const uint16_t* __restrict__ list, uint32_t* count, int* st,
+                                            uint64_t* need) {
+  const uint32_t lane = lane_id();
+  *count = 0;
+  *st = kOk;
+  *need = 0;
+  bool long_cigar = false;  // a record before the stop left to record_invalid_wave (lane-local)
+  if (e == kNone) return false;
+  const BlockInfo b = E.blocks[E.k0 + i];
+  const uint64_t lim = min(b.ustart + b.isize, E.q_end);
+  const uint32_t wc = wcnt[i];
+  const uint32_t n = min(wc & kListCountMask, kListCap);
+  // a plausible() list on fully inflated data already satisfies every rule
+  // that reads the record (block_size >= 32, refID / mate refID in range,
+  // record inside the stream): only span end and dead positions remain
+  const bool light = (wc & kListPlausible) && E.e_inf == E.e_true && (MODE != kReader || E.validate == 0);
+  const uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
+  *count = n;
+  for (uint32_t r0 = 0; r0 < n; r0 += 64) {
+    const uint32_t r = r0 + lane;
+    bool stop = false, counted = false;
+    int s = kOk;
+    uint64_t nd = 0;
+    if (r < n) {
+      const uint64_t q = b.ustart + L[r];
+      check_listed<MODE>(E, q, lim, r == 0 && q == E.p0, light, &stop, &counted, &s, &nd, &long_cigar);
+    }
+    const uint64_t m = __ballot(stop);
+    if (m) {
+      const uint32_t f = (uint32_t)__ffsll((long long)m) - 1;
+      *count = r0 + f + (uint32_t)__shfl((int)counted, (int)f, 64);
+      *st = __shfl(s, (int)f, 64);
+      *need = shfl_u64(nd, f);
+      break;
+    }
+  }
+  return __ballot(long_cigar) != 0;
+}
+
 // The k_rec_count rules, one lane per listed record.
 template <int MODE>
 __global__ __launch_bounds__(64) void k_rec_check(ChainEnv E, const uint64_t* __restrict__ entry,
@@ -3049,97 +3160,12 @@ __global__ __launch_bounds__(64) void k_rec_check(ChainEnv E, const uint64_t* __
                                                   int32_t* __restrict__ err, unsigned long long* __restrict__ need,
                                                   uint8_t* __restrict__ has_long) {
   const uint32_t i = blockIdx.x;
-  const uint32_t lane = lane_id();
-  const uint64_t e = entry[i];
-  uint32_t count = 0;
-  int st = kOk;
-  bool long_cigar = false;  // a record before the stop left to k_rec_check_long (lane-local)
-  if (e != kNone) {
-    const BlockInfo b = E.blocks[E.k0 + i];
-    const uint64_t lim = min(b.ustart + b.isize, E.q_end);
-    const uint32_t wc = wcnt[i];
-    const uint32_t n = min(wc & kListCountMask, kListCap);
-    // a plausible() list on fully inflated data already satisfies every rule
-    // that reads the record (block_size >= 32, refID / mate refID in range,
-    // record inside the stream): only span end and dead positions remain
-    const bool light = (wc & kListPlausible) && E.e_inf == E.e_true && (MODE != kReader || E.validate == 0);
-    const uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
-    count = n;
-    for (uint32_t r0 = 0; r0 < n; r0 += 64) {
-      const uint32_t r = r0 + lane;
-      bool stop = false, counted = false;
-      int s = kOk;
-      uint64_t nd = 0;
-      if (r < n) {
-        const uint64_t q = b.ustart + L[r];
-        const uint64_t avail = E.e_true - q;
-        if (q >= lim) {
-          stop = true;  // outside the span
-        } else if (light && !dead_near(E, q)) {
-          // all rules pass without reading the record
-        } else if (MODE == kReader) {
-          const bool first = r == 0 && q == E.p0;  // first record follows a seek
-          if (!first && is_dead(E, q)) {
-            stop = true;  // readInt at an exhausted block + empty block: EOF
-          } else if (avail < 4) {
-            stop = true;
-          } else if (q + 4 > E.e_inf) {
-            stop = true;
-            nd = q + 4;
-          } else {
-            const int32_t bs = (int32_t)ldu32(E.u, q);
-            if (bs < 32) {
-              stop = true;
-              s = kErrFormat;
-            } else if (dead_in_record(E, q, bs) || avail - 4 < (uint64_t)bs) {
-              stop = true;
-              s = kErrTrunc;
-            } else if (q + 4 + (uint64_t)bs > E.e_inf) {
-              stop = true;
-              nd = q + 4 + (uint64_t)bs;
-            } else {
-              const int32_t ref = (int32_t)ldu32(E.u, q + 4), nref = (int32_t)ldu32(E.u, q + 24);
-              if (ref < -1 || ref >= E.n_ref || nref < -1 || nref >= E.n_ref) {
-                stop = true;
-                s = kErrArg;
-              } else if (E.validate && record_invalid(E, q, bs, E.validate == 2, &long_cigar)) {
-                stop = true;
-                s = kErrFormat;
-              }
-            }
-          }
-        } else {
-          if (is_dead(E, q)) {
-            stop = true;
-          } else if (avail < 4) {
-            stop = true;
-            if (avail > 0) s = kErrIO;  // "less than 4 bytes long"
-          } else if (q + 4 > E.e_inf) {
-            stop = true;
-            nd = q + 4;
-          } else {
-            const int32_t bs = (int32_t)ldu32(E.u, q);
-            if (bs > 0 && ((uint64_t)bs > avail - 4 || is_dead(E, q + 4))) {
-              stop = true;
-              counted = true;
-              s = kErrIO;  // "Skip failed"
-            }
-          }
-        }
-      }
-      const uint64_t m = __ballot(stop);
-      if (m) {
-        const uint32_t f = (uint32_t)__ffsll((long long)m) - 1;
-        count = r0 + f + (uint32_t)__shfl((int)counted, (int)f, 64);
-        st = __shfl(s, (int)f, 64);
-        const uint64_t fnd = shfl_u64(nd, f);
-        if (lane == 0 && fnd) atomicMax(need, (unsigned long long)fnd);
-        break;
-      }
-    }
-  }
-  const bool any_long = __ballot(long_cigar) != 0;
-  if (lane == 0) {
+  uint32_t count;
+  int st;
+  uint64_t nd;
+  const bool any_long = check_block<MODE>(E, i, entry[i], wcnt, list, &count, &st, &nd);
+  if (lane_id() == 0) {
+    if (nd) atomicMax(need, (unsigned long long)nd);
     cnt[i] = count;
     err[i] = st;
     if (MODE == kReader) {
@@ -3194,6 +3220,84 @@ __global__ __launch_bounds__(64) void k_rec_out(ChainEnv E, const uint32_t* __re
   for (uint32_t r = lane_id(); r < n; r += 64) {
     const uint32_t off = L[r];
     const uint64_t q = b.ustart + off, o = o0 + r;
+    rec_pos[o] = q;
+    rec_voff[o] = (b.coff << 16) | off;
+    if (DECODE) decode_record(E.u, q, o, col);
+  }
+}
+
+// Record check and output in one pass (the list path of decode_span_pos):
+// k_rec_check + k_rec_check_long + k_rec_out, one wave per block, so a
+// block's records are read from HBM once after inflate and written out while
+// they are in L2.  A block writes its records at base[i], the exclusive scan
+// of the lists' counts: the true offsets whenever every block before the
+// first one that stops early (a failure, the span end, the window end) keeps
+// its whole list -- the normal case, with no wait on other blocks.  The
+// launch reports what the host needs to check that:
+//   bad[0]   min over blocks that stop early or fail of (i << 40 | base[i] +
+//            count): the first such block and the records up to its stop
+//   flags[0] the first failing block (k_first_error_i32), flags[1] the last
+//            block with records + 1
+// The offsets hold iff no block after the first early stop has records, or
+// that block failed (the records after it are dropped); otherwise the host
+// rescans the counts written to cnt[] and writes the outputs again
+// (k_rec_out).  cnt[] / err[] / need are k_rec_check's.
+constexpr int kBadShift = 40;
+
+template <int MODE, bool DECODE>
+__global__ __launch_bounds__(64) void k_rec_check_out(ChainEnv E, const uint64_t* __restrict__ entry,
+                                                      const uint32_t* __restrict__ wcnt,
+                                                      const uint16_t* __restrict__ list,
+                                                      const uint64_t* __restrict__ base, uint32_t* __restrict__ cnt,
+                                                      int32_t* __restrict__ err, unsigned long long* __restrict__ need,
+                                                      unsigned long long* __restrict__ bad,
+                                                      uint32_t* __restrict__ flags, uint64_t* __restrict__ rec_pos,
+                                                      uint64_t* __restrict__ rec_voff, Columns col, uint64_t cap) {
+  const uint32_t lane = lane_id();
+  const uint32_t i = blockIdx.x;
+  const uint64_t e = entry[i];
+  uint32_t count;
+  int st;
+  uint64_t nd;
+  const bool any_long = check_block<MODE>(E, i, e, wcnt, list, &count, &st, &nd);
+  const BlockInfo b = E.blocks[E.k0 + i];
+  const uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
+  if (MODE == kReader && any_long) {
+    // cigars longer than kWaveCigarOps before the stop, a wave each in list
+    // order (k_rec_check_long): the first invalid one becomes the stop
+    for (uint32_t r0 = 0; r0 < count; r0 += 64) {
+      const uint32_t r = r0 + lane;
+      const uint64_t q = r < count ? b.ustart + L[r] : 0;
+      const bool lg = r < count && (ldu32(E.u, q + 16) & 0xffffu) > kWaveCigarOps;
+      bool hit = false;
+      for (uint64_t wm = __ballot(lg); wm && !hit; wm &= wm - 1) {
+        const uint32_t src = (uint32_t)__ffsll((long long)wm) - 1;
+        const uint64_t qq = shfl_u64(q, src);
+        if (record_invalid_wave(E, qq, (int32_t)ldu32(E.u, qq), E.validate == 2)) {
+          count = r0 + src;
+          st = kErrFormat;
+          nd = 0;
+          hit = true;
+        }
+      }
+      if (hit) break;
+    }
+  }
+  const uint32_t listed = e == kNone ? 0u : min(wcnt[i] & kListCountMask, kListCap);
+  const uint64_t o0 = base[i];
+  if (lane == 0) {
+    if (nd) atomicMax(need, (unsigned long long)nd);
+    cnt[i] = count;
+    err[i] = st;
+    if (count < listed || st != kOk)
+      atomicMin(bad, ((unsigned long long)i << kBadShift) | (unsigned long long)(o0 + count));
+    if (st != kOk) atomicMin(&flags[0], i);
+    if (count) atomicMax(&flags[1], i + 1);
+  }
+  for (uint32_t r = lane; r < count; r += 64) {
+    const uint32_t off = L[r];
+    const uint64_t q = b.ustart + off, o = o0 + r;
+    if (o >= cap) break;  // (sized from the lists' counts: not reached)
     rec_pos[o] = q;
     rec_voff[o] = (b.coff << 16) | off;
     if (DECODE) decode_record(E.u, q, o, col);
@@ -3676,6 +3780,58 @@ hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s) 
     default:
       return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+// *total += sum over blocks with an entry of their listed records (capped at kListCap)
+// cnt[i] = the records block i's list holds (0 off the chain): the
+// optimistic output counts k_rec_check_out's offsets are scanned from
+__global__ void k_list_counts(const uint64_t* __restrict__ entry, const uint32_t* __restrict__ wcnt, uint32_t nb,
+                              uint32_t* __restrict__ cnt) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nb) cnt[i] = entry[i] != kNone ? min(wcnt[i] & kListCountMask, kListCap) : 0u;
+}
+
+static ChainEnv chain_env(const ChainArgs& a) {
+  ChainEnv E;
+  E.u = a.u;
+  E.blocks = a.blocks;
+  E.e_inf = a.e_inf;
+  E.e_true = a.e_true;
+  E.p0 = a.p0;
+  E.q_end = a.q_end;
+  E.dead = a.dead;
+  E.ndead = a.ndead;
+  E.n_ref = a.n_ref;
+  E.k0 = a.k0;
+  E.k1 = a.k1;
+  E.validate = a.validate;
+  E.ref_len = a.ref_len;
+  return E;
+}
+
+hipError_t launch_list_counts(const ChainArgs& a, hipStream_t s) {
+  const uint32_t nb = a.k1 - a.k0;
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_list_counts, dim3((nb + 255) / 256), dim3(256), 0, s, a.entry, a.wcnt, nb, a.cnt);
+  return hipGetLastError();
+}
+
+hipError_t launch_rec_check_out(const ChainArgs& a, int mode, bool decode, const Columns& col, uint64_t cap,
+                                hipStream_t s) {
+  static_assert(kBadShift == kFusedBadShift, "hbam_launch.h kFusedBadShift");
+  const ChainEnv E = chain_env(a);
+  const uint32_t nb = a.k1 - a.k0;
+  if (nb == 0) return hipSuccess;
+  unsigned long long* need = a.need;
+  unsigned long long* bad = reinterpret_cast<unsigned long long*>(a.fuse_bad);
+#define HBAM_CO(M, D)                                                                                            \
+  hipLaunchKernelGGL((k_rec_check_out<M, D>), dim3(nb), dim3(64), 0, s, E, a.entry, a.wcnt, a.list, a.base, a.cnt, \
+                     a.err, need, bad, a.fuse_flags, a.rec_pos, a.rec_voff, col, cap)
+  if (mode == kReader && decode) HBAM_CO(kReader, true);
+  else if (mode == kReader) HBAM_CO(kReader, false);
+  else HBAM_CO(kIndexer, false);
+#undef HBAM_CO
   return hipGetLastError();
 }
 

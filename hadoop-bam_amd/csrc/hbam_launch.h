@@ -34,6 +34,9 @@ struct ChainArgs {
   uint16_t* list;       // kListCap u16 offsets (from ustart) per block
   uint32_t* counters;   // [0] hard link violations, [1] blocks to re-walk, [2] list overflow
   uint8_t* has_long;    // check stage: the block has records left to k_rec_check_long; [nb]: any block
+  // fused check + output (launch_rec_check_out)
+  uint64_t* fuse_bad;    // = ~0: min (i << kFusedBadShift | records up to i's stop) over blocks that stop early
+  uint32_t* fuse_flags;  // [0] first failing block = ~0, [1] last block with records + 1 = 0
 };
 constexpr uint32_t kListCap = 2048;              // >= 65536 / 36 + 2: every reader-mode record start
 constexpr uint64_t kForceEmpty = ~0ull - 1;      // force[]: the block holds no record start
@@ -91,6 +94,16 @@ hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb
 hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s);
 // positions, voffs and (decode) the SoA columns off the per-block lists, one wave per block
 hipError_t launch_rec_out(const ChainArgs& a, int mode, bool decode, const Columns& col, hipStream_t s);
+// a.cnt[i] = the records block i's list holds (0 off the chain): scanned into
+// a.base, the offsets launch_rec_check_out writes at
+hipError_t launch_list_counts(const ChainArgs& a, hipStream_t s);
+// kStageCheck + kStageCheckLong + launch_rec_out in one launch
+// (k_rec_check_out): cnt / err / need as the check, outputs at a.base[i] (the
+// scanned list counts), a.fuse_bad / a.fuse_flags as documented there; cap =
+// the rec_pos / rec_voff / column capacity
+hipError_t launch_rec_check_out(const ChainArgs& a, int mode, bool decode, const Columns& col, uint64_t cap,
+                                hipStream_t s);
+constexpr int kFusedBadShift = 40;
 hipError_t link_scan_bytes(uint32_t nb, size_t* bytes);
 hipError_t launch_rec_decode(const uint8_t* u, const uint64_t* rec_pos, uint64_t n, const Columns& col,
                              hipStream_t s);

@@ -16,7 +16,10 @@ namespace hbam {
 
 namespace {
 constexpr uint32_t kStreamInflateBlocks = 8192;  // run_streamed: blocks per inflate call
-constexpr uint32_t kInflateChunkBlocks = 32768;  // blocks per phase-A/B launch pair (16 K: -0.7 %, 8 K: -4 % on C2)
+#ifndef HBAM_INFLATE_CHUNK
+#define HBAM_INFLATE_CHUNK 32768
+#endif
+constexpr uint32_t kInflateChunkBlocks = HBAM_INFLATE_CHUNK;  // blocks per phase-A/B launch pair (16 K: -0.7 %, 8 K: -4 % on C2)
 constexpr int kMaxChainIters = 64;
 constexpr int kMaxLinkFix = 4;        // re-walk rounds before the serial link
 constexpr int kMaxFreeStarts = 64;    // header candidates tried by a free-start locate
@@ -59,7 +62,7 @@ Pipeline::Pipeline(int device) : device_(device) {
   own(own_file_, own_spare_, dblocks_, ref_len_, du_, tokens_[0], tokens_[1], hout_, tables_[0], tables_[1],
       tinfo_[0], tinfo_[1], g_, x_, x2_, entry_, base_arr_, summary_, dead_, cand_, sorted_, isz_, ust_, cnt_, flags_,
       errv_, need_, rec_pos_, rec_voff_, rcand_, force_, wcnt_, counters_, list_, hlong_, scan_tmp_, cols_, long_rec_,
-      long_n_, wbuf_, woffs_, wbad_, scalars_);
+      long_n_, wbuf_, woffs_, wbad_, scalars_, fuse_);
   for (auto& e : ev_) (void)hipEventCreate(&e);
   for (auto& e : sync_ev_) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   for (auto& e : tab_ev_) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -757,6 +760,16 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
   return decode_span_pos((uint64_t)sp, vend, mode, decode, out);
 }
 
+// HBAM_FUSED_RECORDS=0: the list path as separate launches (check, first
+// error, count scan, output), for A/B measurement
+static bool fused_record_pass() {
+  static const bool on = [] {
+    const char* e = getenv("HBAM_FUSED_RECORDS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool decode, SpanDev* out) {
   HIPCHK(hipSetDevice(device_));
   *out = SpanDev();
@@ -783,6 +796,12 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
   if (timing) HIPCHK(hipEventRecord(ev_[0], stream_));
   float infl_ms = 0, huff_ms = 0, lz_ms = 0, tab_ms = 0;
   bool lists = true;  // chain v2 lists hold every record start (no overflow)
+  const bool dec = decode && mode == kReader;
+  Columns c{};
+  // the list path: check + output in one launch (k_rec_check_out); its results
+  bool fused = false;
+  uint64_t fused_total = 0;
+  uint32_t fused_first = 0xffffffffu;
   for (int it = 0;; ++it) {
     if (it >= kMaxChainIters) return fail(kErrState, "record chain did not converge");
     int rc = inflate(k0, inf_end);
@@ -837,44 +856,127 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
     HIPCHK(launch_chain(a, mode, kStageWalk, stream_));  // candidates + lane-per-block walks
     // link: max-scan of the walk exits; re-walk blocks that are off the chain
     bool serial = false;
+    // HBAM_CURSOR_TRACE: the blocks the link check left off the chain
+    auto dump_off_chain = [&]() {
+      if (!getenv("HBAM_CURSOR_TRACE")) return;
+      std::vector<uint64_t> fv(nb), gv(nb), xv(nb), ev(nb), inv(nb);
+      (void)hipStreamSynchronize(stream_);
+      (void)hipMemcpy(fv.data(), force_.p, nb * 8, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(gv.data(), g_.p, nb * 8, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(xv.data(), x_.p, nb * 8, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(ev.data(), entry_.p, nb * 8, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(inv.data(), base_arr_.p, nb * 8, hipMemcpyDeviceToHost);
+      for (uint32_t i = 0, shown = 0; i < nb && shown < 8; ++i) {
+      if (fv[i] == ~0ull) continue;
+      const BlockInfo& b = hblocks_[a.k0 + i];
+      fprintf(stderr, "[chain]   block %u (of %u) ustart %llu end %llu: force %llx g %llx x %llx in %llx entry %llx\n",
+                i, nb, (unsigned long long)b.ustart, (unsigned long long)(b.ustart + b.isize),
+                (unsigned long long)fv[i], (unsigned long long)gv[i], (unsigned long long)xv[i],
+                (unsigned long long)inv[i], (unsigned long long)ev[i]);
+      ++shown;
+      }
+    };
     for (int fix = 0;; ++fix) {
       HIPCHK(hipMemsetAsync(counters_.p, 0, 8, stream_));
       HIPCHK(launch_chain(a, mode, kStageLinkCheck, stream_));
       uint32_t ctr[2] = {0, 0};
       HIPCHK(rb(ctr, counters_.p, 8, stream_));
       HIPCHK(rb_sync(stream_));
-      if (ctr[0]) { serial = true; break; }
+      if (ctr[0] || (ctr[1] && fix == kMaxLinkFix)) {
+        if (getenv("HBAM_CURSOR_TRACE"))
+          fprintf(stderr, "[chain] serial link: blocks [%u, %u) e_inf %llu e_true %llu p0 %llu rewalk round %d, "
+                  "%u blocks off the chain, serial request %u\n", a.k0, a.k1, (unsigned long long)a.e_inf,
+                  (unsigned long long)a.e_true, (unsigned long long)a.p0, fix, ctr[1], ctr[0]);
+        dump_off_chain();
+        serial = true;
+        break;
+      }
       if (ctr[1] == 0) break;
-      if (fix == kMaxLinkFix) { serial = true; break; }
+      if (getenv("HBAM_CURSOR_TRACE")) {
+        fprintf(stderr, "[chain] rewalk round %d: %u blocks off the chain\n", fix, ctr[1]);
+        dump_off_chain();
+      }
       ++link_rewalks_;
       HIPCHK(launch_chain(a, mode, kStageRewalk, stream_));
     }
     uint64_t sm[2] = {0, 0};
     unsigned long long need = 0;
+    // the lists' record counts scanned into base_arr_ (the output offsets of
+    // k_rec_check_out; their total bounds the span's records) and the list
+    // overflow flag come back with the chain's end in one host round trip
+    HIPCHK(fuse_.reserve(4));
+    uint64_t bound = 0, last_base = 0;
+    uint32_t ovf = 0, last_cnt = 0;
+    auto list_bound = [&]() -> hipError_t {
+      hipError_t e = launch_list_counts(a, stream_);
+      size_t tb = 0;
+      if (e == hipSuccess) e = scan_u32_to_u64(nullptr, &tb, cnt_.p, base_arr_.p, nb, stream_);
+      if (e == hipSuccess) e = scan_tmp_.reserve(tb + 16);
+      if (e == hipSuccess) e = scan_u32_to_u64(scan_tmp_.p, &tb, cnt_.p, base_arr_.p, nb, stream_);
+      if (e == hipSuccess) e = rb(&last_base, base_arr_.p + nb - 1, 8, stream_);
+      if (e == hipSuccess) e = rb(&last_cnt, cnt_.p + nb - 1, 4, stream_);
+      if (e == hipSuccess) e = rb(&ovf, counters_.p + 2, 4, stream_);
+      return e;
+    };
     if (serial) {  // exact serial link (writes entry[] + summary), then lists off entry[]
       ++link_fallbacks_;
       HIPCHK(launch_chain(a, mode, kStageSerialLink, stream_));
       HIPCHK(launch_chain(a, mode, kStageRewalkAll, stream_));
       HIPCHK(rb(sm, summary_.p, 16, stream_));
+      HIPCHK(list_bound());
+      HIPCHK(rb_sync(stream_));
     } else {  // final chain position = max of every walk exit; no stop
       uint64_t t[2] = {0, 0};
-      HIPCHK(rb(&t[0], base_arr_.p + nb - 1, 8, stream_));
+      HIPCHK(rb(&t[0], base_arr_.p + nb - 1, 8, stream_));  // (the link max-scan, before list_bound's scan)
       HIPCHK(rb(&t[1], x2_.p + nb - 1, 8, stream_));
+      HIPCHK(list_bound());
       HIPCHK(rb_sync(stream_));
       sm[0] = nb == 1 ? t[1] : std::max(t[0], t[1]);
       sm[1] = 0;
     }
-    uint32_t ovf = 0;
-    HIPCHK(rb(&ovf, counters_.p + 2, 4, stream_));
-    HIPCHK(rb_sync(stream_));
+    bound = last_base + last_cnt;
     lists = ovf == 0;
-    uint8_t long_left = 0;
-    HIPCHK(hipMemsetAsync(hlong_.p + nb, 0, 1, stream_));
-    HIPCHK(launch_chain(a, mode, lists ? kStageCheck : kStageCount, stream_));  // count + validate
-    HIPCHK(rb(&need, need_.p, 8, stream_));
-    HIPCHK(rb(&long_left, hlong_.p + nb, 1, stream_));
-    HIPCHK(rb_sync(stream_));
-    if (long_left) HIPCHK(launch_chain(a, mode, kStageCheckLong, stream_));  // long cigars, a wave each
+    fused = lists && fused_record_pass();
+    if (fused) {
+      // outputs sized by the lists' records, then check + positions + voffs +
+      // fields + keys in one launch, each block at its scanned list offset
+      HIPCHK(rec_pos_.reserve(bound + 1));
+      HIPCHK(rec_voff_.reserve(bound + 1));
+      if (dec) {
+        int rc = alloc_columns(bound, total_u_, &c);
+        if (rc != kOk) return rc;
+      }
+      HIPCHK(hipMemsetAsync(fuse_.p, 0xff, 12, stream_));  // early-stop key, first failing block: none
+      HIPCHK(hipMemsetAsync(fuse_.p + 3, 0, 4, stream_));   // last block with records + 1: none
+      a.fuse_bad = reinterpret_cast<uint64_t*>(fuse_.p);
+      a.fuse_flags = fuse_.p + 2;
+      a.rec_pos = rec_pos_.p;
+      a.rec_voff = rec_voff_.p;
+      if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
+      HIPCHK(launch_rec_check_out(a, mode, dec, c, bound + 1, stream_));
+      uint64_t bad = 0;
+      uint32_t fl[2] = {0, 0};
+      HIPCHK(rb(&need, need_.p, 8, stream_));
+      HIPCHK(rb(&bad, fuse_.p, 8, stream_));
+      HIPCHK(rb(fl, fuse_.p + 2, 8, stream_));
+      HIPCHK(rb_sync(stream_));
+      fused_first = fl[0];
+      if (bad == ~0ull) {
+        fused_total = bound;  // every block kept its whole list
+      } else {
+        const uint64_t k = bad >> kFusedBadShift;
+        if (fl[1] <= k + 1 || fl[0] == k) fused_total = bad & ((1ull << kFusedBadShift) - 1);
+        else fused = false;  // records after an early stop: the counts are rescanned (k_rec_out)
+      }
+    } else {
+      uint8_t long_left = 0;
+      HIPCHK(hipMemsetAsync(hlong_.p + nb, 0, 1, stream_));
+      HIPCHK(launch_chain(a, mode, lists ? kStageCheck : kStageCount, stream_));  // count + validate
+      HIPCHK(rb(&need, need_.p, 8, stream_));
+      HIPCHK(rb(&long_left, hlong_.p + nb, 1, stream_));
+      HIPCHK(rb_sync(stream_));
+      if (long_left) HIPCHK(launch_chain(a, mode, kStageCheckLong, stream_));  // long cigars, a wave each
+    }
     const uint64_t final_pos = sm[0];
     const bool stopped = sm[1] != 0;
     if (need > a.e_inf && inf_end < nblk) {  // a record needs bytes beyond the inflated range
@@ -895,16 +997,18 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
   const uint32_t nb = k1 - k0;
   // first failing block: records before it stand, later blocks are dropped
   const uint32_t none = 0xffffffffu;
-  HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags_.p + 3), (int)none, 1, stream_));
-  HIPCHK(launch_first_error_i32(errv_.p, nb, flags_.p + 3, stream_));
-  uint32_t first = none;
-  HIPCHK(rb(&first, flags_.p + 3, 4, stream_));
-  HIPCHK(rb_sync(stream_));
+  uint32_t first = fused_first;
+  if (!fused) {
+    HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags_.p + 3), (int)none, 1, stream_));
+    HIPCHK(launch_first_error_i32(errv_.p, nb, flags_.p + 3, stream_));
+    HIPCHK(rb(&first, flags_.p + 3, 4, stream_));
+    HIPCHK(rb_sync(stream_));
+  }
   if (first != none) {
     int32_t code = 0;
     HIPCHK(rb(&code, errv_.p + first, 4, stream_));
     HIPCHK(rb_sync(stream_));
-    HIPCHK(launch_truncate_counts(cnt_.p, nb, flags_.p + 3, stream_));
+    if (!fused) HIPCHK(launch_truncate_counts(cnt_.p, nb, flags_.p + 3, stream_));
     out->status = code;
     const BlockInfo& b = hblocks_[k0 + first];
     const char* what = code == kErrFormat ? "Invalid record (SAMFormatException)"
@@ -913,36 +1017,37 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
                                            : "Invalid alignment";
     out->error = std::string(what) + " (BGZF block at offset " + std::to_string(b.coff) + ")";
   }
-  HIPCHK(base_arr_.reserve(nb + 1));
-  size_t tb = 0;
-  HIPCHK(scan_u32_to_u64(nullptr, &tb, cnt_.p, base_arr_.p, nb, stream_));
-  HIPCHK(scan_tmp_.reserve(tb + 16));
-  HIPCHK(scan_u32_to_u64(scan_tmp_.p, &tb, cnt_.p, base_arr_.p, nb, stream_));
-  uint64_t last_base = 0;
-  uint32_t last_cnt = 0;
-  HIPCHK(rb(&last_base, base_arr_.p + nb - 1, 8, stream_));
-  HIPCHK(rb(&last_cnt, cnt_.p + nb - 1, 4, stream_));
-  HIPCHK(rb_sync(stream_));
-  const uint64_t total = last_base + last_cnt;
-  HIPCHK(rec_pos_.reserve(total + 1));
-  HIPCHK(rec_voff_.reserve(total + 1));
-  a.base = base_arr_.p;
-  a.rec_pos = rec_pos_.p;
-  a.rec_voff = rec_voff_.p;
+  uint64_t total = fused_total;
+  if (!fused) {
+    HIPCHK(base_arr_.reserve(nb + 1));
+    size_t tb = 0;
+    HIPCHK(scan_u32_to_u64(nullptr, &tb, cnt_.p, base_arr_.p, nb, stream_));
+    HIPCHK(scan_tmp_.reserve(tb + 16));
+    HIPCHK(scan_u32_to_u64(scan_tmp_.p, &tb, cnt_.p, base_arr_.p, nb, stream_));
+    uint64_t last_base = 0;
+    uint32_t last_cnt = 0;
+    HIPCHK(rb(&last_base, base_arr_.p + nb - 1, 8, stream_));
+    HIPCHK(rb(&last_cnt, cnt_.p + nb - 1, 4, stream_));
+    HIPCHK(rb_sync(stream_));
+    total = last_base + last_cnt;
+    HIPCHK(rec_pos_.reserve(total + 1));
+    HIPCHK(rec_voff_.reserve(total + 1));
+    a.base = base_arr_.p;
+    a.rec_pos = rec_pos_.p;
+    a.rec_voff = rec_voff_.p;
+    if (dec) {
+      int rc = alloc_columns(total, total_u_, &c);
+      if (rc != kOk) return rc;
+    }
+  }
   out->n = total;
   out->rec_pos = rec_pos_.p;
   out->rec_voff = rec_voff_.p;
-  const bool dec = decode && mode == kReader;
-  Columns c{};
-  if (dec) {
-    int rc = alloc_columns(total, total_u_, &c);
-    if (rc != kOk) return rc;
-    out->col = c;
-  }
-  if (lists) {  // positions + voffs (+ fused decode) straight off the per-block lists
+  if (dec) out->col = c;
+  if (!fused && lists) {  // positions + voffs (+ decode) off the per-block lists, after the count scan
     if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
     HIPCHK(launch_rec_out(a, mode, dec, c, stream_));
-  } else {      // a block listed more starts than kListCap: per-block walks
+  } else if (!fused) {  // a block listed more starts than kListCap: per-block walks
     HIPCHK(launch_chain(a, mode, kStageEmit, stream_));
     if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
     if (dec) HIPCHK(launch_rec_decode(du_.p, rec_pos_.p, total, c, stream_));

@@ -329,6 +329,7 @@ class Pipeline {
   DevBuf<uint32_t> wcnt_, counters_;
   DevBuf<uint16_t> list_;
   DevBuf<uint8_t> hlong_;  // check stage: blocks with records for k_rec_check_long
+  DevBuf<uint32_t> fuse_;  // k_rec_check_out: [0..1] early-stop key (u64), [2] first failing block, [3] last block with records + 1
   DevBuf<uint8_t> scan_tmp_;
   DevBuf<uint8_t> cols_;  // SoA backing store
   uint64_t cols_cap_ = 0;

@@ -1,6 +1,6 @@
 """Per-batch timing of the drop-in call (developer probe): hbam_decode_span in 1M-record
 batches from the mapped file and from a resident copy, every batch timed.
-usage: python scripts/dropin_probe2.py [records] [--torch] [--pinned]"""
+usage: python scripts/dropin_probe2.py [records] [--torch] [--pinned] [--smi] [--steps a,b+c,...]"""
 import os
 import sys
 import time
@@ -39,6 +39,72 @@ def link_rates():
     return out
 
 
+class Sampler:
+    """--smi: the GPU's clock levels (pp_dpm_sclk/mclk/fclk: the starred
+    level) and PCIe link speed / width from sysfs, every 20 ms while a marked
+    loop runs; each loop reports the distinct values it saw, with counts."""
+
+    FILES = ("pp_dpm_sclk", "pp_dpm_mclk", "pp_dpm_fclk", "current_link_speed", "current_link_width")
+
+    def __init__(self):
+        import glob
+        import threading
+        self.dev = None
+        try:
+            import torch
+            pr = torch.cuda.get_device_properties(0)
+            cand = "/sys/bus/pci/devices/%04x:%02x:%02x.0" % (getattr(pr, "pci_domain_id", 0), pr.pci_bus_id,
+                                                              pr.pci_device_id)
+            if os.path.exists(os.path.join(cand, "pp_dpm_sclk")):
+                self.dev = cand
+        except Exception:
+            pass
+        if self.dev is None:  # the first amdgpu device with clock files
+            c = sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk"))
+            self.dev = os.path.dirname(c[0]) if c else None
+        self.seen = {}
+        self.on = False
+        self.lock = threading.Lock()
+        threading.Thread(target=self.run, daemon=True).start()
+
+    def read(self):
+        out = {}
+        for f in self.FILES:
+            try:
+                txt = open(os.path.join(self.dev, f)).read()
+            except OSError:
+                continue
+            if f.startswith("pp_dpm"):
+                cur = [ln.split(":", 1)[1].replace("*", "").strip() for ln in txt.splitlines() if "*" in ln]
+                out[f[7:]] = cur[0] if cur else "?"
+            else:
+                out[f] = txt.strip()
+        return out
+
+    def run(self):
+        while True:
+            if self.on and self.dev:
+                v = self.read()
+                with self.lock:
+                    for k, x in v.items():
+                        d = self.seen.setdefault(k, {})
+                        d[x] = d.get(x, 0) + 1
+            time.sleep(0.02)
+
+    def start(self):
+        with self.lock:
+            self.seen = {}
+        self.on = True
+
+    def stop(self, label):
+        self.on = False
+        with self.lock:
+            print(f"SMI {label} dev={self.dev} {self.seen}", flush=True)
+
+
+SMI = None
+
+
 def batches(f, first, nrec):
     b = hbam.Batch()
     v, ts, n = first, [], 0
@@ -60,6 +126,10 @@ def main():
         import torch
         torch.cuda.init()
         torch.empty(1, device="cuda")
+    global SMI
+    if "--smi" in sys.argv:
+        SMI = Sampler()
+        print("SMI idle", SMI.dev, SMI.read() if SMI.dev else None, flush=True)
     data, info = synth.make_bam(n, as_numpy=True)
     path = "/dev/shm/hbam_dropin_probe2.bam"
     data.tofile(path)
@@ -124,9 +194,13 @@ def main():
             with hbam.BamFile(path=path) as f:
                 first = f.header()["first_record_voff"]
                 mark(f"mapped{rep}_begin")
+                if SMI:
+                    SMI.start()
                 t = time.perf_counter()
                 m, ts = batches(f, first, 1 << 20)
                 dt = time.perf_counter() - t
+                if SMI:
+                    SMI.stop(f"mapped{rep}")
                 mark(f"mapped{rep}_end")
                 print(f"mapped rep {rep}: {m} records {dt:.3f}s {info['uncompressed'] / dt / 1e9:.1f} GB/s batches ms {ts}",
                       flush=True)

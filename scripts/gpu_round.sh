@@ -41,15 +41,39 @@ for s in $STEPS; do
       # after hbam_gpu_run_streamed (the slowed next context)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace \
         --output-format csv -d $OUT/qtrace -- python3 $R/scripts/dropin_probe2.py 10000000 --torch \
-        --steps none,run_streamed,none,none > $OUT/qtrace.log 2>&1) \
+        --smi --steps none,run_streamed,none,none > $OUT/qtrace.log 2>&1) \
         || { echo "qtrace failed"; tail -30 $OUT/qtrace.log; exit 4; }
-      grep -E "^(mapped|resident)" $OUT/qtrace.log | cut -c1-90 ;;
+      grep -E "^(mapped|resident|SMI)" $OUT/qtrace.log | cut -c1-300 ;;
+    dropin_ab)
+      # the drop-in 1 M-batch loop, window ramp off / on (two fresh processes)
+      for r in 0 1; do
+        HBAM_DROPIN_RAMP=$r timeout -k 10 300 python -u scripts/dropin_probe2.py 10000000 --torch --steps none,none \
+          > $OUT/dropin_ramp$r.log 2>&1 || { echo "dropin probe failed"; tail -30 $OUT/dropin_ramp$r.log; exit 6; }
+        echo "ramp=$r"; grep -E "^(mapped|resident)" $OUT/dropin_ramp$r.log | cut -c1-120
+      done ;;
     variants)
-      # stage times + overlapped wall time per pass of the in-tree experiment builds
+      # stage times + overlapped wall time per pass: the default build, the
+      # in-tree experiment builds (lib/variants), the unfused record pass
       timeout -k 10 400 python -u scripts/probe_inflate.py 10000000 hadoop-bam_amd/lib/libhbam.so \
-        hadoop-bam_amd/lib/variants/*.so > $OUT/variants.log 2>&1 \
+        $(ls hadoop-bam_amd/lib/variants/*.so 2>/dev/null) > $OUT/variants.log 2>&1 \
         || { echo "variants failed"; tail -30 $OUT/variants.log; exit 5; }
+      HBAM_FUSED_RECORDS=0 timeout -k 10 200 python -u scripts/probe_inflate.py 10000000 >> $OUT/variants.log 2>&1 \
+        || { echo "unfused probe failed"; tail -30 $OUT/variants.log; exit 5; }
       cat $OUT/variants.log ;;
+    dtrace)
+      # host-side timeline of the drop-in 1 M-batch loop (window copies, decode
+      # steps, batch issues, serial-link fallbacks)
+      HBAM_CURSOR_TRACE=1 timeout -k 10 300 python -u scripts/dropin_probe2.py 10000000 --torch --steps none,none \
+        > $OUT/dtrace.log 2> $OUT/dtrace.err || { echo "dtrace failed"; tail -30 $OUT/dtrace.err; exit 7; }
+      grep -E "^(mapped|resident)" $OUT/dtrace.log | cut -c1-160; grep -c "serial link" $OUT/dtrace.err || true
+      HBAM_CURSOR_TRACE=1 timeout -k 10 200 python -u scripts/probe_inflate.py 10000000 > $OUT/ptrace.log \
+        2> $OUT/ptrace.err || { echo "ptrace failed"; tail -30 $OUT/ptrace.err; exit 7; }
+      grep -A3 "chain\]" $OUT/dtrace.err | head -40; grep "chain\]" $OUT/ptrace.err | head -24 ;;
+    collect)
+      # rocprofv3 kernel trace + stats and the PMC passes of bench.py --serial (profiles/collect.sh)
+      timeout -k 10 900 bash profiles/collect.sh $TAG > $OUT/collect.log 2>&1 \
+        || { echo "collect failed"; tail -30 $OUT/collect.log; exit 8; }
+      python3 -c "import json; d=json.load(open('$R/gpurun_out/prof_$TAG/summary.json'))['kernels']; [print('%-45s calls %4d main_avg_us %9.1f' % (k[:45], v['calls'], v.get('main_avg_ns', 0) / 1e3)) for k, v in sorted(d.items(), key=lambda x: -x[1].get('total_ns', 0))[:22]]" ;;
     rehearsal)
       timeout -k 10 600 python -u bench.py --gpus 2 --dist-backend gloo --one-device --c3-gb 7 --steps 3 --warmup 1 \
         > $OUT/rehearsal.json 2> $OUT/rehearsal.err || { echo "rehearsal failed"; tail -30 $OUT/rehearsal.err; exit 3; }
