@@ -164,17 +164,27 @@ uint64_t SpanCursor::block_end(const std::vector<BlockInfo>& B, uint64_t pos) co
 
 // Window sizes of a bounded split: the first batch cannot leave before the
 // first window is copied and decoded, and nothing else overlaps that wait, so
-// the windows ramp up -- 1/8, 1/4, 1/2 of the drop-in window, then the whole
-// -- and the first batches cross PCIe while the larger windows decode
-// (HBAM_DROPIN_RAMP=0: every window full size).
+// the windows ramp up from kRampFirst by kRampGrowth per window to the
+// drop-in window, and the first batches cross PCIe while the larger windows
+// decode.  HBAM_DROPIN_RAMP="<first MiB>,<growth>" (developer knob; "0": every
+// window full size).
 uint64_t SpanCursor::ramp_window(uint64_t full, uint64_t id) {
-  static const bool ramp = [] {
-    const char* e = getenv("HBAM_DROPIN_RAMP");
-    return !(e && e[0] == '0');
+  struct Ramp {
+    uint64_t first;
+    double growth;
+  };
+  static const Ramp r = [] {
+    Ramp v{32ull << 20, 2.0};
+    if (const char* e = getenv("HBAM_DROPIN_RAMP")) {
+      double mib = 0, g = 2.0;
+      if (sscanf(e, "%lf,%lf", &mib, &g) >= 1) v = Ramp{(uint64_t)(mib * (1 << 20)), g > 1.0 ? g : 2.0};
+    }
+    return v;
   }();
-  constexpr uint64_t kMinRamp = 16ull << 20;
-  if (!ramp || id >= 3 || full < 2 * kMinRamp) return full;
-  return std::max(kMinRamp, full >> (3 - id));
+  if (r.first == 0 || r.first >= full) return full;
+  double w = (double)r.first;
+  for (uint64_t k = 0; k < id && w < (double)full; ++k) w *= r.growth;
+  return w < (double)full ? ((uint64_t)w + 0xffff) & ~0xffffull : full;
 }
 
 int SpanCursor::decode_window(BamFile& f, Carry from, bool cont, uint64_t m, Window* w, std::string* err) {

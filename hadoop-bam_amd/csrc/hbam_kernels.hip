@@ -2804,6 +2804,23 @@ __global__ __launch_bounds__(64) void k_rec_cand(ChainEnv E, uint64_t* __restric
         break;
       }
     }
+    // A start 1-3 bytes before a true record reads that record's block_size
+    // shifted up by whole bytes (~2^8-2^24 times it) and, with refID 0, its
+    // fields stay in range: plausible2 passes and the walk leaves the block
+    // at once -- past the inflated end of a window it cannot be checked, and
+    // the link check then re-walks the block and the ones its far exit hid
+    // (one round each; C2 passes took two, drop-in windows fell back to the
+    // serial link).  When c's record leaves the block, a plausible2 start
+    // 1-3 bytes later whose record ends inside the block is taken instead.
+    if (c != kNone && lane == 0 && c + 4 + (uint64_t)(int32_t)ldu32(E.u, c) >= bend) {
+      for (uint32_t d = 1; d <= 3; ++d) {
+        const uint64_t q = c + d;
+        if (q + 36 <= E.e_inf && q + 4 + (uint64_t)(int32_t)ldu32(E.u, q) < bend && plausible2(E, q)) {
+          c = q;
+          break;
+        }
+      }
+    }
   }
   if (lane == 0) cand[blockIdx.x] = c;
 }

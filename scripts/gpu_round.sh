@@ -45,11 +45,11 @@ for s in $STEPS; do
         || { echo "qtrace failed"; tail -30 $OUT/qtrace.log; exit 4; }
       grep -E "^(mapped|resident|SMI)" $OUT/qtrace.log | cut -c1-300 ;;
     dropin_ab)
-      # the drop-in 1 M-batch loop, window ramp off / on (two fresh processes)
-      for r in 0 1; do
+      # the drop-in 1 M-batch loop under window ramps (HBAM_DROPIN_RAMP="first MiB,growth"; 0 = none)
+      for r in ${RAMPS:-0 32,2}; do
         HBAM_DROPIN_RAMP=$r timeout -k 10 300 python -u scripts/dropin_probe2.py 10000000 --torch --steps none,none \
-          > $OUT/dropin_ramp$r.log 2>&1 || { echo "dropin probe failed"; tail -30 $OUT/dropin_ramp$r.log; exit 6; }
-        echo "ramp=$r"; grep -E "^(mapped|resident)" $OUT/dropin_ramp$r.log | cut -c1-120
+          > $OUT/dropin_ramp_$r.log 2>&1 || { echo "dropin probe failed"; tail -30 $OUT/dropin_ramp_$r.log; exit 6; }
+        echo "ramp=$r"; grep -E "^(mapped|resident)" $OUT/dropin_ramp_$r.log | cut -c1-140
       done ;;
     variants)
       # stage times + overlapped wall time per pass: the default build, the
@@ -65,10 +65,10 @@ for s in $STEPS; do
       # steps, batch issues, serial-link fallbacks)
       HBAM_CURSOR_TRACE=1 timeout -k 10 300 python -u scripts/dropin_probe2.py 10000000 --torch --steps none,none \
         > $OUT/dtrace.log 2> $OUT/dtrace.err || { echo "dtrace failed"; tail -30 $OUT/dtrace.err; exit 7; }
-      grep -E "^(mapped|resident)" $OUT/dtrace.log | cut -c1-160; grep -c "serial link" $OUT/dtrace.err || true
+      grep -E "^(mapped|resident)" $OUT/dtrace.log | cut -c1-160; (grep -c "serial link" $OUT/dtrace.err || true)
       HBAM_CURSOR_TRACE=1 timeout -k 10 200 python -u scripts/probe_inflate.py 10000000 > $OUT/ptrace.log \
         2> $OUT/ptrace.err || { echo "ptrace failed"; tail -30 $OUT/ptrace.err; exit 7; }
-      grep -A3 "chain\]" $OUT/dtrace.err | head -40; grep "chain\]" $OUT/ptrace.err | head -24 ;;
+      (grep -A3 "chain\]" $OUT/dtrace.err | head -40; grep "chain\]" $OUT/ptrace.err | head -24) || true ;;
     collect)
       # rocprofv3 kernel trace + stats and the PMC passes of bench.py --serial (profiles/collect.sh)
       timeout -k 10 900 bash profiles/collect.sh $TAG > $OUT/collect.log 2>&1 \
