@@ -249,19 +249,23 @@ def pmc_traffic(path, vstart, vend, kernel):
 # side legs (N=1, rank 0)
 # ---------------------------------------------------------------------------
 def dropin_leg(path, first, records):
-    """The call a JVM makes (hbam.h): hbam_open(path) maps the file; each
-    hbam_decode_span batch copies its windows host->HBM, decodes them and
-    copies the 15 SoA columns plus the rest-of-record bytes into pinned host
-    memory (BAMRecordReader.nextKeyValue's data).  Each batch size opens the
-    split twice in this process: the first open allocates its page-locked
-    batch buffers (device blocks may come from the process cache, hbam_mem.h,
-    filled by the decodes before), the second finds both cached -- the case
-    of an executor that reads many splits."""
+    """The call a JVM makes (hbam.h): hbam_open(path) maps the file (with
+    opts.batch_records = the batch size, as GpuBAMRecordReader passes it, so
+    the page-locked batch slots are pinned on a helper thread from the open
+    on); each hbam_decode_span batch copies its windows host->HBM, decodes
+    them and copies the 15 SoA columns plus the rest-of-record bytes into
+    pinned host memory (BAMRecordReader.nextKeyValue's data).  Each batch
+    size opens the split twice in this process: the first open allocates its
+    page-locked batch buffers (device blocks may come from the process cache,
+    hbam_mem.h, filled by the decodes before), the second finds both cached
+    -- the case of an executor that reads many splits.  seconds = the batch
+    loop; open_seconds = the hbam_open before it (header read)."""
     import hbam
     res = {}
     for label, batch in (("batches_64K", 1 << 16), ("batches_1M", 1 << 20)):
         for run in ("first_open", "second_open"):
-            with hbam.BamFile(path=path) as f:
+            t0 = time.perf_counter()
+            with hbam.BamFile(path=path, batch_records=batch) as f:
                 t = time.perf_counter()
                 n, k, nbytes = f.scan_batches(first, ALL, batch)
                 dt = time.perf_counter() - t
@@ -269,6 +273,7 @@ def dropin_leg(path, first, records):
             assert n == records, (n, records)
             res.setdefault(label, {})[run] = {
                 "records": n, "batches": k, "rest_bytes_to_host": nbytes, "seconds": round(dt, 3),
+                "open_seconds": round(t - t0, 4),
                 "uncompressed_GBps": round(u / dt / 1e9, 3), "records_per_s": round(n / dt, 1)}
     # the same 1 M-record loop with the file read through hbam_open_reader (a
     # positioned-read callback, as a Hadoop FSDataInputStream through JNI):
@@ -277,7 +282,8 @@ def dropin_leg(path, first, records):
     try:
         size = os.fstat(fd).st_size
         for run in ("first_open", "second_open"):
-            with hbam.BamFile(reader=lambda off, n: os.pread(fd, n, off), size=size, parallel_reads=True) as f:
+            with hbam.BamFile(reader=lambda off, n: os.pread(fd, n, off), size=size, parallel_reads=True,
+                              batch_records=1 << 20) as f:
                 t = time.perf_counter()
                 n, k, nbytes = f.scan_batches(first, ALL, 1 << 20)
                 dt = time.perf_counter() - t

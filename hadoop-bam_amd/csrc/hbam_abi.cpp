@@ -66,11 +66,13 @@ OpenOptions options_of(const hbam_opts* opts, bool header) {
   r.stringency = o.stringency;
   r.window_bytes = o.window_bytes;
   r.parallel_reads = o.parallel_reads != 0;
+  r.batch_records = o.batch_records;
   r.parse_header = header;
   return r;
 }
 
-int finish_open(int rc, std::unique_ptr<BamFile>&& f, const std::string& err, hbam_ctx** out) {
+int finish_open(int rc, std::unique_ptr<BamFile>&& f, const std::string& err, hbam_ctx** out,
+                const hbam_opts* opts = nullptr) {
   auto* c = new hbam_ctx();
   *out = c;  // on failure the caller may read hbam_last_error, then must hbam_close
   if (rc != HBAM_OK) {
@@ -79,6 +81,9 @@ int finish_open(int rc, std::unique_ptr<BamFile>&& f, const std::string& err, hb
     return rc;
   }
   c->f = std::move(f);
+  // the caller's batch size is known: its page-locked batch slots are pinned
+  // on a helper thread while it goes on (the first hbam_decode_span joins it)
+  if (opts && opts->batch_records) c->cursor.start_prealloc(opts->batch_records, opts->device);
   return HBAM_OK;
 }
 
@@ -219,14 +224,14 @@ int hbam_open_mem(const void* data, uint64_t len, const hbam_opts* opts, hbam_ct
   std::unique_ptr<BamFile> f;
   std::string err;
   int rc = BamFile::open_memory(static_cast<const uint8_t*>(data), len, options_of(opts, true), &f, &err);
-  return finish_open(rc, std::move(f), err, out);
+  return finish_open(rc, std::move(f), err, out, opts);
 }
 
 int hbam_open_bgzf(const void* data, uint64_t len, const hbam_opts* opts, hbam_ctx** out) {
   std::unique_ptr<BamFile> f;
   std::string err;
   int rc = BamFile::open_memory(static_cast<const uint8_t*>(data), len, options_of(opts, false), &f, &err);
-  return finish_open(rc, std::move(f), err, out);
+  return finish_open(rc, std::move(f), err, out, opts);
 }
 
 int hbam_open(const char* path, const hbam_opts* opts, hbam_ctx** out) {
@@ -234,7 +239,7 @@ int hbam_open(const char* path, const hbam_opts* opts, hbam_ctx** out) {
   std::unique_ptr<BamFile> f;
   std::string err;
   int rc = BamFile::open_path(path, options_of(opts, true), &f, &err);
-  return finish_open(rc, std::move(f), err, out);
+  return finish_open(rc, std::move(f), err, out, opts);
 }
 
 int hbam_open_reader(uint64_t size, hbam_read_fn read, void* user, const hbam_opts* opts, hbam_ctx** out) {
@@ -243,7 +248,7 @@ int hbam_open_reader(uint64_t size, hbam_read_fn read, void* user, const hbam_op
   std::unique_ptr<BamFile> f;
   std::string err;
   int rc = BamFile::open_reader(size, read, user, options_of(opts, true), &f, &err);
-  return finish_open(rc, std::move(f), err, out);
+  return finish_open(rc, std::move(f), err, out, opts);
 }
 
 void hbam_close(hbam_ctx* ctx) { delete ctx; }

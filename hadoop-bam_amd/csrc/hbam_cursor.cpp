@@ -197,6 +197,15 @@ int SpanCursor::decode_window(BamFile& f, Carry from, bool cont, uint64_t m, Win
   Step st;
   ctrace("decode_window start", nwin_);
   const uint64_t full = f.dropin_window_bytes();
+  // ramped windows grow the staging buffer at every window: size it once for
+  // the whole window up front, while nothing is in flight
+  if (nwin_ == 0 && ramp_window(full, 0) < full) {
+    const int r = f.pipe().reserve_stage(std::min<uint64_t>(full, f.file_size()));
+    if (r != kOk) {
+      *err = f.pipe().error();
+      return r;
+    }
+  }
   int rc = f.decode_step(from, vend_, hbam::kReader, true, cont, &st, ramp_window(full, nwin_),
                          ramp_window(full, nwin_ + 1));
   ctrace("decode_step done", st.span.n);
@@ -244,11 +253,11 @@ int SpanCursor::decode_window(BamFile& f, Carry from, bool cont, uint64_t m, Win
 // pinning 2 x ~0.45 GB for 1 M-record batches took ~35 ms of the first
 // batch).  The estimate is the columns plus 400 B of rests per record
 // (150 bp reads: ~304); a bigger batch reallocates in issue() as before.
-void SpanCursor::start_prealloc(uint64_t m) {
+void SpanCursor::start_prealloc(uint64_t m, int device) {
   join_prealloc();
   const size_t est = ColLayout(m, false).bytes + 400 * m + 64;
   if (slot_[0].cap >= est && slot_[1].cap >= est) return;
-  const int dev = device_;
+  const int dev = device >= 0 ? device : device_;
   prealloc_ = std::thread([this, est, dev]() {
     if (hipSetDevice(dev) != hipSuccess) return;  // (the NUMA node of the allocation follows the device)
     for (auto& s : slot_) {

@@ -99,6 +99,7 @@ struct OpenOptions {
   int stringency = hbam::kStrict;
   uint64_t window_bytes = kDefaultWindowBytes;
   bool parallel_reads = false;  // a reader callback may run on several threads at once
+  uint64_t batch_records = 0;   // hbam_decode_span's max_records, when the caller knows it
 };
 
 // One opened BAM (or BGZF) file on one GPU.
@@ -362,6 +363,9 @@ class SpanCursor {
   // the same split without re-decoding.  *out stays valid until the next call.
   int next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t max_records, BatchView* out,
                  uint64_t* next_voff, std::string* err);
+  // pin both batch slots for batches of m records on a helper thread (device:
+  // the ctx's device, before the first batch has set it)
+  void start_prealloc(uint64_t m, int device = -1);
   // device view of the records of the last batch when they lie in one window
   bool last_batch_span(SpanDev* out) const;
   // BAMRecordReader.getProgress's in.position() after record i of the last
@@ -428,7 +432,6 @@ class SpanCursor {
   // the first batches' page-locked slots, mapped and pinned on a helper
   // thread while the first window decodes (joined before a slot is used)
   std::thread prealloc_;
-  void start_prealloc(uint64_t m);
   void join_prealloc();
   int cur_ = -1;                   // slot of the last batch handed out
   uint64_t* small_ = nullptr;      // page-locked scratch for the boundary reads

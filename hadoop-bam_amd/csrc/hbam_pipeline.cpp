@@ -235,6 +235,13 @@ int Pipeline::stage_wait() {
   return kOk;
 }
 
+int Pipeline::reserve_stage(uint64_t bytes) {
+  HIPCHK(hipSetDevice(device_));
+  if (int rc = stage_wait()) return rc;
+  HIPCHK(stage_.reserve(bytes));
+  return kOk;
+}
+
 int Pipeline::stage(const HostSource& src, uint64_t lo, uint64_t hi) {
   HIPCHK(hipSetDevice(device_));
   if (hi <= lo || (lo == stage_lo_ && hi == stage_hi_)) return kOk;  // nothing new to stage

@@ -165,6 +165,9 @@ class Pipeline {
   // from there (device-to-device) instead of the host, so a window's H2D
   // overlaps the previous window's decode.  src must outlive the copy.
   int stage(const HostSource& src, uint64_t lo, uint64_t hi);
+  // the staging buffer sized for windows of up to `bytes` at once (growing it
+  // later waits for the device)
+  int reserve_stage(uint64_t bytes);
   // Use device-resident file bytes [base, base + len) (readable for kFilePad
   // bytes past len).
   int attach_device(const uint8_t* dptr, uint64_t len, uint64_t base, bool at_eof);

@@ -32,11 +32,11 @@ STRICT, LENIENT, SILENT = 0, 1, 2  # hadoopbam.samheaderreader.validation-string
 
 class Opts(C.Structure):
     _fields_ = [("device", i32), ("check_crc", i32), ("stringency", i32), ("parallel_reads", i32),
-                ("window_bytes", u64)]
+                ("window_bytes", u64), ("batch_records", u64)]
 
 
-def _opts(device=0, check_crc=False, stringency=STRICT, window_bytes=0, parallel_reads=False):
-    return Opts(device, int(check_crc), stringency, int(parallel_reads), window_bytes)
+def _opts(device=0, check_crc=False, stringency=STRICT, window_bytes=0, parallel_reads=False, batch_records=0):
+    return Opts(device, int(check_crc), stringency, int(parallel_reads), window_bytes, batch_records)
 
 
 class HeaderInfo(C.Structure):
@@ -313,12 +313,15 @@ class BamFile:
     pread); reader= + size= reads through a positioned-read callback
     (hbam_open_reader: read(offset, n) -> bytes, as a Hadoop FSDataInputStream
     does through JNI; parallel_reads: it may be called from several library
-    threads at once); window_bytes = compressed bytes per HBM window (0: 4 GiB)."""
+    threads at once); window_bytes = compressed bytes per HBM window (0: 4 GiB);
+    batch_records = the max_records decode_span / scan_batches will use (the
+    batch slots are then page-locked from the open on, hbam_opts)."""
 
     def __init__(self, data: bytes = None, path: str = None, device=0, bam=True, check_crc=False,
-                 stringency=STRICT, window_bytes=0, reader=None, size=None, parallel_reads=False):
+                 stringency=STRICT, window_bytes=0, reader=None, size=None, parallel_reads=False,
+                 batch_records=0):
         self._h = P()
-        o = _opts(device, check_crc, stringency, window_bytes, parallel_reads)
+        o = _opts(device, check_crc, stringency, window_bytes, parallel_reads, batch_records)
         if reader is not None:
             self._cb = reader_callback(reader)
             rc = _L.hbam_open_reader(size, self._cb, None, C.byref(o), C.byref(self._h))

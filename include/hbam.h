@@ -51,7 +51,7 @@ extern "C" {
 #define HBAM_E_STATE 6
 #define HBAM_E_NOMEM 7
 
-#define HBAM_ABI_VERSION 4
+#define HBAM_ABI_VERSION 5
 
 /* htsjdk ValidationStringency, as util/SAMHeaderReader.java:45-46 reads it */
 #define HBAM_STRICT 0  /* htsjdk's default: SAMRecord.isValid errors -> SAMFormatException */
@@ -68,6 +68,9 @@ typedef struct hbam_opts {
   int32_t parallel_reads; /* hbam_open_reader: nonzero = the read callback may run on several library
                              threads at once (PositionedReadable positioned reads are thread-safe) */
   uint64_t window_bytes; /* hadoopbam.gpu.window-bytes: compressed bytes per HBM window (0 = 4 GiB) */
+  uint64_t batch_records; /* hadoopbam.gpu.batch-records: the max_records the caller will pass to
+                             hbam_decode_span (0 = not known); its page-locked batch slots are then
+                             allocated on a helper thread from the open on */
 } hbam_opts;
 
 /* BAM header summary ([htsjdk] BAMFileReader.readHeader). */

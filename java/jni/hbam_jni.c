@@ -74,10 +74,10 @@ static jobjectArray wrap_batch(JNIEnv *env, const hbam_batch *b) {
 }
 
 JNIEXPORT jlong FN(open)(JNIEnv *env, jclass c, jstring path, jint device, jboolean crc, jint stringency,
-                         jlong window) {
+                         jlong window, jlong batch) {
   const char *p = (*env)->GetStringUTFChars(env, path, NULL);
   if (!p) return 0;
-  hbam_opts o = {device, crc ? 1 : 0, stringency, 0, (uint64_t)window};
+  hbam_opts o = {device, crc ? 1 : 0, stringency, 0, (uint64_t)window, (uint64_t)batch};
   hbam_ctx *ctx = NULL;
   int rc = hbam_open(p, &o, &ctx);
   (*env)->ReleaseStringUTFChars(env, path, p);
@@ -130,7 +130,7 @@ static int64_t jreader_read(void *user, uint64_t off, void *dst, uint64_t len) {
 }
 
 JNIEXPORT jlong FN(openReader)(JNIEnv *env, jclass c, jlong size, jobject reader, jboolean parallel, jint device,
-                               jboolean crc, jint stringency, jlong window) {
+                               jboolean crc, jint stringency, jlong window, jlong batch) {
   struct jreader *r = (struct jreader *)calloc(1, sizeof *r);
   jclass rc_cls = reader ? (*env)->GetObjectClass(env, reader) : NULL;
   if (!r || !rc_cls || (*env)->GetJavaVM(env, &r->vm) != 0) {
@@ -144,7 +144,7 @@ JNIEXPORT jlong FN(openReader)(JNIEnv *env, jclass c, jlong size, jobject reader
     return 0; /* NoSuchMethodError pending */
   }
   r->reader = (*env)->NewGlobalRef(env, reader);
-  hbam_opts o = {device, crc ? 1 : 0, stringency, parallel ? 1 : 0, (uint64_t)window};
+  hbam_opts o = {device, crc ? 1 : 0, stringency, parallel ? 1 : 0, (uint64_t)window, (uint64_t)batch};
   hbam_ctx *ctx = NULL;
   int rc = hbam_open_reader((uint64_t)size, jreader_read, r, &o, &ctx);
   if (rc != HBAM_OK) {

@@ -107,7 +107,7 @@ public class GpuBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     // a local path is read with pread, HDFS and the rest through positioned
     // reads of the FSDataInputStream (hbam_open_reader)
     file = HbamFiles.open(path, conf, device(conf), stringencyCode(stringency),
-                          conf.getLong(WINDOW_BYTES_PROPERTY, 0L));
+                          conf.getLong(WINDOW_BYTES_PROPERTY, 0L), batchRecords);
     ctx = file.ctx;
     cursor[0] = virtualStart;
     cols = null;

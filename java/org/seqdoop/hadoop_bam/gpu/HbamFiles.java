@@ -118,15 +118,26 @@ public final class HbamFiles {
   /** Open file of conf's file system on the GPU path (hbam_open or hbam_open_reader). */
   public static Handle open(Path file, Configuration conf, int device, int stringency, long windowBytes)
       throws IOException {
+    return open(file, conf, device, stringency, windowBytes, 0L);
+  }
+
+  /**
+   * As {@link #open(Path, Configuration, int, int, long)} for a reader that
+   * will call decodeSpan with batchRecords records per batch: the library
+   * pins its batch buffers from the open on (hbam_opts.batch_records).
+   */
+  public static Handle open(Path file, Configuration conf, int device, int stringency, long windowBytes,
+                            long batchRecords) throws IOException {
     final FileSystem fs = file.getFileSystem(conf);
     if (isLocal(fs)) {
       final String p = fs.makeQualified(file).toUri().getPath();
-      return new Handle(HbamNative.open(p, device, false, stringency, windowBytes), null);
+      return new Handle(HbamNative.open(p, device, false, stringency, windowBytes, batchRecords), null);
     }
     final long size = fs.getFileStatus(file).getLen();
     final FSDataInputStream in = fs.open(file);
     try {
-      return new Handle(HbamNative.openReader(size, new FsReader(in), true, device, false, stringency, windowBytes),
+      return new Handle(HbamNative.openReader(size, new FsReader(in), true, device, false, stringency, windowBytes,
+                                              batchRecords),
                         in);
     } catch (IOException | RuntimeException e) {
       in.close();
@@ -136,7 +147,8 @@ public final class HbamFiles {
 
   /** Open a stream of inputSize bytes read front to back (SplittingBAMIndexer.index(InputStream, ...)). */
   public static Handle open(InputStream in, long inputSize, int device, int stringency) throws IOException {
-    return new Handle(HbamNative.openReader(inputSize, new StreamReader(in), false, device, false, stringency, 0L),
+    return new Handle(HbamNative.openReader(inputSize, new StreamReader(in), false, device, false, stringency, 0L,
+                                            0L),
                       in);
   }
 }

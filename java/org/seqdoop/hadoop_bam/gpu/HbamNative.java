@@ -53,10 +53,12 @@ public final class HbamNative {
    * @param device hadoopbam.gpu.device (HIP ordinal; LOCAL_RANK under one process per GPU)
    * @param stringency STRICT / LENIENT / SILENT
    * @param windowBytes hadoopbam.gpu.window-bytes (compressed bytes per HBM window; 0 = 4 GiB)
+   * @param batchRecords hadoopbam.gpu.batch-records the reader will pass to decodeSpan (0 = not
+   *     known): its page-locked batch buffers are pinned from the open on
    * @return the ctx handle
    */
-  public static native long open(String path, int device, boolean checkCrc, int stringency, long windowBytes)
-      throws IOException;
+  public static native long open(String path, int device, boolean checkCrc, int stringency, long windowBytes,
+                                 long batchRecords) throws IOException;
 
   /**
    * Positioned reads of a file, as PositionedReadable.read(position, buf,
@@ -79,7 +81,8 @@ public final class HbamNative {
    * reference to reader until {@link #close}.
    */
   public static native long openReader(long size, PositionedReader reader, boolean parallelReads, int device,
-                                       boolean checkCrc, int stringency, long windowBytes) throws IOException;
+                                       boolean checkCrc, int stringency, long windowBytes, long batchRecords)
+      throws IOException;
 
   public static native void close(long ctx);
 

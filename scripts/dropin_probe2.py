@@ -191,7 +191,7 @@ def main():
                         g.close()
                     del raw
             print("after", step, flush=True)
-            with hbam.BamFile(path=path) as f:
+            with hbam.BamFile(path=path, batch_records=1 << 20) as f:
                 first = f.header()["first_record_voff"]
                 mark(f"mapped{rep}_begin")
                 if SMI:

@@ -51,6 +51,17 @@ for s in $STEPS; do
           > $OUT/dropin_ramp_$r.log 2>&1 || { echo "dropin probe failed"; tail -30 $OUT/dropin_ramp_$r.log; exit 6; }
         echo "ramp=$r"; grep -E "^(mapped|resident)" $OUT/dropin_ramp_$r.log | cut -c1-140
       done ;;
+    order)
+      # the drop-in loop before and after hbam_gpu_run_streamed (the pinned-host leg), clocks and link sampled
+      timeout -k 10 400 python -u scripts/dropin_probe2.py 10000000 --torch --smi --steps none,run_streamed,none,none \
+        > $OUT/order.log 2>&1 || { echo "order probe failed"; tail -30 $OUT/order.log; exit 9; }
+      grep -E "^(mapped|resident|SMI)" $OUT/order.log | cut -c1-260 ;;
+    ordertrace)
+      # the same with the host-side timeline (HBAM_CURSOR_TRACE) of each loop
+      HBAM_CURSOR_TRACE=1 timeout -k 10 400 python -u scripts/dropin_probe2.py 10000000 --torch \
+        --steps none,run_streamed,none > $OUT/ordertrace.log 2> $OUT/ordertrace.err \
+        || { echo "order trace failed"; tail -30 $OUT/ordertrace.err; exit 9; }
+      grep -E "^(mapped|resident)" $OUT/ordertrace.log | cut -c1-200 ;;
     variants)
       # stage times + overlapped wall time per pass: the default build, the
       # in-tree experiment builds (lib/variants), the unfused record pass
