@@ -1626,7 +1626,13 @@ constexpr uint32_t kMapMax = 65280;
 constexpr uint32_t kLitTag = 0xFF00u;
 constexpr int kLzRing = 4;  // phase-B fill: 64-token groups loaded ahead (4 vs 8 measured equal)
 constexpr int kLzTokGroups = 32;  // token groups a wave keeps in registers (32 K tokens per block)
-constexpr int kLzChase = 2;  // positions chased together per thread (4: slower, longer chains)
+#ifndef HBAM_LZ_JUMP
+#define HBAM_LZ_JUMP 1
+#endif
+#ifndef HBAM_LZ_CHASE
+#define HBAM_LZ_CHASE 2
+#endif
+constexpr int kLzChase = HBAM_LZ_CHASE;  // positions chased together per thread (4: slower before pointer jumping)
 
 // exclusive scan over the workgroup; returns the prefix, *total = sum
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
@@ -1899,6 +1905,15 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
       for (int k = 0; k < kLzChase; ++k) n[k] = m[v[k] < kLitTag ? v[k] : at[k]];
 #pragma unroll
       for (int k = 0; k < kLzChase; ++k) v[k] = v[k] < kLitTag ? n[k] : v[k];
+#if HBAM_LZ_JUMP
+      // pointer jumping: every step stores how far the chase got, so a lane
+      // whose chain runs through this position skips the hops already made
+      // (a run of dist-1 matches resolves in ~log2(len) steps instead of
+      // len).  Any stored value is a position holding the same byte, or the
+      // byte itself, so racing stores keep every entry valid.
+#pragma unroll
+      for (int k = 0; k < kLzChase; ++k) m[at[k]] = (uint16_t)v[k];
+#endif
     }
 #pragma unroll
     for (int k = 0; k < kLzChase; ++k)
@@ -3262,46 +3277,80 @@ __global__ __launch_bounds__(64) void k_rec_out(ChainEnv E, const uint32_t* __re
 constexpr int kBadShift = 40;
 
 template <int MODE, bool DECODE>
-__global__ __launch_bounds__(64) void k_rec_check_out(ChainEnv E, const uint64_t* __restrict__ entry,
-                                                      const uint32_t* __restrict__ wcnt,
-                                                      const uint16_t* __restrict__ list,
-                                                      const uint64_t* __restrict__ base, uint32_t* __restrict__ cnt,
-                                                      int32_t* __restrict__ err, unsigned long long* __restrict__ need,
-                                                      unsigned long long* __restrict__ bad,
-                                                      uint32_t* __restrict__ flags, uint64_t* __restrict__ rec_pos,
-                                                      uint64_t* __restrict__ rec_voff, Columns col, uint64_t cap) {
+__global__ __launch_bounds__(64, 6) void k_rec_check_out(ChainEnv E, const uint64_t* __restrict__ entry,
+                                                         const uint32_t* __restrict__ wcnt,
+                                                         const uint16_t* __restrict__ list,
+                                                         const uint64_t* __restrict__ base, uint32_t* __restrict__ cnt,
+                                                         int32_t* __restrict__ err,
+                                                         unsigned long long* __restrict__ need,
+                                                         unsigned long long* __restrict__ bad,
+                                                         uint32_t* __restrict__ flags, uint64_t* __restrict__ rec_pos,
+                                                         uint64_t* __restrict__ rec_voff, Columns col, uint64_t cap) {
   const uint32_t lane = lane_id();
   const uint32_t i = blockIdx.x;
   const uint64_t e = entry[i];
-  uint32_t count;
-  int st;
-  uint64_t nd;
-  const bool any_long = check_block<MODE>(E, i, e, wcnt, list, &count, &st, &nd);
   const BlockInfo b = E.blocks[E.k0 + i];
   const uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
-  if (MODE == kReader && any_long) {
-    // cigars longer than kWaveCigarOps before the stop, a wave each in list
-    // order (k_rec_check_long): the first invalid one becomes the stop
-    for (uint32_t r0 = 0; r0 < count; r0 += 64) {
-      const uint32_t r = r0 + lane;
-      const uint64_t q = r < count ? b.ustart + L[r] : 0;
-      const bool lg = r < count && (ldu32(E.u, q + 16) & 0xffffu) > kWaveCigarOps;
-      bool hit = false;
-      for (uint64_t wm = __ballot(lg); wm && !hit; wm &= wm - 1) {
+  const uint64_t lim = min(b.ustart + b.isize, E.q_end);
+  const uint32_t wc = wcnt[i];
+  const uint32_t listed = e == kNone ? 0u : min(wc & kListCountMask, kListCap);
+  // (check_block's rules) a plausible() list on fully inflated data already
+  // satisfies every rule that reads the record
+  const bool light = (wc & kListPlausible) && E.e_inf == E.e_true && (MODE != kReader || E.validate == 0);
+  const uint64_t o0 = base[i];
+  uint32_t count = listed;
+  int st = kOk;
+  uint64_t nd = 0;
+  // 64 records at a time: check them, validate their long cigars, and write
+  // the ones before the first stop while their lines are still in L1/L2 (a
+  // whole block checked before any output re-fetched every line: 5.9 GB per
+  // C2 pass)
+  for (uint32_t r0 = 0; r0 < listed; r0 += 64) {
+    const uint32_t r = r0 + lane;
+    const uint64_t q = r < listed ? b.ustart + L[r] : 0;
+    bool stop = false, counted = false, long_cigar = false;
+    int s = kOk;
+    uint64_t x = 0;
+    if (r < listed)
+      check_listed<MODE>(E, q, lim, r == 0 && q == E.p0, light, &stop, &counted, &s, &x, &long_cigar);
+    uint32_t m = min(64u, listed - r0);  // records of this chunk that stand
+    const uint64_t sm = __ballot(stop);
+    bool halt = sm != 0;  // the block's count ends in this chunk
+    if (sm) {
+      const uint32_t f = (uint32_t)__ffsll((long long)sm) - 1;
+      m = f + (uint32_t)__shfl((int)counted, (int)f, 64);
+      st = __shfl(s, (int)f, 64);
+      nd = shfl_u64(x, f);
+    }
+    if (MODE == kReader) {
+      // cigars longer than kWaveCigarOps before the stop, a wave each in order
+      // (k_rec_check_long): the first invalid one becomes the stop
+      const bool lg = lane < m && long_cigar;
+      for (uint64_t wm = __ballot(lg); wm; wm &= wm - 1) {
         const uint32_t src = (uint32_t)__ffsll((long long)wm) - 1;
         const uint64_t qq = shfl_u64(q, src);
         if (record_invalid_wave(E, qq, (int32_t)ldu32(E.u, qq), E.validate == 2)) {
-          count = r0 + src;
+          m = src;
           st = kErrFormat;
           nd = 0;
-          hit = true;
+          halt = true;
+          break;
         }
       }
-      if (hit) break;
+    }
+    if (lane < m) {
+      const uint64_t o = o0 + r;
+      if (o < cap) {  // (sized from the lists' counts: always)
+        rec_pos[o] = q;
+        rec_voff[o] = (b.coff << 16) | (q - b.ustart);
+        if (DECODE) decode_record(E.u, q, o, col);
+      }
+    }
+    if (halt) {
+      count = r0 + m;
+      break;
     }
   }
-  const uint32_t listed = e == kNone ? 0u : min(wcnt[i] & kListCountMask, kListCap);
-  const uint64_t o0 = base[i];
   if (lane == 0) {
     if (nd) atomicMax(need, (unsigned long long)nd);
     cnt[i] = count;
@@ -3310,14 +3359,6 @@ __global__ __launch_bounds__(64) void k_rec_check_out(ChainEnv E, const uint64_t
       atomicMin(bad, ((unsigned long long)i << kBadShift) | (unsigned long long)(o0 + count));
     if (st != kOk) atomicMin(&flags[0], i);
     if (count) atomicMax(&flags[1], i + 1);
-  }
-  for (uint32_t r = lane; r < count; r += 64) {
-    const uint32_t off = L[r];
-    const uint64_t q = b.ustart + off, o = o0 + r;
-    if (o >= cap) break;  // (sized from the lists' counts: not reached)
-    rec_pos[o] = q;
-    rec_voff[o] = (b.coff << 16) | off;
-    if (DECODE) decode_record(E.u, q, o, col);
   }
 }
 
