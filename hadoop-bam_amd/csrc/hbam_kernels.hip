@@ -335,36 +335,45 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
                                                      uint32_t* tab, uint32_t* cnt, uint16_t* sorted, uint32_t* sub,
                                                      int subcap) {
   const uint32_t lane = lane_id();
-  if (lane < 16) cnt[lane] = 0;
-  wave_sync();
-  for (int s = lane; s < nsym; s += 64) {
-    const uint32_t l = lens[s];
-    if (l) atomicAdd(&cnt[l], 1u);
+  // counts per code length by ballots, then the Kraft check, the canonical
+  // offsets and first codes as wave-uniform arithmetic (LDS atomics and a
+  // one-lane loop over LDS cost ~3 K cycles per table)
+  uint32_t cntv[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) cntv[q] = 0;
+  for (int c0 = 0; c0 < nsym; c0 += 64) {
+    const int s = c0 + (int)lane;
+    const uint32_t l = s < nsym ? lens[s] : 0;
+#pragma unroll
+    for (uint32_t q = 1; q < 16; ++q) cntv[q] += (uint32_t)__popcll(__ballot(l == q));
   }
-  wave_sync();
-  if (lane == 0) {
-    int left = 1, maxl = 0, over = 0;
-    uint32_t o = 0, code = 0, prev = 0;
-    for (int l = 1; l < 16; ++l) {
-      const uint32_t c = cnt[l];
-      left = (left << 1) - (int)c;
-      if (c) maxl = l;
-      if (left < 0) over = 1;
-      L.offs[l] = o;
-      o += c;
-      code = (code + prev) << 1;
-      L.firstc[l] = code;
-      prev = c;
-    }
-    uint32_t st = 0;
-    if (over) st = 1;
-    else if (maxl == 0) st = mode == 2 ? 1 : 2;
-    else if (left > 0 && (mode == 2 || maxl != 1)) st = 1;
-    L.bt_status = st;
+  int left = 1, maxl = 0;
+  bool over = false;
+  uint32_t o = 0, code = 0, prev = 0, my_cnt = 0, my_off = 0, my_first = 0;
+#pragma unroll
+  for (uint32_t l = 1; l < 16; ++l) {
+    const uint32_t c = cntv[l];
+    left = (left << 1) - (int)c;
+    maxl = c ? (int)l : maxl;
+    over = over || left < 0;
+    code = (code + prev) << 1;
+    my_cnt = lane == l ? c : my_cnt;
+    my_off = lane == l ? o : my_off;
+    my_first = lane == l ? code : my_first;
+    o += c;
+    prev = c;
   }
+  if (lane < 16) {
+    cnt[lane] = my_cnt;
+    L.offs[lane] = my_off;
+    L.firstc[lane] = my_first;
+  }
+  uint32_t st = 0;
+  if (over) st = 1;
+  else if (maxl == 0) st = mode == 2 ? 1 : 2;
+  else if (left > 0 && (mode == 2 || maxl != 1)) st = 1;
   for (int i = lane; i < (1 << root); i += 64) tab[i] = kBadEntry;
   wave_sync();
-  const uint32_t st = rfl(L.bt_status);
   if (st == 1) return 1;
   if (st == 2) return 0;  // no codes: all-invalid table
   const uint32_t rmask = (1u << root) - 1;
@@ -385,18 +394,30 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
       rank = l == q ? basev[q] + (uint32_t)__popcll(m & ltmask) : rank;
       basev[q] += (uint32_t)__popcll(m);
     }
+    uint32_t rev = 0, e = 0;
     if (l) {
       sorted[L.offs[l] + rank] = (uint16_t)s;
       const uint32_t code = L.firstc[l] + rank;
-      const uint32_t rev = __brev(code) >> (32 - l);
+      rev = __brev(code) >> (32 - l);
       L.rev_of[s] = (uint16_t)rev;
       if ((int)l <= root) {
-        const uint32_t e = make_entry(mode, (uint32_t)s, l);
-        for (uint32_t i = rev; i < (1u << root); i += (1u << l)) tab[i] = e;
+        e = make_entry(mode, (uint32_t)s, l);
+        // a code that fills fewer than 64 root entries fills them itself; the
+        // wave fills the wider ones together below (a lane alone took up to
+        // 2^(root - l) dependent trips, and the wave waited for the longest)
+        if ((int)l > root - 6)
+          for (uint32_t i = rev; i < (1u << root); i += (1u << l)) tab[i] = e;
       } else {
         atomicMax(&tab[rev & rmask], kLongTag | (l - (uint32_t)root));  // widest sub-table under the prefix
         any_long = true;
       }
+    }
+    for (uint64_t wm = __ballot(l != 0 && (int)l <= root - 6); wm; wm &= wm - 1) {
+      const int src = __ffsll((long long)wm) - 1;
+      const uint32_t wl = (uint32_t)__shfl((int)l, src, 64);
+      const uint32_t wr = (uint32_t)__shfl((int)rev, src, 64);
+      const uint32_t we = (uint32_t)__shfl((int)e, src, 64);
+      for (uint32_t k = lane; k < (1u << (root - (int)wl)); k += 64) tab[wr + (k << wl)] = we;
     }
   }
   wave_sync();
@@ -1033,8 +1054,13 @@ __device__ __forceinline__ uint32_t peek32(const uint32_t* W, uint32_t p) {
 }
 
 __device__ int dyn_header_par(HuffLds& L, ClLds& C, const uint32_t* __restrict__ W, uint32_t p, uint32_t E,
-                              uint32_t* end_pos) {
+                              uint32_t* end_pos, uint64_t* probe = nullptr) {
   const uint32_t lane = lane_id();
+#ifdef HBAM_TAB_PROBE
+#define DH_PROBE(k) do { if (probe) probe[k] = clock64(); } while (0)
+#else
+#define DH_PROBE(k) do { (void)probe; } while (0)
+#endif
   if (p + 14 > E) return DH_TRUNC;
   const uint32_t h = rfl(peek32(W, p));
   const uint32_t hlit = (h & 31) + 257, hdist = ((h >> 5) & 31) + 1, hclen = ((h >> 10) & 15) + 4;
@@ -1047,6 +1073,7 @@ __device__ int dyn_header_par(HuffLds& L, ClLds& C, const uint32_t* __restrict__
   wave_sync();
   p += 3 * hclen;
   if (rfl(build_table(L, L.cl_lens, 19, 7, 2, L.dist, L.cnt_dist, L.sort_dist, nullptr, 0))) return DH_TRUNC;
+  DH_PROBE(0);
   const uint32_t ntot = hlit + hdist;
   uint32_t done = 0, prevv = 0, have_prev = 0;
   for (;;) {  // windows of 64 * kClSlice bits
@@ -1146,14 +1173,20 @@ __device__ int dyn_header_par(HuffLds& L, ClLds& C, const uint32_t* __restrict__
     p = rfl((uint32_t)__shfl(x, 63, 64));
   }
   wave_sync();
+  DH_PROBE(1);
   if (rfl(L.lens[256]) == 0) return DH_TRUNC;
-  if (rfl(build_table(L, L.lens, (int)hlit, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit, L.litsub, kLitSubCap)) ||
-      rfl(build_table(L, L.lens + hlit, (int)hdist, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist, L.distsub,
+  if (rfl(build_table(L, L.lens, (int)hlit, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit, L.litsub, kLitSubCap)))
+    return DH_TRUNC;
+  DH_PROBE(2);
+  if (rfl(build_table(L, L.lens + hlit, (int)hdist, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist, L.distsub,
                       kDistSubCap)))
     return DH_TRUNC;
+  DH_PROBE(3);
   pair_literals(L);
+  DH_PROBE(4);
   return DH_OK;
 }
+#undef DH_PROBE
 
 // First DEFLATE block of every BGZF block: header + tables built ahead of the
 // decode kernel, one wave per block at high occupancy, so the serial header
@@ -1175,6 +1208,10 @@ __global__ __launch_bounds__(64) void k_huff_tables(const uint8_t* __restrict__ 
   __shared__ ClLds C;
   const uint32_t lane = lane_id();
   const uint32_t bi = b0 + blockIdx.x;
+#ifdef HBAM_TAB_PROBE
+  uint64_t tp[5] = {(uint64_t)clock64(), 0, 0, 0, 0};
+  uint64_t dp[5] = {0, 0, 0, 0, 0};
+#endif
   const BlockInfo blk = blocks[bi];
   HuffTableInfo ti{1u, 0u, 0u, 0u};
   const uint64_t sbyte = blk.coff + 18;
@@ -1195,6 +1232,9 @@ __global__ __launch_bounds__(64) void k_huff_tables(const uint8_t* __restrict__ 
     const uint4* __restrict__ src = reinterpret_cast<const uint4*>(file + abase + sb);
     for (uint32_t i = lane; i <= nreal; i += 64) s_in[i] = src[i];  // +1 pad chunk (file is padded)
     wave_sync();
+#ifdef HBAM_TAB_PROBE
+    tp[1] = clock64();
+#endif
     SReader R;
     R.W = reinterpret_cast<const uint32_t*>(s_in);
     const uint32_t Ereal = 8u * ((uint32_t)(sbyte - abase) + (blk.csize - 26)) - 8u * sb;
@@ -1206,14 +1246,35 @@ __global__ __launch_bounds__(64) void k_huff_tables(const uint8_t* __restrict__ 
       R.consume(3);
       uint32_t b0pos = 0;
       const uint32_t hp = R.pos();
+#ifdef HBAM_TAB_PROBE
+      if (dyn_header_par(L, C, R.W, hp, E, &b0pos, dp) == DH_OK) {
+#else
       if (dyn_header_par(L, C, R.W, hp, E, &b0pos) == DH_OK) {
+#endif
         wave_sync();
+#ifdef HBAM_TAB_PROBE
+        tp[2] = clock64();
+#endif
         const uint32_t h = rfl(peek32(R.W, hp));
         const uint32_t est = block_bits_estimate(L.lens, (h & 31) + 257, ((h >> 5) & 31) + 1);
+#ifdef HBAM_TAB_PROBE
+        tp[3] = clock64();
+#endif
         uint4* __restrict__ dst = reinterpret_cast<uint4*>(tables + (uint64_t)blockIdx.x * kTableImage);
         const uint4* img = reinterpret_cast<const uint4*>(&L);
         for (uint32_t i = lane; i < kTableImage / 16; i += 64) dst[i] = img[i];
         ti = HuffTableInfo{0u, b0pos + 8u * sb, fin, est};
+#ifdef HBAM_TAB_PROBE
+        tp[4] = clock64();
+        if (lane == 0 && (blockIdx.x & 4095) == 17)
+          printf("tabprobe r%u b%u stage %llu cltab %llu lens %llu littab %llu disttab %llu pairs %llu est %llu "
+                 "copy %llu total %llu\n", round, blockIdx.x,
+                 (unsigned long long)(tp[1] - tp[0]), (unsigned long long)(dp[0] - tp[1]),
+                 (unsigned long long)(dp[1] - dp[0]), (unsigned long long)(dp[2] - dp[1]),
+                 (unsigned long long)(dp[3] - dp[2]), (unsigned long long)(dp[4] - dp[3]),
+                 (unsigned long long)(tp[3] - tp[2]), (unsigned long long)(tp[4] - tp[3]),
+                 (unsigned long long)(tp[4] - tp[0]));
+#endif
       }
     }
   }
