@@ -1319,6 +1319,13 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
   const uint32_t bi = b0 + blockIdx.x;
   const BlockInfo blk = blocks[bi];
   const uint32_t isize = blk.isize;
+#ifdef HBAM_HUFF_PROBE
+  // clock probes (developer builds): cycles per stage of this workgroup-round
+  uint64_t pt = clock64(), pstage = 0, pctl = 0, pspec = 0, psync = 0, pscan = 0, pemit = 0, npass = 0;
+#define HP_MARK(acc) do { const uint64_t t_ = clock64(); acc += t_ - pt; pt = t_; } while (0)
+#else
+#define HP_MARK(acc) do { } while (0)
+#endif
   if (isize == 0) {  // inflate(buf,off,0) returns 0 without reading: nothing to validate
     if (tid == 0 && round == 0) { hout[bi].ntok = 0; hout[bi].status = kOk; }
     return;
@@ -1365,6 +1372,7 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
     }
   }
   __syncthreads();
+  HP_MARK(pstage);
   // compressed bits: the LDS copy, or (unstaged) the file in HBM
   const uint32_t* __restrict__ W =
       STAGE ? reinterpret_cast<const uint32_t*>(s_in) : reinterpret_cast<const uint32_t*>(file + abase);
@@ -1577,6 +1585,7 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
       if (lane == 0) C.act = act;
     }
     __syncthreads();
+    HP_MARK(pctl);
     if (C.act != kActDecode) break;
 
     // ---- all-lane decode of this DEFLATE block's symbols
@@ -1589,12 +1598,19 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
     uint32_t mj = 0, x, nt, nb;
     uint32_t ev = lane_decode<LD_SPEC>(L, W, a, stop, E, x, nt, nb, mp, mj, nullptr, 0, 0);
     const uint32_t sx = x, snt = nt, snb = nb, sev = ev;
+#ifdef HBAM_HUFF_PROBE
+    bool first_sync = true;
+#endif
     for (;;) {  // sync: restart each slice from its predecessor's exit
       if (lane == 63) {
         C.xx[wave] = x;
         C.xe[wave] = ev;
       }
       __syncthreads();
+#ifdef HBAM_HUFF_PROBE
+      if (first_sync) HP_MARK(pspec);
+      first_sync = false;
+#endif
       uint32_t px = __shfl_up(x, 1, 64), pev = __shfl_up(ev, 1, 64);
       if (lane == 0 && wave > 0) {
         px = C.xx[wave - 1];
@@ -1620,15 +1636,21 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
         }
       }
     }
+    HP_MARK(psync);
     const uint32_t lend0 = wg_min(ev != EV_STOP ? tid : 0xffffffffu, C.red);
     const uint32_t lend = lend0 == 0xffffffffu ? (uint32_t)kHuffThreads - 1 : lend0;
     const bool valid = tid <= lend;
     uint32_t toff, boff;
     wg_excl_scan2(valid ? nt : 0u, valid ? nb : 0u, C.red, toff, boff);
+    HP_MARK(pscan);
     uint32_t x3 = a, nt3 = 0, nb3 = 0, ev3 = EV_STOP;
     if (valid)
       ev3 = lane_decode<LD_EMIT>(L, W, a, stop, E, x3, nt3, nb3, mp, mj, tok_out + tok0 + toff, out0 + boff, isize);
     const uint32_t m3 = wg_min((valid && ev3 != EV_STOP) ? tid : 0xffffffffu, C.red);
+    HP_MARK(pemit);
+#ifdef HBAM_HUFF_PROBE
+    ++npass;
+#endif
     const uint32_t f = m3 != 0xffffffffu ? m3 : lend;
     if (tid == f) {
       C.fe = ev3;
@@ -1639,6 +1661,14 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
     }
     __syncthreads();
   }
+#ifdef HBAM_HUFF_PROBE
+  if (tid == 0 && (blockIdx.x & 4095) == 17)
+    printf("huffprobe r%u b%u stage %u passes %u stage_cyc %llu ctl %llu spec %llu sync %llu scan %llu emit %llu\n",
+           round, blockIdx.x, (unsigned)STAGE, (unsigned)npass, (unsigned long long)pstage, (unsigned long long)pctl,
+           (unsigned long long)pspec, (unsigned long long)psync, (unsigned long long)pscan,
+           (unsigned long long)pemit);
+#endif
+#undef HP_MARK
   if (tid == 0) {
     if (wave == 0 && pending && err == kOk) {
       hout[bi] = HuffOut{ntok, kHuffPending, resume_bit, outpos};
