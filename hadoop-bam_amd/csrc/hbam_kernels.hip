@@ -244,6 +244,17 @@ constexpr int kHuffWaves = kHuffThreads / 64;
 #define HBAM_HUFF_STAGE_MAX (40 * 1024)
 #endif
 constexpr uint32_t kHuffStageMaxLds = HBAM_HUFF_STAGE_MAX;
+// 16 B loads in flight per thread while a phase-A workgroup stages its block
+// and table image through registers (HBAM_STAGE_GLDS=0; 4, 6, 8 and 10 measured
+// the same)
+#ifndef HBAM_STAGE_BATCH
+#define HBAM_STAGE_BATCH 4
+#endif
+// 1: stage with global_load_lds_dwordx4, no register round trip (phase A
+// 8.52 -> 8.00 ms per C2 pass)
+#ifndef HBAM_STAGE_GLDS
+#define HBAM_STAGE_GLDS 1
+#endif
 
 // Wave-local ordering of LDS traffic (code run by one wave only).
 __device__ __forceinline__ void wave_sync() {
@@ -1354,7 +1365,19 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
     const uint4* __restrict__ tsrc = reinterpret_cast<const uint4*>(tables + (uint64_t)blockIdx.x * kTableImage);
     uint4* sdst = s_in + q0;
     uint4* tdst = reinterpret_cast<uint4*>(&L);
-    constexpr int kStageBatch = 4;
+#if HBAM_STAGE_GLDS
+    // global -> LDS without registers (global_load_lds_dwordx4): each wave
+    // instruction moves 64 consecutive 16 B units to LDS base + lane x 16, all
+    // of a workgroup's copies in flight at once (__syncthreads drains them)
+    typedef __attribute__((address_space(3))) void* lds_vp;
+    typedef __attribute__((address_space(1))) void* gbl_vp;
+    const uint32_t wv = tid >> 6, ln = tid & 63;
+    for (uint32_t u0 = 64 * wv; u0 < nq; u0 += kHuffThreads)
+      if (u0 + ln < nq) __builtin_amdgcn_global_load_lds((gbl_vp)(src + u0 + ln), (lds_vp)(sdst + u0), 16, 0, 0);
+    for (uint32_t u0 = 64 * wv; u0 < nt; u0 += kHuffThreads)
+      if (u0 + ln < nt) __builtin_amdgcn_global_load_lds((gbl_vp)(tsrc + u0 + ln), (lds_vp)(tdst + u0), 16, 0, 0);
+#else
+    constexpr int kStageBatch = HBAM_STAGE_BATCH;
     for (uint32_t i0 = tid; i0 < nq + nt; i0 += kStageBatch * kHuffThreads) {
       uint4 v[kStageBatch];
 #pragma unroll
@@ -1370,6 +1393,7 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
         else if (i < nq + nt) tdst[i - nq] = v[k];
       }
     }
+#endif
   }
   __syncthreads();
   HP_MARK(pstage);
