@@ -48,6 +48,31 @@ __device__ __forceinline__ uint64_t ldu64(const uint8_t* base, uint64_t off) {
   return (uint64_t)ldu32(base, off) | ((uint64_t)ldu32(base, off + 4) << 32);
 }
 
+// A record's block_size and 32 fixed-field bytes (q .. q + 36) from three
+// dword-aligned loads (two dwordx4, one dwordx2) instead of one ldu32 (two
+// dword loads) per field: the record walks and the check/output pass issue
+// ~6x fewer load instructions per record.  at(k) = the u32 at q + 4k, k <= 8.
+// Reads up to 3 bytes past q + 36 (the stream is padded).
+struct __attribute__((aligned(4))) U32x4 { uint32_t x, y, z, w; };
+struct __attribute__((aligned(4))) U32x2 { uint32_t x, y; };
+struct RecHead {
+  uint32_t w[10];
+  uint32_t sh;
+  __device__ __forceinline__ uint32_t at(int k) const { return __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh); }
+};
+__device__ __forceinline__ RecHead load_head(const uint8_t* base, uint64_t q) {
+  const uint8_t* b = base + (q & ~3ull);
+  const U32x4 a = *reinterpret_cast<const U32x4*>(b);
+  const U32x4 c = *reinterpret_cast<const U32x4*>(b + 16);
+  const U32x2 d = *reinterpret_cast<const U32x2*>(b + 32);
+  RecHead h;
+  h.w[0] = a.x; h.w[1] = a.y; h.w[2] = a.z; h.w[3] = a.w;
+  h.w[4] = c.x; h.w[5] = c.y; h.w[6] = c.z; h.w[7] = c.w;
+  h.w[8] = d.x; h.w[9] = d.y;
+  h.sh = (uint32_t)(q & 3);
+  return h;
+}
+
 // ---------------------------------------------------------------------------
 // BGZF block discovery
 // ---------------------------------------------------------------------------
@@ -70,7 +95,10 @@ __global__ __launch_bounds__(256) void k_bgzf_scan(const uint8_t* __restrict__ b
   // coordinates (base + offset).
   // Four such wave steps per iteration (4 KiB per wave), their loads issued
   // together: one load in flight per wave left the scan latency-bound.
-  constexpr int kU = 4;
+#ifndef HBAM_SCAN_U
+#define HBAM_SCAN_U 4
+#endif
+  constexpr int kU = HBAM_SCAN_U;
   const uint64_t nc = (len + 15) / 16;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * kU;
   const uint32_t lane = lane_id();
@@ -2186,15 +2214,16 @@ __device__ bool aux_find(const uint8_t* u, uint64_t a, uint64_t e, uint16_t tag,
 constexpr uint32_t kWaveCigarOps = 32;
 __device__ bool record_invalid(const ChainEnv& E, uint64_t q, int32_t bs, bool strict, bool* defer = nullptr) {
   const uint8_t* u = E.u;
-  const int32_t ref = (int32_t)ldu32(u, q + 4), pos = (int32_t)ldu32(u, q + 8);
-  const uint32_t w12 = ldu32(u, q + 12), w16 = ldu32(u, q + 16);
+  const RecHead h = load_head(u, q);
+  const int32_t ref = (int32_t)h.at(1), pos = (int32_t)h.at(2);
+  const uint32_t w12 = h.at(3), w16 = h.at(4);
   const uint32_t lrn = w12 & 0xffu, mapq = (w12 >> 8) & 0xffu, bin = w12 >> 16;
   const uint32_t ncig = w16 & 0xffffu, flag = w16 >> 16;
   if (defer && ncig > kWaveCigarOps) {
     *defer = true;
     return false;
   }
-  const int32_t lseq = (int32_t)ldu32(u, q + 20), nref = (int32_t)ldu32(u, q + 24), npos = (int32_t)ldu32(u, q + 28);
+  const int32_t lseq = (int32_t)h.at(5), nref = (int32_t)h.at(6), npos = (int32_t)h.at(7);
   // structure: the lazy fields isValid decodes must lie inside the record
   if (lrn < 1 || lseq < 0) return true;
   const int64_t need = 32 + (int64_t)lrn + 4 * (int64_t)ncig + ((int64_t)lseq + 1) / 2 + (int64_t)lseq;
@@ -2524,14 +2553,15 @@ __device__ __forceinline__ bool dead_near(const ChainEnv& E, uint64_t q) {
 // drop-in window.)
 __device__ __forceinline__ bool plausible(const ChainEnv& E, uint64_t q) {
   if (q + 36 > E.e_inf) return E.e_inf < E.e_true && q + 4 <= E.e_inf && (int32_t)ldu32(E.u, q) >= 32;
-  int32_t bs = (int32_t)ldu32(E.u, q);
-  int32_t ref = (int32_t)ldu32(E.u, q + 4);
-  int32_t pos = (int32_t)ldu32(E.u, q + 8);
-  uint32_t lrn = ldu32(E.u, q + 12) & 0xffu;
-  uint32_t ncig = ldu32(E.u, q + 16) & 0xffffu;
-  int32_t lseq = (int32_t)ldu32(E.u, q + 20);
-  int32_t nref = (int32_t)ldu32(E.u, q + 24);
-  int32_t npos = (int32_t)ldu32(E.u, q + 28);
+  const RecHead h = load_head(E.u, q);
+  int32_t bs = (int32_t)h.at(0);
+  int32_t ref = (int32_t)h.at(1);
+  int32_t pos = (int32_t)h.at(2);
+  uint32_t lrn = h.at(3) & 0xffu;
+  uint32_t ncig = h.at(4) & 0xffffu;
+  int32_t lseq = (int32_t)h.at(5);
+  int32_t nref = (int32_t)h.at(6);
+  int32_t npos = (int32_t)h.at(7);
   if (ref < -1 || ref >= E.n_ref || nref < -1 || nref >= E.n_ref) return false;
   if (pos < -1 || npos < -1 || lrn < 1 || lseq < 0) return false;
   int64_t need = 32 + (int64_t)lrn + 4 * (int64_t)ncig + (int64_t)lseq + ((int64_t)lseq + 1) / 2;
@@ -2775,15 +2805,16 @@ __device__ uint64_t murmur3_dev(const uint8_t* u, uint64_t off, uint32_t len, in
 // Fields + key of the record at q into slot i of the columns.
 __device__ __forceinline__ void decode_record(const uint8_t* __restrict__ u, uint64_t q, uint64_t i,
                                               const Columns& col) {
-  const int32_t bs = (int32_t)ldu32(u, q);
-  const int32_t ref = (int32_t)ldu32(u, q + 4);
-  const int32_t pos = (int32_t)ldu32(u, q + 8);
-  const uint32_t w12 = ldu32(u, q + 12);
-  const uint32_t w16 = ldu32(u, q + 16);
-  const int32_t lseq = (int32_t)ldu32(u, q + 20);
-  const int32_t nref = (int32_t)ldu32(u, q + 24);
-  const int32_t npos = (int32_t)ldu32(u, q + 28);
-  const int32_t tlen = (int32_t)ldu32(u, q + 32);
+  const RecHead h = load_head(u, q);
+  const int32_t bs = (int32_t)h.at(0);
+  const int32_t ref = (int32_t)h.at(1);
+  const int32_t pos = (int32_t)h.at(2);
+  const uint32_t w12 = h.at(3);
+  const uint32_t w16 = h.at(4);
+  const int32_t lseq = (int32_t)h.at(5);
+  const int32_t nref = (int32_t)h.at(6);
+  const int32_t npos = (int32_t)h.at(7);
+  const int32_t tlen = (int32_t)h.at(8);
   const uint16_t flag = (uint16_t)(w16 >> 16);
   col.ref_id[i] = ref;
   col.pos[i] = pos;
