@@ -2212,9 +2212,10 @@ __device__ bool aux_find(const uint8_t* u, uint64_t a, uint64_t e, uint16_t tag,
 // *defer (when given): a cigar longer than kWaveCigarOps operators is not
 // checked here (false returned, *defer set) -- record_invalid_wave takes it.
 constexpr uint32_t kWaveCigarOps = 32;
-__device__ bool record_invalid(const ChainEnv& E, uint64_t q, int32_t bs, bool strict, bool* defer = nullptr) {
+// (h: the record's head, load_head(E.u, q), already in registers)
+__device__ __forceinline__ bool record_invalid_h(const ChainEnv& E, uint64_t q, int32_t bs, bool strict, bool* defer,
+                                                 const RecHead& h) {
   const uint8_t* u = E.u;
-  const RecHead h = load_head(u, q);
   const int32_t ref = (int32_t)h.at(1), pos = (int32_t)h.at(2);
   const uint32_t w12 = h.at(3), w16 = h.at(4);
   const uint32_t lrn = w12 & 0xffu, mapq = (w12 >> 8) & 0xffu, bin = w12 >> 16;
@@ -2340,6 +2341,10 @@ __device__ bool record_invalid(const ChainEnv& E, uint64_t q, int32_t bs, bool s
     }
   }
   return false;
+}
+
+__device__ bool record_invalid(const ChainEnv& E, uint64_t q, int32_t bs, bool strict, bool* defer = nullptr) {
+  return record_invalid_h(E, q, bs, strict, defer, load_head(E.u, q));
 }
 
 // record_invalid by a whole wave, for records with long cigars (ONT-like
@@ -2803,9 +2808,8 @@ __device__ uint64_t murmur3_dev(const uint8_t* u, uint64_t off, uint32_t len, in
 }
 
 // Fields + key of the record at q into slot i of the columns.
-__device__ __forceinline__ void decode_record(const uint8_t* __restrict__ u, uint64_t q, uint64_t i,
-                                              const Columns& col) {
-  const RecHead h = load_head(u, q);
+__device__ __forceinline__ void decode_record_h(const uint8_t* __restrict__ u, uint64_t q, uint64_t i,
+                                                const Columns& col, const RecHead& h) {
   const int32_t bs = (int32_t)h.at(0);
   const int32_t ref = (int32_t)h.at(1);
   const int32_t pos = (int32_t)h.at(2);
@@ -2842,10 +2846,14 @@ __device__ __forceinline__ void decode_record(const uint8_t* __restrict__ u, uin
         return;
       }
     }
-    const int32_t h = (int32_t)murmur3_dev(u, q + 36, (uint32_t)(bs - 32), 0);
-    key = (int64_t)((0x7fffffffull << 32) | (uint64_t)(int64_t)h);
+    const int32_t mh = (int32_t)murmur3_dev(u, q + 36, (uint32_t)(bs - 32), 0);
+    key = (int64_t)((0x7fffffffull << 32) | (uint64_t)(int64_t)mh);
   }
   col.key[i] = key;
+}
+__device__ __forceinline__ void decode_record(const uint8_t* __restrict__ u, uint64_t q, uint64_t i,
+                                              const Columns& col) {
+  decode_record_h(u, q, i, col, load_head(u, q));
 }
 
 // Murmur keys of long unmapped records (C4-like reads: the rest is tens of
@@ -3260,8 +3268,9 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, uint32_t src) {
 // *s = its status, *nd = bytes past the inflated range the record needs,
 // *long_cigar = its cigar was left to record_invalid_wave.
 template <int MODE>
-__device__ __forceinline__ void check_listed(const ChainEnv& E, uint64_t q, uint64_t lim, bool first, bool light,
-                                             bool* stop, bool* counted, int* s, uint64_t* nd, bool* long_cigar) {
+__device__ __forceinline__ void check_listed_h(const ChainEnv& E, uint64_t q, uint64_t lim, bool first, bool light,
+                                               bool* stop, bool* counted, int* s, uint64_t* nd, bool* long_cigar,
+                                               const RecHead& h) {
   const uint64_t avail = E.e_true - q;
   if (q >= lim) {
     *stop = true;  // outside the span
@@ -3276,7 +3285,7 @@ __device__ __forceinline__ void check_listed(const ChainEnv& E, uint64_t q, uint
       *stop = true;
       *nd = q + 4;
     } else {
-      const int32_t bs = (int32_t)ldu32(E.u, q);
+      const int32_t bs = (int32_t)h.at(0);
       if (bs < 32) {
         *stop = true;
         *s = kErrFormat;
@@ -3287,11 +3296,11 @@ __device__ __forceinline__ void check_listed(const ChainEnv& E, uint64_t q, uint
         *stop = true;
         *nd = q + 4 + (uint64_t)bs;
       } else {
-        const int32_t ref = (int32_t)ldu32(E.u, q + 4), nref = (int32_t)ldu32(E.u, q + 24);
+        const int32_t ref = (int32_t)h.at(1), nref = (int32_t)h.at(6);
         if (ref < -1 || ref >= E.n_ref || nref < -1 || nref >= E.n_ref) {
           *stop = true;
           *s = kErrArg;
-        } else if (E.validate && record_invalid(E, q, bs, E.validate == 2, long_cigar)) {
+        } else if (E.validate && record_invalid_h(E, q, bs, E.validate == 2, long_cigar, h)) {
           *stop = true;
           *s = kErrFormat;
         }
@@ -3307,7 +3316,7 @@ __device__ __forceinline__ void check_listed(const ChainEnv& E, uint64_t q, uint
       *stop = true;
       *nd = q + 4;
     } else {
-      const int32_t bs = (int32_t)ldu32(E.u, q);
+      const int32_t bs = (int32_t)h.at(0);
       if (bs > 0 && ((uint64_t)bs > avail - 4 || is_dead(E, q + 4))) {
         *stop = true;
         *counted = true;
@@ -3315,6 +3324,11 @@ __device__ __forceinline__ void check_listed(const ChainEnv& E, uint64_t q, uint
       }
     }
   }
+}
+template <int MODE>
+__device__ __forceinline__ void check_listed(const ChainEnv& E, uint64_t q, uint64_t lim, bool first, bool light,
+                                             bool* stop, bool* counted, int* s, uint64_t* nd, bool* long_cigar) {
+  check_listed_h<MODE>(E, q, lim, first, light, stop, counted, s, nd, long_cigar, load_head(E.u, q));
 }
 
 // One block's listed records checked by its wave: *count = the records before
@@ -3490,8 +3504,13 @@ __global__ __launch_bounds__(64, 6) void k_rec_check_out(ChainEnv E, const uint6
     bool stop = false, counted = false, long_cigar = false;
     int s = kOk;
     uint64_t x = 0;
-    if (r < listed)
-      check_listed<MODE>(E, q, lim, r == 0 && q == E.p0, light, &stop, &counted, &s, &x, &long_cigar);
+    // the record's head is loaded once for the checks and the output (three
+    // passes over it re-fetched its lines from HBM: 5.3 GB per C2 pass)
+    RecHead h{};
+    if (r < listed) {
+      h = load_head(E.u, q);
+      check_listed_h<MODE>(E, q, lim, r == 0 && q == E.p0, light, &stop, &counted, &s, &x, &long_cigar, h);
+    }
     uint32_t m = min(64u, listed - r0);  // records of this chunk that stand
     const uint64_t sm = __ballot(stop);
     bool halt = sm != 0;  // the block's count ends in this chunk
@@ -3522,7 +3541,7 @@ __global__ __launch_bounds__(64, 6) void k_rec_check_out(ChainEnv E, const uint6
       if (o < cap) {  // (sized from the lists' counts: always)
         rec_pos[o] = q;
         rec_voff[o] = (b.coff << 16) | (q - b.ustart);
-        if (DECODE) decode_record(E.u, q, o, col);
+        if (DECODE) decode_record_h(E.u, q, o, col, h);
       }
     }
     if (halt) {
