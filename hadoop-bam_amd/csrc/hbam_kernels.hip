@@ -374,21 +374,45 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
                                                      uint32_t* tab, uint32_t* cnt, uint16_t* sorted, uint32_t* sub,
                                                      int subcap) {
   const uint32_t lane = lane_id();
+#ifdef HBAM_TAB_PROBE
+  const uint64_t bt0 = clock64();
+  uint64_t bt1 = 0, bt2 = 0, bt3 = 0;
+#define BT_REPORT(tag) do { if (mode == 0 && lane == 0 && (blockIdx.x & 4095) == 17) \
+    printf("btprobe %s count %llu place %llu long %llu total %llu\n", tag, (unsigned long long)(bt1 - bt0), \
+           (unsigned long long)(bt2 ? bt2 - bt1 : 0), (unsigned long long)(bt3 ? bt3 - bt2 : 0), \
+           (unsigned long long)(clock64() - bt0)); } while (0)
+#else
+#define BT_REPORT(tag) do { } while (0)
+#endif
+  // Every symbol's code length stays in registers (nsym <= 320: 5 groups of
+  // 64), so do the canonical offsets and first codes (wave-uniform, picked
+  // per lane by a select chain): each LDS read on this path is a dependent
+  // round trip in a wave that has nothing else to do.
+  constexpr int kGroups = 5;
+  const int ng = (nsym + 63) >> 6;
+  uint32_t lv[kGroups];
+#pragma unroll
+  for (int g = 0; g < kGroups; ++g) {
+    const int s = 64 * g + (int)lane;
+    lv[g] = g < ng && s < nsym ? lens[s] : 0u;
+  }
   // counts per code length by ballots, then the Kraft check, the canonical
   // offsets and first codes as wave-uniform arithmetic (LDS atomics and a
   // one-lane loop over LDS cost ~3 K cycles per table)
   uint32_t cntv[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) cntv[q] = 0;
-  for (int c0 = 0; c0 < nsym; c0 += 64) {
-    const int s = c0 + (int)lane;
-    const uint32_t l = s < nsym ? lens[s] : 0;
 #pragma unroll
-    for (uint32_t q = 1; q < 16; ++q) cntv[q] += (uint32_t)__popcll(__ballot(l == q));
+  for (int g = 0; g < kGroups; ++g) {
+    if (g >= ng) break;  // wave-uniform
+#pragma unroll
+    for (uint32_t q = 1; q < 16; ++q) cntv[q] += (uint32_t)__popcll(__ballot(lv[g] == q));
   }
   int left = 1, maxl = 0;
   bool over = false;
-  uint32_t o = 0, code = 0, prev = 0, my_cnt = 0, my_off = 0, my_first = 0;
+  uint32_t o = 0, code = 0, prev = 0, my_cnt = 0;
+  uint32_t offu[16], firstu[16];
+  offu[0] = firstu[0] = 0;
 #pragma unroll
   for (uint32_t l = 1; l < 16; ++l) {
     const uint32_t c = cntv[l];
@@ -397,22 +421,21 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
     over = over || left < 0;
     code = (code + prev) << 1;
     my_cnt = lane == l ? c : my_cnt;
-    my_off = lane == l ? o : my_off;
-    my_first = lane == l ? code : my_first;
+    offu[l] = o;
+    firstu[l] = code;
     o += c;
     prev = c;
   }
-  if (lane < 16) {
-    cnt[lane] = my_cnt;
-    L.offs[lane] = my_off;
-    L.firstc[lane] = my_first;
-  }
+  if (lane < 16) cnt[lane] = my_cnt;
   uint32_t st = 0;
   if (over) st = 1;
   else if (maxl == 0) st = mode == 2 ? 1 : 2;
   else if (left > 0 && (mode == 2 || maxl != 1)) st = 1;
   for (int i = lane; i < (1 << root); i += 64) tab[i] = kBadEntry;
   wave_sync();
+#ifdef HBAM_TAB_PROBE
+  bt1 = clock64();
+#endif
   if (st == 1) return 1;
   if (st == 2) return 0;  // no codes: all-invalid table
   const uint32_t rmask = (1u << root) - 1;
@@ -423,22 +446,27 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
   uint32_t basev[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) basev[q] = 0;
-  for (int c0 = 0; c0 < nsym; c0 += 64) {
-    const int s = c0 + (int)lane;
-    const uint32_t l = s < nsym ? lens[s] : 0;
-    uint32_t rank = 0;
+  uint32_t revv[kGroups];
+#pragma unroll
+  for (int g = 0; g < kGroups; ++g) {
+    revv[g] = 0;
+    if (g >= ng) break;  // wave-uniform
+    const int s = 64 * g + (int)lane;
+    const uint32_t l = lv[g];
+    uint32_t rank = 0, off = 0, first = 0;
 #pragma unroll
     for (uint32_t q = 1; q < 16; ++q) {
       const uint64_t m = __ballot(l == q);
       rank = l == q ? basev[q] + (uint32_t)__popcll(m & ltmask) : rank;
+      off = l == q ? offu[q] : off;
+      first = l == q ? firstu[q] : first;
       basev[q] += (uint32_t)__popcll(m);
     }
     uint32_t rev = 0, e = 0;
     if (l) {
-      sorted[L.offs[l] + rank] = (uint16_t)s;
-      const uint32_t code = L.firstc[l] + rank;
-      rev = __brev(code) >> (32 - l);
-      L.rev_of[s] = (uint16_t)rev;
+      sorted[off + rank] = (uint16_t)s;
+      rev = __brev(first + rank) >> (32 - l);
+      revv[g] = rev;
       if ((int)l <= root) {
         e = make_entry(mode, (uint32_t)s, l);
         // a code that fills fewer than 64 root entries fills them itself; the
@@ -460,32 +488,49 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
     }
   }
   wave_sync();
-  if (__ballot(any_long) == 0) return 0;
-  // sub-table bases: exclusive scan of the sub-table sizes in root-index order
-  uint32_t used = 0;
-  for (int c0 = 0; c0 < (1 << root); c0 += 64) {
-    const uint32_t i = c0 + lane;
-    const uint32_t t = tab[i];
-    const bool mk = t >= kLongTag;
-    const uint32_t bits = t & 15u;
-    const uint32_t sz = mk ? (1u << bits) : 0u;
-    uint32_t inc = sz;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t v = __shfl_up(inc, d, 64);
-      if (lane >= (uint32_t)d) inc += v;
-    }
-    const uint32_t base = used + inc - sz;
-    if (mk) tab[i] = base + sz <= (uint32_t)subcap ? ((K_LONG << 26) | (bits << 16) | base) : (K_SLOW << 26);
-    used += (uint32_t)__shfl(inc, 63, 64);
+#ifdef HBAM_TAB_PROBE
+  bt2 = clock64();
+#endif
+  if (__ballot(any_long) == 0) {
+    BT_REPORT("short");
+    return 0;
   }
+  // sub-table bases: exclusive sum of the sub-table sizes in root-index
+  // order.  A table has a handful of long-code prefixes, so the marked
+  // entries of each 64-entry chunk are walked in lane order (a 6-step
+  // shuffle scan of every chunk, ds_bpermute each step, took ~12 K cycles);
+  // the root entries are read all at once first
+  constexpr int kChunks = (1 << kLitRoot) / 64;
+  const int nch = (1 << root) >> 6;
+  uint32_t tv[kChunks];
+#pragma unroll
+  for (int c = 0; c < kChunks; ++c) tv[c] = c < nch ? tab[64 * c + lane] : 0u;
+  uint32_t used = 0;
+#pragma unroll
+  for (int c = 0; c < kChunks; ++c) {
+    const uint32_t t = tv[c];  // 0 past the root table: no marks
+    for (uint64_t mm = __ballot(t >= kLongTag); mm; mm &= mm - 1) {
+      const int j = __ffsll((long long)mm) - 1;
+      const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)t, j) & 15u;
+      const uint32_t sz = 1u << bits;
+      if ((int)lane == j)
+        tab[64 * c + lane] = used + sz <= (uint32_t)subcap ? ((K_LONG << 26) | (bits << 16) | used) : (K_SLOW << 26);
+      used += sz;
+    }
+  }
+#ifdef HBAM_TAB_PROBE
+  bt3 = clock64();
+#endif
   const uint32_t nused = min(used, (uint32_t)subcap);
   for (uint32_t i = lane; i < nused; i += 64) sub[i] = kBadEntry;
   wave_sync();
-  for (int s = lane; s < nsym; s += 64) {
-    const uint32_t l = lens[s];
+#pragma unroll
+  for (int g = 0; g < kGroups; ++g) {
+    if (g >= ng) break;  // wave-uniform
+    const uint32_t l = lv[g];
     if ((int)l > root) {
-      const uint32_t rev = L.rev_of[s];
+      const int s = 64 * g + (int)lane;
+      const uint32_t rev = revv[g];
       const uint32_t e = tab[rev & rmask];
       if ((e >> 26) == K_LONG) {
         const uint32_t b = e & 0xffffu, sb = (e >> 16) & 15u;
@@ -495,7 +540,9 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
     }
   }
   wave_sync();
+  BT_REPORT("long");
   return 0;
+#undef BT_REPORT
 }
 
 // Fold two consecutive literals into one litlen entry when both codes fit in
