@@ -51,6 +51,20 @@ for s in $STEPS; do
           > $OUT/dropin_ramp_$r.log 2>&1 || { echo "dropin probe failed"; tail -30 $OUT/dropin_ramp_$r.log; exit 6; }
         echo "ramp=$r"; grep -E "^(mapped|resident)" $OUT/dropin_ramp_$r.log | cut -c1-140
       done ;;
+    feeds)
+      # the drop-in 1 M-batch loop with fewer host copy threads staging the next window beside the batch D2H
+      for f in ${FEEDS:-2 4 8}; do
+        HBAM_FEED_THREADS=$f timeout -k 10 300 python -u scripts/dropin_probe2.py 10000000 --torch --steps none,none \
+          > $OUT/dropin_feed_$f.log 2>&1 || { echo "dropin probe failed"; tail -30 $OUT/dropin_feed_$f.log; exit 6; }
+        echo "feed threads=$f"; grep -E "^(mapped|resident)" $OUT/dropin_feed_$f.log | cut -c1-140
+      done ;;
+    envs)
+      # the drop-in 1 M-batch loop under each VAR=VALUE of ENVS (runtime knobs)
+      for e in ${ENVS:-NONE=0}; do
+        env $e timeout -k 10 300 python -u scripts/dropin_probe2.py 10000000 --torch --steps none,none \
+          > $OUT/dropin_env_$e.log 2>&1 || { echo "dropin probe failed"; tail -30 $OUT/dropin_env_$e.log; exit 6; }
+        echo "env $e"; grep -E "^(mapped|resident)" $OUT/dropin_env_$e.log | cut -c1-140
+      done ;;
     order)
       # the drop-in loop before and after hbam_gpu_run_streamed (the pinned-host leg), clocks and link sampled
       timeout -k 10 400 python -u scripts/dropin_probe2.py 10000000 --torch --smi --steps none,run_streamed,none,none \
