@@ -13,6 +13,9 @@
 // stays here: building the LazyBAMRecord of each record from the batch's
 // columns, exactly the arguments htsjdk's BAMRecordCodec.decode passes to
 // LazyBAMRecordFactory.createBAMRecord (LazyBAMRecordFactory.java:37-50).
+// With hadoopbam.gpu.encode-writables the values are GpuSAMRecordWritables
+// that also carry their SAMRecordWritable.write bytes, encoded per batch on
+// the GPU (hbam_encode_writables).
 //
 // Bounded traversal (intervals / unmapped-only, BAMRecordReader.java:170-178)
 // is outside the GPU path: such splits are read by the stock BAMRecordReader
@@ -45,8 +48,12 @@ public class GpuBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
   public static final String WINDOW_BYTES_PROPERTY = "hadoopbam.gpu.window-bytes";
 
   private final LongWritable key = new LongWritable();
-  private final SAMRecordWritable record = new SAMRecordWritable();
   private final LazyBAMRecordFactory factory = new LazyBAMRecordFactory();
+  // a GpuSAMRecordWritable carrying its record's writable bytes when
+  // hadoopbam.gpu.encode-writables is set (GpuSAMRecordWritable.java)
+  private SAMRecordWritable record = new SAMRecordWritable();
+  private boolean encode;
+  private GpuSAMRecordWritable.EncodedBatch encoded;  // the current batch's writable bytes
 
   private HbamFiles.Handle file;  // the open ctx (and its stream on a non-local file system)
   private long ctx;  // file.ctx, 0 when closed
@@ -102,6 +109,8 @@ public class GpuBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     fileStart = virtualStart >>> 16;
     virtualEnd = split.getEndVirtualOffset();
     batchRecords = conf.getLong(BATCH_RECORDS_PROPERTY, 1L << 20);
+    encode = conf.getBoolean(GpuSAMRecordWritable.ENCODE_PROPERTY, false);
+    record = encode ? new GpuSAMRecordWritable() : new SAMRecordWritable();
 
     // the file through its own file system, as WrapSeekable.openPath (:147):
     // a local path is read with pread, HDFS and the rest through positioned
@@ -124,6 +133,8 @@ public class GpuBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     for (ByteBuffer b : cols) b.order(ByteOrder.LITTLE_ENDIAN);
     n = cols[HbamNative.KEY].capacity() / 8;
     i = 0;
+    // hbam_encode_writables encodes the last decodeSpan batch: now, before the next call
+    encoded = encode && n > 0 ? GpuSAMRecordWritable.EncodedBatch.of(ctx, n) : null;
   }
 
   @Override
@@ -134,6 +145,7 @@ public class GpuBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
       ctx = 0;
     }
     cols = null;
+    encoded = null;
   }
 
   /**
@@ -176,14 +188,21 @@ public class GpuBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
       }
     }
     key.set(cols[HbamNative.KEY].getLong(8 * i));
-    record.set(recordAt(i));
+    final SAMRecord r = recordAt(cols, i, header, factory);
+    r.setValidationStringency(stringency);
+    if (encoded != null) ((GpuSAMRecordWritable) record).setEncoded(r, encoded, i);
+    else record.set(r);
     ++i;
     started = true;
     return true;
   }
 
-  /** The LazyBAMRecord htsjdk's BAMRecordCodec.decode builds for record j. */
-  private SAMRecord recordAt(int j) {
+  /**
+   * The LazyBAMRecord htsjdk's BAMRecordCodec.decode builds for record j of a
+   * batch (decodeSpan or decodeWritables columns); header null as
+   * SAMRecordWritable's lazyCodec (SAMRecordWritable.java:47-48).
+   */
+  static SAMRecord recordAt(ByteBuffer[] cols, int j, SAMFileHeader header, LazyBAMRecordFactory factory) {
     final ByteBuffer data = cols[HbamNative.DATA];
     final long off = cols[HbamNative.REST_OFF].getLong(8 * j);
     final int len = cols[HbamNative.REST_LEN].getInt(4 * j);
@@ -205,7 +224,6 @@ public class GpuBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
         cols[HbamNative.NEXT_POS].getInt(4 * j) + 1,
         cols[HbamNative.TLEN].getInt(4 * j),
         rest);
-    r.setValidationStringency(stringency);
     return r;
   }
 

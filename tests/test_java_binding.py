@@ -4,7 +4,8 @@ No JDK exists in this image, so the Java classes and the JNI glue are checked
 textually: every native method of HbamNative has its JNI function, every
 hbam_* call of the glue is declared in include/hbam.h, and every HbamNative
 method the delegating classes (GpuBAMRecordReader, GpuBAMInputFormat,
-GpuSplittingBAMIndexer) call exists with that arity."""
+GpuSplittingBAMIndexer, GpuSAMRecordWritable, GpuBAMRecordWriter) call exists
+with that arity."""
 import os
 import re
 
@@ -53,7 +54,7 @@ def test_delegating_classes_call_existing_natives():
     natives = _natives()
     seen = set()
     for cls in ("GpuBAMRecordReader.java", "GpuBAMInputFormat.java", "GpuSplittingBAMIndexer.java",
-                os.path.join("gpu", "HbamFiles.java")):
+                "GpuSAMRecordWritable.java", "GpuBAMRecordWriter.java", os.path.join("gpu", "HbamFiles.java")):
         src = _strip_comments(open(os.path.join(JAVA, cls)).read())
         assert "package org.seqdoop.hadoop_bam" in src
         for m in re.finditer(r"HbamNative\.(\w+)\(", src):
@@ -73,7 +74,8 @@ def test_delegating_classes_call_existing_natives():
             assert nargs == natives[name], (cls, name, nargs, natives[name])
             seen.add(name)
     # the reader path, the indexer and the planner all go through the boundary
-    assert {"open", "openReader", "close", "decodeSpan", "readerPosition", "getSplits", "splittingIndex"} <= seen
+    assert {"open", "openReader", "close", "decodeSpan", "readerPosition", "getSplits", "splittingIndex",
+            "encodeWritables", "decodeWritables", "bgzfCompress"} <= seen
 
 
 def test_reader_mirrors_the_reference_reader_surface():
@@ -125,3 +127,34 @@ def test_write_time_indexer_keeps_o1_state():
     assert "private long count;" in src
     assert src.count("count == 0 || (count + 1) % granularity == 0") == 2
     assert "long[] voffs" not in src and "Arrays.copyOf" not in src
+
+
+REF = "/root/reference/src/main/java/org/seqdoop/hadoop_bam"
+
+
+def test_writable_and_writer_mirror_the_reference_surface():
+    """GpuSAMRecordWritable is a SAMRecordWritable (write / readFields of
+    SAMRecordWritable.java:55-68 overridden); GpuBAMRecordWriter has
+    BAMRecordWriter's constructors, close and writeAlignment
+    (BAMRecordWriter.java:61-150), and the key-ignoring writer its write
+    (KeyIgnoringBAMRecordWriter.java:63-65)."""
+    w = _strip_comments(open(os.path.join(JAVA, "GpuSAMRecordWritable.java")).read())
+    assert "class GpuSAMRecordWritable extends SAMRecordWritable" in w
+    have = _public_signatures(w)
+    assert {("write", ("DataOutput",)), ("readFields", ("DataInput",)), ("set", ("SAMRecord",))} <= have
+    r = _strip_comments(open(os.path.join(JAVA, "GpuBAMRecordWriter.java")).read())
+    assert "extends RecordWriter<K, SAMRecordWritable>" in r
+    if os.path.exists(os.path.join(REF, "BAMRecordWriter.java")):
+        ref = _public_signatures(_strip_comments(open(os.path.join(REF, "BAMRecordWriter.java")).read()))
+        ref = {("GpuBAMRecordWriter" if n == "BAMRecordWriter" else n, t) for n, t in ref}
+    else:  # the reference's list, as read from the file above when it was present
+        ref = {("GpuBAMRecordWriter", ("Path", "Path", "boolean", "TaskAttemptContext")),
+               ("GpuBAMRecordWriter", ("Path", "SAMFileHeader", "boolean", "TaskAttemptContext")),
+               ("GpuBAMRecordWriter", ("OutputStream", "SAMFileHeader", "boolean")),
+               ("close", ("TaskAttemptContext",))}
+    assert ref <= _public_signatures(r), ref - _public_signatures(r)
+    assert "protected void writeAlignment(final SAMRecord rec)" in r
+    k = _strip_comments(open(os.path.join(JAVA, "GpuKeyIgnoringBAMRecordWriter.java")).read())
+    assert "extends GpuBAMRecordWriter<K>" in k and "public void write(K ignored, SAMRecordWritable rec)" in k
+    # the stock stream's cut: BlockCompressedOutputStream's buffer size, htsjdk's default level
+    assert "BlockCompressedStreamConstants.DEFAULT_UNCOMPRESSED_BLOCK_SIZE" in r and "Defaults.COMPRESSION_LEVEL" in r
