@@ -355,12 +355,16 @@ int SpanCursor::issue(const Window& w, uint64_t k, uint64_t m, Slot* s, std::str
   // the batch-major copy of the columns when this batch is one of its blocks
   // (block k / pack_m holds min(pack_m, n - k) records)
   s->packed = w.pack_m && k % w.pack_m == 0 && m == std::min(w.pack_m, w.n - k);
+  // rest_off stays on the device: the rests are back to back, so the host
+  // takes it as the prefix sum of rest_len when the batch lands (next_batch);
+  // 8 of a record's ~364 bytes on a link-bound loop
   if (s->packed) {
-    CCHK(hipMemcpyAsync(h, w.packed.p + (k / w.pack_m) * ColLayout(w.pack_m, false).bytes, L.bytes,
+    const uint8_t* blk = w.packed.p + (k / w.pack_m) * ColLayout(w.pack_m, false).bytes;
+    CCHK(hipMemcpyAsync(h, blk, L.off[ColLayout::kRestOff], hipMemcpyDeviceToHost, d2h_));
+    CCHK(hipMemcpyAsync(h + L.off[ColLayout::kVoff], blk + L.off[ColLayout::kVoff], L.bytes - L.off[ColLayout::kVoff],
                         hipMemcpyDeviceToHost, d2h_));
   } else {
     CCHK(col(ColLayout::kKey, src.key));
-    CCHK(col(ColLayout::kRestOff, src.rest_off));
     CCHK(col(ColLayout::kVoff, src.voff));
     CCHK(col(ColLayout::kRefId, src.ref_id));
     CCHK(col(ColLayout::kPos, src.pos));
@@ -467,16 +471,23 @@ int SpanCursor::next_batch(BamFile& f, uint64_t vstart, uint64_t vend, uint64_t 
   ctrace("batch landed", k_);
   S.busy = false;
   // the batch: columns at ColLayout(m), the rests after them; rest_off in
-  // the rests from the batch's first record (the export kept them slot-
-  // relative in the record bytes)
+  // the rests from the batch's first record, the prefix sum of rest_len
+  // (issue() leaves it out of the copy)
   const ColLayout L(m, false);
   uint8_t* h = S.mem;
-  if (!S.packed) {  // slot position of record i's rest -> its offset among the batch's rests
-    uint64_t* ro = reinterpret_cast<uint64_t*>(h + L.off[ColLayout::kRestOff]);
-    const uint64_t base = S.start;
-    for (uint64_t i = 0; i < m; ++i) ro[i] -= base + 36 * (i + 1);
-  }
   const hbam::Columns c = L.at(h, nullptr);
+  {
+    uint64_t acc = 0;
+    for (uint64_t i = 0; i < m; ++i) {
+      c.rest_off[i] = acc;
+      acc += c.rest_len[i];
+    }
+    if (acc != (S.end - S.start) - 36 * m) {
+      valid_ = false;
+      *err = "batch rest lengths do not add up to its record bytes";
+      return kErrState;
+    }
+  }
   out->n = m;
   out->ref_id = c.ref_id;
   out->pos = c.pos;

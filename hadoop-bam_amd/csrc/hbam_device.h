@@ -53,7 +53,7 @@ constexpr int32_t kHuffPending = -2;
 constexpr uint32_t kInflateRounds = 4;  // zlib: <= 4 DEFLATE blocks of 16383 symbols per 64 KiB BGZF block
 
 // Phase-A table prebuild (k_huff_tables -> k_inflate_huff), per block of a chunk.
-constexpr uint32_t kHuffTableImage = 11008;  // bytes of the LDS table image
+constexpr uint32_t kHuffTableImage = 8704;  // bytes of the LDS table image
 struct HuffTableInfo {
   uint32_t status;     // 0: tables + B0 valid; else decode the block's headers inline
   uint32_t B0;         // bit of the first symbol (relative to the 16 B-aligned cdata base)

@@ -295,11 +295,14 @@ constexpr int kDistRoot = 9;
 // Variable-size sub-tables (as zlib's inflate_table): the root entry of a
 // long-code prefix holds the sub-table base and its index width (= the longest
 // code under that prefix - root).  A complete litlen code with a 10-bit root
-// needs at most 310 sub entries (zlib ENOUGH_LENS 1334 - 1024); the distance
-// code with a 9-bit root fits the same capacity.  Prefixes that would not fit
-// fall back to K_SLOW (canonical decode), which valid streams never reach.
-constexpr int kLitSubCap = 512;
-constexpr int kDistSubCap = 512;
+// needs at most 310 sub entries (zlib ENOUGH_LENS 1334 - 1024), the distance
+// code with a 9-bit root at most 80 (ENOUGH_DISTS 592 - 512); build_table
+// accepts complete codes only (and the one-code case).  Prefixes that would
+// not fit fall back to K_SLOW (canonical decode), which valid streams never
+// reach.  The caps size the table image every block writes and phase A reads
+// back, and the LDS that bounds k_huff_tables' resident waves.
+constexpr int kLitSubCap = 320;
+constexpr int kDistSubCap = 128;
 enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_LONG = 3, K_BAD = 4, K_SLOW = 5 };
 constexpr uint32_t kBadEntry = K_BAD << 26;
 constexpr uint32_t kLongTag = 0xF0000000u;  // build-time mark: kLongTag | (max len - root)
@@ -747,8 +750,8 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
       {  // a code longer than the root (rare): every lane reads, long ones keep it
         const bool lg = (e >> 26) == K_LONG;
         if (__builtin_amdgcn_ballot_w64(lg)) {
-          const uint32_t es = L.litsub[((e & 0xffffu) + __builtin_amdgcn_ubfe(lo, kLitRoot, (e >> 16) & 15u)) &
-                                       (kLitSubCap - 1)];
+          const uint32_t es = L.litsub[min((e & 0xffffu) + __builtin_amdgcn_ubfe(lo, kLitRoot, (e >> 16) & 15u),
+                                           (uint32_t)kLitSubCap - 1)];  // in bounds for the lanes that drop it
           e = lg ? es : e;
         }
       }
@@ -764,8 +767,8 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
       {
         const bool lg = (d >> 26) == K_LONG;
         if (__builtin_amdgcn_ballot_w64(lg)) {
-          const uint32_t ds = L.distsub[((d & 0xffffu) + __builtin_amdgcn_ubfe(b2, kDistRoot, (d >> 16) & 15u)) &
-                                        (kDistSubCap - 1)];
+          const uint32_t ds = L.distsub[min((d & 0xffffu) + __builtin_amdgcn_ubfe(b2, kDistRoot, (d >> 16) & 15u),
+                                            (uint32_t)kDistSubCap - 1)];
           d = lg ? ds : d;
         }
       }
@@ -1291,7 +1294,7 @@ __global__ __launch_bounds__(64) void k_huff_tables(const uint8_t* __restrict__ 
                                                     const HuffOut* __restrict__ hout, uint32_t round) {
   __shared__ __attribute__((aligned(16))) HuffLds L;
   __shared__ __attribute__((aligned(16))) uint4 s_in[kTabStageBytes / 16 + 1];
-  __shared__ ClLds C;
+  ClLds& C = *reinterpret_cast<ClLds*>(L.lit);  // code-length symbols: done before lit[] is built
   const uint32_t lane = lane_id();
   const uint32_t bi = b0 + blockIdx.x;
 #ifdef HBAM_TAB_PROBE
