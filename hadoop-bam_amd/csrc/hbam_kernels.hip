@@ -377,6 +377,138 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
                                                      uint32_t* tab, uint32_t* cnt, uint16_t* sorted, uint32_t* sub,
                                                      int subcap) {
   const uint32_t lane = lane_id();
+  // counts per code length by ballots, then the Kraft check, the canonical
+  // offsets and first codes as wave-uniform arithmetic (LDS atomics and a
+  // one-lane loop over LDS cost ~3 K cycles per table)
+  uint32_t cntv[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) cntv[q] = 0;
+  for (int c0 = 0; c0 < nsym; c0 += 64) {
+    const int s = c0 + (int)lane;
+    const uint32_t l = s < nsym ? lens[s] : 0;
+#pragma unroll
+    for (uint32_t q = 1; q < 16; ++q) cntv[q] += (uint32_t)__popcll(__ballot(l == q));
+  }
+  int left = 1, maxl = 0;
+  bool over = false;
+  uint32_t o = 0, code = 0, prev = 0, my_cnt = 0, my_off = 0, my_first = 0;
+#pragma unroll
+  for (uint32_t l = 1; l < 16; ++l) {
+    const uint32_t c = cntv[l];
+    left = (left << 1) - (int)c;
+    maxl = c ? (int)l : maxl;
+    over = over || left < 0;
+    code = (code + prev) << 1;
+    my_cnt = lane == l ? c : my_cnt;
+    my_off = lane == l ? o : my_off;
+    my_first = lane == l ? code : my_first;
+    o += c;
+    prev = c;
+  }
+  if (lane < 16) {
+    cnt[lane] = my_cnt;
+    L.offs[lane] = my_off;
+    L.firstc[lane] = my_first;
+  }
+  uint32_t st = 0;
+  if (over) st = 1;
+  else if (maxl == 0) st = mode == 2 ? 1 : 2;
+  else if (left > 0 && (mode == 2 || maxl != 1)) st = 1;
+  for (int i = lane; i < (1 << root); i += 64) tab[i] = kBadEntry;
+  wave_sync();
+  if (st == 1) return 1;
+  if (st == 2) return 0;  // no codes: all-invalid table
+  const uint32_t rmask = (1u << root) - 1;
+  const uint64_t ltmask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  bool any_long = false;
+  // next canonical rank per code length: wave-uniform, kept in registers (an
+  // LDS counter costs a dependent LDS round trip per length and group)
+  uint32_t basev[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) basev[q] = 0;
+  for (int c0 = 0; c0 < nsym; c0 += 64) {
+    const int s = c0 + (int)lane;
+    const uint32_t l = s < nsym ? lens[s] : 0;
+    uint32_t rank = 0;
+#pragma unroll
+    for (uint32_t q = 1; q < 16; ++q) {
+      const uint64_t m = __ballot(l == q);
+      rank = l == q ? basev[q] + (uint32_t)__popcll(m & ltmask) : rank;
+      basev[q] += (uint32_t)__popcll(m);
+    }
+    uint32_t rev = 0, e = 0;
+    if (l) {
+      sorted[L.offs[l] + rank] = (uint16_t)s;
+      const uint32_t code = L.firstc[l] + rank;
+      rev = __brev(code) >> (32 - l);
+      L.rev_of[s] = (uint16_t)rev;
+      if ((int)l <= root) {
+        e = make_entry(mode, (uint32_t)s, l);
+        // a code that fills fewer than 64 root entries fills them itself; the
+        // wave fills the wider ones together below (a lane alone took up to
+        // 2^(root - l) dependent trips, and the wave waited for the longest)
+        if ((int)l > root - 6)
+          for (uint32_t i = rev; i < (1u << root); i += (1u << l)) tab[i] = e;
+      } else {
+        atomicMax(&tab[rev & rmask], kLongTag | (l - (uint32_t)root));  // widest sub-table under the prefix
+        any_long = true;
+      }
+    }
+    for (uint64_t wm = __ballot(l != 0 && (int)l <= root - 6); wm; wm &= wm - 1) {
+      const int src = __ffsll((long long)wm) - 1;
+      const uint32_t wl = (uint32_t)__shfl((int)l, src, 64);
+      const uint32_t wr = (uint32_t)__shfl((int)rev, src, 64);
+      const uint32_t we = (uint32_t)__shfl((int)e, src, 64);
+      for (uint32_t k = lane; k < (1u << (root - (int)wl)); k += 64) tab[wr + (k << wl)] = we;
+    }
+  }
+  wave_sync();
+  if (__ballot(any_long) == 0) return 0;
+  // sub-table bases: exclusive scan of the sub-table sizes in root-index order
+  uint32_t used = 0;
+  for (int c0 = 0; c0 < (1 << root); c0 += 64) {
+    const uint32_t i = c0 + lane;
+    const uint32_t t = tab[i];
+    const bool mk = t >= kLongTag;
+    const uint32_t bits = t & 15u;
+    const uint32_t sz = mk ? (1u << bits) : 0u;
+    uint32_t inc = sz;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t v = __shfl_up(inc, d, 64);
+      if (lane >= (uint32_t)d) inc += v;
+    }
+    const uint32_t base = used + inc - sz;
+    if (mk) tab[i] = base + sz <= (uint32_t)subcap ? ((K_LONG << 26) | (bits << 16) | base) : (K_SLOW << 26);
+    used += (uint32_t)__shfl(inc, 63, 64);
+  }
+  const uint32_t nused = min(used, (uint32_t)subcap);
+  for (uint32_t i = lane; i < nused; i += 64) sub[i] = kBadEntry;
+  wave_sync();
+  for (int s = lane; s < nsym; s += 64) {
+    const uint32_t l = lens[s];
+    if ((int)l > root) {
+      const uint32_t rev = L.rev_of[s];
+      const uint32_t e = tab[rev & rmask];
+      if ((e >> 26) == K_LONG) {
+        const uint32_t b = e & 0xffffu, sb = (e >> 16) & 15u;
+        const uint32_t ent = make_entry(mode, (uint32_t)s, l);
+        for (uint32_t k = rev >> root; k < (1u << sb); k += 1u << (l - root)) sub[b + k] = ent;
+      }
+    }
+  }
+  wave_sync();
+  return 0;
+}
+
+// The same build with its per-length state and the code lengths in registers
+// (k_huff_tables, §7 item 2 of DESIGN.md): ~25 % faster per table, but its
+// ~116 VGPRs would spill k_inflate_huff, whose rare inline header path calls
+// the LDS-state build_table above.
+__device__ __attribute__((noinline)) int build_table_r(HuffLds& L, const uint8_t* lens, int nsym, int root, int mode,
+                                                     uint32_t* tab, uint32_t* cnt, uint16_t* sorted, uint32_t* sub,
+                                                     int subcap) {
+  const uint32_t lane = lane_id();
 #ifdef HBAM_TAB_PROBE
   const uint64_t bt0 = clock64();
   uint64_t bt1 = 0, bt2 = 0, bt3 = 0;
@@ -1142,6 +1274,14 @@ __device__ __forceinline__ uint32_t peek32(const uint32_t* W, uint32_t p) {
   return __builtin_amdgcn_alignbit(W[(p >> 5) + 1], W[p >> 5], p & 31);
 }
 
+// build_table_r for k_huff_tables (REG), build_table for k_inflate_huff's inline path
+template <bool REG, typename... A>
+__device__ __forceinline__ int build_tab(A&&... a) {
+  if constexpr (REG) return build_table_r(static_cast<A&&>(a)...);
+  else return build_table(static_cast<A&&>(a)...);
+}
+
+template <bool REG>
 __device__ int dyn_header_par(HuffLds& L, ClLds& C, const uint32_t* __restrict__ W, uint32_t p, uint32_t E,
                               uint32_t* end_pos, uint64_t* probe = nullptr) {
   const uint32_t lane = lane_id();
@@ -1161,7 +1301,7 @@ __device__ int dyn_header_par(HuffLds& L, ClLds& C, const uint32_t* __restrict__
   if (lane < hclen) L.cl_lens[kClOrder[lane]] = (uint8_t)(peek32(W, p + 3 * lane) & 7);
   wave_sync();
   p += 3 * hclen;
-  if (rfl(build_table(L, L.cl_lens, 19, 7, 2, L.dist, L.cnt_dist, L.sort_dist, nullptr, 0))) return DH_TRUNC;
+  if (rfl(build_tab<REG>(L, L.cl_lens, 19, 7, 2, L.dist, L.cnt_dist, L.sort_dist, nullptr, 0))) return DH_TRUNC;
   DH_PROBE(0);
   const uint32_t ntot = hlit + hdist;
   uint32_t done = 0, prevv = 0, have_prev = 0;
@@ -1264,10 +1404,10 @@ __device__ int dyn_header_par(HuffLds& L, ClLds& C, const uint32_t* __restrict__
   wave_sync();
   DH_PROBE(1);
   if (rfl(L.lens[256]) == 0) return DH_TRUNC;
-  if (rfl(build_table(L, L.lens, (int)hlit, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit, L.litsub, kLitSubCap)))
+  if (rfl(build_tab<REG>(L, L.lens, (int)hlit, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit, L.litsub, kLitSubCap)))
     return DH_TRUNC;
   DH_PROBE(2);
-  if (rfl(build_table(L, L.lens + hlit, (int)hdist, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist, L.distsub,
+  if (rfl(build_tab<REG>(L, L.lens + hlit, (int)hdist, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist, L.distsub,
                       kDistSubCap)))
     return DH_TRUNC;
   DH_PROBE(3);
@@ -1336,9 +1476,9 @@ __global__ __launch_bounds__(64) void k_huff_tables(const uint8_t* __restrict__ 
       uint32_t b0pos = 0;
       const uint32_t hp = R.pos();
 #ifdef HBAM_TAB_PROBE
-      if (dyn_header_par(L, C, R.W, hp, E, &b0pos, dp) == DH_OK) {
+      if (dyn_header_par<true>(L, C, R.W, hp, E, &b0pos, dp) == DH_OK) {
 #else
-      if (dyn_header_par(L, C, R.W, hp, E, &b0pos) == DH_OK) {
+      if (dyn_header_par<true>(L, C, R.W, hp, E, &b0pos) == DH_OK) {
 #endif
         wave_sync();
 #ifdef HBAM_TAB_PROBE
@@ -1655,7 +1795,7 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
             est = block_bits_estimate(L.lens, 288, 32);
           } else {  // dynamic Huffman: code lengths decoded by the 64 lanes of the wave
             uint32_t endp = 0;
-            int dh = dyn_header_par(L, *reinterpret_cast<ClLds*>(L.lit), W, R.pos(), E, &endp);
+            int dh = dyn_header_par<false>(L, *reinterpret_cast<ClLds*>(L.lit), W, R.pos(), E, &endp);
             if (rfl(dh) == DH_OK) {
               R.seek(endp);
             } else {  // an anomaly: the serial parse owns zlib's error semantics
