@@ -177,8 +177,8 @@ SALU_PER_CU_CYCLE = 1  # one scalar ALU per CU
 PMC_PASSES = (  # one rocprofv3 --pmc run each (FETCH_SIZE / WRITE_SIZE use 3 / 2 of the 4 TCC slots)
     ("fetch", ["FETCH_SIZE"]),
     ("write", ["WRITE_SIZE"]),
-    ("issue", ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_WAVES",
-               "GRBM_GUI_ACTIVE"]),
+    ("issue", ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
+               "SQ_WAIT_INST_LDS", "SQ_WAVE_CYCLES", "SQ_WAVES", "GRBM_GUI_ACTIVE"]),
 )
 
 
@@ -239,9 +239,17 @@ def pmc_traffic(path, vstart, vend, kernel):
                                                     max(out.get("SQ_INSTS_LDS", 0), 1), 3),
             "waves_per_launch": int(out.get("SQ_WAVES", 0)), "cycles_per_launch": int(cyc),
             "valu_frac": round(valu * VALU_CYCLES / (N_SIMD * cyc), 4),
+            # LDS-array cycles (SQ_LDS_IDX_ACTIVE: every cycle the array serves a
+            # wave-instruction, conflicts included) against one array per CU
+            "lds_idx_active_per_launch": int(out.get("SQ_LDS_IDX_ACTIVE", 0)),
+            "lds_cycles_per_lds_inst": round(out.get("SQ_LDS_IDX_ACTIVE", 0) / max(out.get("SQ_INSTS_LDS", 0), 1), 3),
+            "lds_frac": round(out.get("SQ_LDS_IDX_ACTIVE", 0) / (N_CU * cyc), 4),
+            "wait_inst_lds_frac_of_wave_cycles": round(out.get("SQ_WAIT_INST_LDS", 0) /
+                                                       max(out.get("SQ_WAVE_CYCLES", 0), 1), 4),
             "salu_frac": round(salu / (N_CU * SALU_PER_CU_CYCLE * cyc), 4),
             "rule": f"valu_frac = SQ_INSTS_VALU x {VALU_CYCLES} cycles / ({N_SIMD} SIMDs x cycles); salu_frac = "
-                    f"SQ_INSTS_SALU / ({N_CU} CUs x cycles); cycles = GRBM_GUI_ACTIVE / 8 (XCDs) of the launch"}
+                    f"SQ_INSTS_SALU / ({N_CU} CUs x cycles); lds_frac = SQ_LDS_IDX_ACTIVE / ({N_CU} CUs x cycles); "
+                    f"cycles = GRBM_GUI_ACTIVE / 8 (XCDs) of the launch"}
     return res
 
 
@@ -426,7 +434,9 @@ def roofline_of(stats, world=1):
         n_launch *= INFLATE_ROUNDS
     b_alg = st["compressed_bytes"] + st["inflated_bytes"] + SOA_BYTES_PER_RECORD * st["records"]
     achieved = b_alg / (dom_ms * 1e-3) / 1e9
-    return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+    # "unmeasured" until the in-session PMC passes (main()) set limits / bound:
+    # the kernel's binding unit is a measured claim, never a default
+    return {"bound": "unmeasured", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
             "launches_per_pass": n_launch, "avg_launch_ms": round(dom_ms / n_launch, 4),
             "alg_bytes_per_launch": int(b_alg / n_launch),
@@ -624,7 +634,7 @@ def write_legs(path, size, info_u):
         d2d = g.d2d_bandwidth(1 << 32, 5)
         res["writable_encode"] = {
             "bytes": nb, "ms": round(ms, 4), "GBps_encoded": round(nb / ms / 1e6, 2),
-            "roofline": {"bound": "hbm", "achieved": round(2 * nb / ms / 1e6, 2), "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "unmeasured", "achieved": round(2 * nb / ms / 1e6, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(2 * nb / ms / 1e6 / HBM_PEAK_GBS, 4)},
             "frac_of_measured_d2d": round(2 * nb / ms / 1e6 / d2d, 4)}
         res["d2d_copy_GBps_measured"] = round(d2d, 1)
@@ -834,13 +844,14 @@ def run_c2(D, args, steps, warmup, extras):
                         if "issue" in tr:
                             rf["issue"] = tr["issue"]
                             lim = {"hbm": rf["frac"], "valu_issue": tr["issue"]["valu_frac"],
-                                   "salu_issue": tr["issue"]["salu_frac"],
+                                   "salu_issue": tr["issue"]["salu_frac"], "lds": tr["issue"]["lds_frac"],
                                    "hbm_traffic": tr["bytes_per_launch"] / (rf["avg_launch_ms"] * 1e-3) / 1e9
                                    / HBM_PEAK_GBS}
                             rf["limits"] = {k: round(v, 4) for k, v in lim.items()}
                             rf["bound"] = max(lim, key=lim.get).replace("hbm_traffic", "hbm")
                             rf["bound_rule"] = ("the largest of: algorithmic HBM bytes / peak (frac), measured "
-                                                "HBM traffic / peak, VALU and SALU issue fractions (issue); "
+                                                "HBM traffic / peak, VALU and SALU issue fractions and the "
+                                                "LDS-array busy fraction (issue); "
                                                 "achieved / peak / frac stay the algorithmic-bytes HBM figures")
                     elif tr:
                         out["roofline"]["traffic_error"] = tr["error"]

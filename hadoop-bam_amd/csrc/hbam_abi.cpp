@@ -124,6 +124,7 @@ int decode_device(BamFile& f, uint64_t vstart, uint64_t vend, int32_t flags, hba
   (void)hipEventCreate(&e1);
   (void)hipEventRecord(e0, p.stream());
   const uint64_t lf0 = p.link_fallbacks(), il0 = p.inflate_launches(), lr0 = p.link_rewalks();
+  const uint64_t rf0 = p.record_fallbacks();
   f.invalidate_window();  // a timed pass locates and inflates afresh
   Carry c{vstart >> 16, vstart & 0xffff};
   bool cont = false;
@@ -200,6 +201,7 @@ int decode_device(BamFile& f, uint64_t vstart, uint64_t vend, int32_t flags, hba
   st->link_fallbacks = (int32_t)(p.link_fallbacks() - lf0);
   st->inflate_launches = (int32_t)(p.inflate_launches() - il0);
   st->link_rewalks = (int32_t)(p.link_rewalks() - lr0);
+  st->record_fallbacks = (int32_t)(p.record_fallbacks() - rf0);
   if (rc != HBAM_OK) st->status = rc;
   return rc != HBAM_OK ? rc : st->status;
 }
@@ -409,6 +411,17 @@ int hbam_reader_position(hbam_ctx* ctx, uint64_t i, uint64_t* pos) {
   return ctx->cursor.reader_position(i, pos, &ctx->err);
 }
 
+int hbam_pipeline_counters(hbam_ctx* ctx, uint64_t out[5]) {
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  hbam::Pipeline& p = ctx->f->pipe();
+  out[0] = p.link_fallbacks();
+  out[1] = p.link_rewalks();
+  out[2] = p.record_fallbacks();
+  out[3] = p.inflate_launches();
+  out[4] = p.records_after_stop();
+  return HBAM_OK;
+}
+
 int hbam_decode_span_device(hbam_ctx* ctx, uint64_t vstart, uint64_t vend, int32_t flags, hbam_gpu_stats* st) {
   if (!ctx || !ctx->f) return HBAM_E_STATE;
   ctx->cursor.reset();
@@ -598,10 +611,15 @@ int hbam_splitting_index_for_records(const hbam_opts* opts, const uint64_t* voff
 }
 
 int hbam_guess_record_starts(hbam_ctx* ctx, const uint64_t* begs, const uint64_t* ends, uint64_t n, uint64_t* out) {
+  return hbam_guess_record_starts_hdr(ctx, -1, begs, ends, n, out);
+}
+
+int hbam_guess_record_starts_hdr(hbam_ctx* ctx, int32_t header_n_ref, const uint64_t* begs, const uint64_t* ends,
+                                 uint64_t n, uint64_t* out) {
   if (!ctx || !ctx->f) return HBAM_E_STATE;
   ctx->cursor.reset();
   std::vector<uint64_t> b(begs, begs + n), e(ends, ends + n), r;
-  hadoop_bam::BAMSplitGuesser g(*ctx->f);
+  hadoop_bam::BAMSplitGuesser g(*ctx->f, header_n_ref);
   int rc = g.guessNextBAMRecordStarts(b, e, &r);
   if (rc != HBAM_OK) {
     ctx->err = ctx->f->error();

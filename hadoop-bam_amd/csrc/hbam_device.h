@@ -27,6 +27,10 @@ enum : int {
   kErrDevice = 5,
   kErrState = 6,
   kErrNoMem = 7,
+  // (device-side per-block status, never returned) the block's records end
+  // the iteration without an error: EOF at an empty block after an exhausted
+  // one, or the end of the stream (k_rec_count)
+  kStopClean = -1,
 };
 
 struct BlockInfo {

@@ -520,7 +520,7 @@ int prepare_window(BamFile& f, uint64_t lo, uint64_t hi, hbam::DevBuf<uint8_t>* 
 // points [a, b) through kernel K; results into out by slot
 template <typename Launch>
 int run_points(BamFile& f, const std::vector<GuessPoint>& pts, size_t a, size_t b, const hbam::DevBuf<uint8_t>& dvalid,
-               std::vector<uint64_t>* out, std::string* err, Launch&& launch) {
+               std::vector<uint64_t>* out, std::string* err, int32_t n_ref, Launch&& launch) {
   using namespace hbam;
   Pipeline& p = f.pipe();
   const uint32_t m = (uint32_t)(b - a);
@@ -548,7 +548,7 @@ int run_points(BamFile& f, const std::vector<GuessPoint>& pts, size_t a, size_t 
   E.nblk = (uint32_t)p.blocks().size();
   E.u = p.d_u();
   E.valid = dvalid.p;
-  E.n_ref = f.n_ref();
+  E.n_ref = n_ref;
   launch(E, dbeg.p, dend.p, m, dout.p, dst.p, s);
   if (!chk(hipGetLastError())) return kErrDevice;
   if (!chk(hipMemcpyAsync(res.data(), dout.p, m * 8, hipMemcpyDeviceToHost, s)) || !chk(hipStreamSynchronize(s)))
@@ -559,7 +559,7 @@ int run_points(BamFile& f, const std::vector<GuessPoint>& pts, size_t a, size_t 
 }  // namespace
 
 int guess_batch(BamFile& f, const std::vector<uint64_t>& begs, const std::vector<uint64_t>& ends,
-                std::vector<uint64_t>* out, std::string* err) {
+                std::vector<uint64_t>* out, std::string* err, int32_t n_ref) {
   using namespace hbam;
   const size_t n = begs.size();
   out->assign(n, 0);
@@ -584,7 +584,7 @@ int guess_batch(BamFile& f, const std::vector<uint64_t>& begs, const std::vector
   return for_each_window(f, pts, [&](uint64_t lo, uint64_t hi, size_t a, size_t b) {
     int rc = prepare_window(f, lo, hi, &dvalid, err);
     if (rc != kOk) return rc;
-    return run_points(f, pts, a, b, dvalid, out, err,
+    return run_points(f, pts, a, b, dvalid, out, err, n_ref < 0 ? f.n_ref() : n_ref,
                       [](const GuessEnv& E, const uint64_t* db, const uint64_t* de, uint32_t m, uint64_t* dout,
                          int32_t* dst, hipStream_t s) {
                         hipLaunchKernelGGL(k_guess_splits, dim3((m + 63) / 64), dim3(64), 0, s, E, db, de, m, dout,
@@ -616,7 +616,7 @@ int guess_bgzf_batch(BamFile& f, const std::vector<uint64_t>& begs, const std::v
   return for_each_window(f, pts, [&](uint64_t lo, uint64_t hi, size_t a, size_t b) {
     int rc = prepare_window(f, lo, hi, &dvalid, err);
     if (rc != kOk) return rc;
-    return run_points(f, pts, a, b, dvalid, out, err,
+    return run_points(f, pts, a, b, dvalid, out, err, f.n_ref(),
                       [](const GuessEnv& E, const uint64_t* db, const uint64_t* de, uint32_t m, uint64_t* dout,
                          int32_t*, hipStream_t s) {
                         hipLaunchKernelGGL(k_guess_bgzf_starts, dim3((m + 63) / 64), dim3(64), 0, s, E, db, de, m,

@@ -691,11 +691,11 @@ void SplittingBAMIndexer::finish(uint64_t inputSize) { writeVirtualOffset(inputS
 // BAMSplitGuesser (GPU batch; see hbam_guess.hip)
 // ---------------------------------------------------------------------------
 int guess_batch(BamFile& f, const std::vector<uint64_t>& begs, const std::vector<uint64_t>& ends,
-                std::vector<uint64_t>* out, std::string* err);
+                std::vector<uint64_t>* out, std::string* err, int32_t n_ref);
 
 int BAMSplitGuesser::guessNextBAMRecordStarts(const std::vector<uint64_t>& begs, const std::vector<uint64_t>& ends,
                                               std::vector<uint64_t>* out) {
-  return guess_batch(f_, begs, ends, out, &f_.error());
+  return guess_batch(f_, begs, ends, out, &f_.error(), n_ref_);
 }
 
 // ---------------------------------------------------------------------------

@@ -253,6 +253,10 @@ class SplittingBAMIndexer {
 class BAMSplitGuesser {
  public:
   explicit BAMSplitGuesser(BamFile& f) : f_(f) {}
+  // BAMSplitGuesser(SeekableStream, InputStream headerStream, Configuration)
+  // (BAMSplitGuesser.java:93-103): the reference count of a header read from
+  // another stream than the data's (< 0: the data file's own header)
+  BAMSplitGuesser(BamFile& f, int32_t header_n_ref) : f_(f), n_ref_(header_n_ref) {}
   // guessNextBAMRecordStart(beg, end) for many split points; returns end when
   // nothing is found, as the reference does.
   int guessNextBAMRecordStarts(const std::vector<uint64_t>& begs, const std::vector<uint64_t>& ends,
@@ -260,6 +264,7 @@ class BAMSplitGuesser {
 
  private:
   BamFile& f_;
+  int32_t n_ref_ = -1;
 };
 
 // util/BGZFSplitGuesser.guessNextBGZFBlockStart(beg, end) (:64-112) for many

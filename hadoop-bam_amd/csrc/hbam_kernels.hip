@@ -94,7 +94,9 @@ __global__ __launch_bounds__(256) void k_bgzf_scan(const uint8_t* __restrict__ b
   // 0x1f bytes get the full header test.  Candidates are reported in file
   // coordinates (base + offset).
   // Four such wave steps per iteration (4 KiB per wave), their loads issued
-  // together: one load in flight per wave left the scan latency-bound.
+  // together: one load in flight per wave left the scan latency-bound.  The
+  // last lane's 4 bytes past the iteration's last chunk are loaded with them
+  // (loaded at their use, they cost a second memory latency per iteration).
 #ifndef HBAM_SCAN_U
 #define HBAM_SCAN_U 4
 #endif
@@ -110,6 +112,8 @@ __global__ __launch_bounds__(256) void k_bgzf_scan(const uint8_t* __restrict__ b
       const uint64_t c = c0 + 64 * u + lane;
       vv[u] = c < nc ? reinterpret_cast<const uint4*>(buf)[c] : make_uint4(0, 0, 0, 0);
     }
+    const uint64_t clast = c0 + 64 * (kU - 1) + 63;  // (buf is zero padded past len)
+    const uint32_t tail = lane == 63 && clast < nc ? *reinterpret_cast<const uint32_t*>(buf + 16 * clast + 16) : 0u;
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
     const uint64_t c = c0 + 64 * u + lane;  // the wave stays converged through the shuffle
@@ -117,7 +121,7 @@ __global__ __launch_bounds__(256) void k_bgzf_scan(const uint8_t* __restrict__ b
     uint32_t nx = (uint32_t)__shfl_down((int)v.x, 1, 64);
     // the wave's last lane: the next step's first chunk (lane 0), or memory
     const uint32_t next0 = u + 1 < kU ? (uint32_t)__shfl((int)vv[u + 1 < kU ? u + 1 : u].x, 0, 64) : 0u;
-    if (lane == 63) nx = u + 1 < kU ? next0 : (c < nc ? *reinterpret_cast<const uint32_t*>(buf + 16 * c + 16) : 0u);
+    if (lane == 63) nx = u + 1 < kU ? next0 : tail;
     const uint32_t w[5] = {v.x, v.y, v.z, v.w, nx};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -272,17 +276,6 @@ constexpr int kHuffWaves = kHuffThreads / 64;
 #define HBAM_HUFF_STAGE_MAX (40 * 1024)
 #endif
 constexpr uint32_t kHuffStageMaxLds = HBAM_HUFF_STAGE_MAX;
-// 16 B loads in flight per thread while a phase-A workgroup stages its block
-// and table image through registers (HBAM_STAGE_GLDS=0; 4, 6, 8 and 10 measured
-// the same)
-#ifndef HBAM_STAGE_BATCH
-#define HBAM_STAGE_BATCH 4
-#endif
-// 1: stage with global_load_lds_dwordx4, no register round trip (phase A
-// 8.52 -> 8.00 ms per C2 pass)
-#ifndef HBAM_STAGE_GLDS
-#define HBAM_STAGE_GLDS 1
-#endif
 
 // Wave-local ordering of LDS traffic (code run by one wave only).
 __device__ __forceinline__ void wave_sync() {
@@ -509,16 +502,6 @@ __device__ __attribute__((noinline)) int build_table_r(HuffLds& L, const uint8_t
                                                      uint32_t* tab, uint32_t* cnt, uint16_t* sorted, uint32_t* sub,
                                                      int subcap) {
   const uint32_t lane = lane_id();
-#ifdef HBAM_TAB_PROBE
-  const uint64_t bt0 = clock64();
-  uint64_t bt1 = 0, bt2 = 0, bt3 = 0;
-#define BT_REPORT(tag) do { if (mode == 0 && lane == 0 && (blockIdx.x & 4095) == 17) \
-    printf("btprobe %s count %llu place %llu long %llu total %llu\n", tag, (unsigned long long)(bt1 - bt0), \
-           (unsigned long long)(bt2 ? bt2 - bt1 : 0), (unsigned long long)(bt3 ? bt3 - bt2 : 0), \
-           (unsigned long long)(clock64() - bt0)); } while (0)
-#else
-#define BT_REPORT(tag) do { } while (0)
-#endif
   // Every symbol's code length stays in registers (nsym <= 320: 5 groups of
   // 64), so do the canonical offsets and first codes (wave-uniform, picked
   // per lane by a select chain): each LDS read on this path is a dependent
@@ -568,9 +551,6 @@ __device__ __attribute__((noinline)) int build_table_r(HuffLds& L, const uint8_t
   else if (left > 0 && (mode == 2 || maxl != 1)) st = 1;
   for (int i = lane; i < (1 << root); i += 64) tab[i] = kBadEntry;
   wave_sync();
-#ifdef HBAM_TAB_PROBE
-  bt1 = clock64();
-#endif
   if (st == 1) return 1;
   if (st == 2) return 0;  // no codes: all-invalid table
   const uint32_t rmask = (1u << root) - 1;
@@ -623,11 +603,7 @@ __device__ __attribute__((noinline)) int build_table_r(HuffLds& L, const uint8_t
     }
   }
   wave_sync();
-#ifdef HBAM_TAB_PROBE
-  bt2 = clock64();
-#endif
   if (__ballot(any_long) == 0) {
-    BT_REPORT("short");
     return 0;
   }
   // sub-table bases: exclusive sum of the sub-table sizes in root-index
@@ -653,9 +629,6 @@ __device__ __attribute__((noinline)) int build_table_r(HuffLds& L, const uint8_t
       used += sz;
     }
   }
-#ifdef HBAM_TAB_PROBE
-  bt3 = clock64();
-#endif
   const uint32_t nused = min(used, (uint32_t)subcap);
   for (uint32_t i = lane; i < nused; i += 64) sub[i] = kBadEntry;
   wave_sync();
@@ -675,9 +648,7 @@ __device__ __attribute__((noinline)) int build_table_r(HuffLds& L, const uint8_t
     }
   }
   wave_sync();
-  BT_REPORT("long");
   return 0;
-#undef BT_REPORT
 }
 
 // Fold two consecutive literals into one litlen entry when both codes fit in
@@ -1283,13 +1254,8 @@ __device__ __forceinline__ int build_tab(A&&... a) {
 
 template <bool REG>
 __device__ int dyn_header_par(HuffLds& L, ClLds& C, const uint32_t* __restrict__ W, uint32_t p, uint32_t E,
-                              uint32_t* end_pos, uint64_t* probe = nullptr) {
+                              uint32_t* end_pos) {
   const uint32_t lane = lane_id();
-#ifdef HBAM_TAB_PROBE
-#define DH_PROBE(k) do { if (probe) probe[k] = clock64(); } while (0)
-#else
-#define DH_PROBE(k) do { (void)probe; } while (0)
-#endif
   if (p + 14 > E) return DH_TRUNC;
   const uint32_t h = rfl(peek32(W, p));
   const uint32_t hlit = (h & 31) + 257, hdist = ((h >> 5) & 31) + 1, hclen = ((h >> 10) & 15) + 4;
@@ -1302,7 +1268,6 @@ __device__ int dyn_header_par(HuffLds& L, ClLds& C, const uint32_t* __restrict__
   wave_sync();
   p += 3 * hclen;
   if (rfl(build_tab<REG>(L, L.cl_lens, 19, 7, 2, L.dist, L.cnt_dist, L.sort_dist, nullptr, 0))) return DH_TRUNC;
-  DH_PROBE(0);
   const uint32_t ntot = hlit + hdist;
   uint32_t done = 0, prevv = 0, have_prev = 0;
   for (;;) {  // windows of 64 * kClSlice bits
@@ -1402,20 +1367,15 @@ __device__ int dyn_header_par(HuffLds& L, ClLds& C, const uint32_t* __restrict__
     p = rfl((uint32_t)__shfl(x, 63, 64));
   }
   wave_sync();
-  DH_PROBE(1);
   if (rfl(L.lens[256]) == 0) return DH_TRUNC;
   if (rfl(build_tab<REG>(L, L.lens, (int)hlit, kLitRoot, 0, L.lit, L.cnt_lit, L.sort_lit, L.litsub, kLitSubCap)))
     return DH_TRUNC;
-  DH_PROBE(2);
   if (rfl(build_tab<REG>(L, L.lens + hlit, (int)hdist, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist, L.distsub,
                       kDistSubCap)))
     return DH_TRUNC;
-  DH_PROBE(3);
   pair_literals(L);
-  DH_PROBE(4);
   return DH_OK;
 }
-#undef DH_PROBE
 
 // First DEFLATE block of every BGZF block: header + tables built ahead of the
 // decode kernel, one wave per block at high occupancy, so the serial header
@@ -1437,10 +1397,6 @@ __global__ __launch_bounds__(64) void k_huff_tables(const uint8_t* __restrict__ 
   ClLds& C = *reinterpret_cast<ClLds*>(L.lit);  // code-length symbols: done before lit[] is built
   const uint32_t lane = lane_id();
   const uint32_t bi = b0 + blockIdx.x;
-#ifdef HBAM_TAB_PROBE
-  uint64_t tp[5] = {(uint64_t)clock64(), 0, 0, 0, 0};
-  uint64_t dp[5] = {0, 0, 0, 0, 0};
-#endif
   const BlockInfo blk = blocks[bi];
   HuffTableInfo ti{1u, 0u, 0u, 0u};
   const uint64_t sbyte = blk.coff + 18;
@@ -1461,9 +1417,6 @@ __global__ __launch_bounds__(64) void k_huff_tables(const uint8_t* __restrict__ 
     const uint4* __restrict__ src = reinterpret_cast<const uint4*>(file + abase + sb);
     for (uint32_t i = lane; i <= nreal; i += 64) s_in[i] = src[i];  // +1 pad chunk (file is padded)
     wave_sync();
-#ifdef HBAM_TAB_PROBE
-    tp[1] = clock64();
-#endif
     SReader R;
     R.W = reinterpret_cast<const uint32_t*>(s_in);
     const uint32_t Ereal = 8u * ((uint32_t)(sbyte - abase) + (blk.csize - 26)) - 8u * sb;
@@ -1475,35 +1428,14 @@ __global__ __launch_bounds__(64) void k_huff_tables(const uint8_t* __restrict__ 
       R.consume(3);
       uint32_t b0pos = 0;
       const uint32_t hp = R.pos();
-#ifdef HBAM_TAB_PROBE
-      if (dyn_header_par<true>(L, C, R.W, hp, E, &b0pos, dp) == DH_OK) {
-#else
       if (dyn_header_par<true>(L, C, R.W, hp, E, &b0pos) == DH_OK) {
-#endif
         wave_sync();
-#ifdef HBAM_TAB_PROBE
-        tp[2] = clock64();
-#endif
         const uint32_t h = rfl(peek32(R.W, hp));
         const uint32_t est = block_bits_estimate(L.lens, (h & 31) + 257, ((h >> 5) & 31) + 1);
-#ifdef HBAM_TAB_PROBE
-        tp[3] = clock64();
-#endif
         uint4* __restrict__ dst = reinterpret_cast<uint4*>(tables + (uint64_t)blockIdx.x * kTableImage);
         const uint4* img = reinterpret_cast<const uint4*>(&L);
         for (uint32_t i = lane; i < kTableImage / 16; i += 64) dst[i] = img[i];
         ti = HuffTableInfo{0u, b0pos + 8u * sb, fin, est};
-#ifdef HBAM_TAB_PROBE
-        tp[4] = clock64();
-        if (lane == 0 && (blockIdx.x & 4095) == 17)
-          printf("tabprobe r%u b%u stage %llu cltab %llu lens %llu littab %llu disttab %llu pairs %llu est %llu "
-                 "copy %llu total %llu\n", round, blockIdx.x,
-                 (unsigned long long)(tp[1] - tp[0]), (unsigned long long)(dp[0] - tp[1]),
-                 (unsigned long long)(dp[1] - dp[0]), (unsigned long long)(dp[2] - dp[1]),
-                 (unsigned long long)(dp[3] - dp[2]), (unsigned long long)(dp[4] - dp[3]),
-                 (unsigned long long)(tp[3] - tp[2]), (unsigned long long)(tp[4] - tp[3]),
-                 (unsigned long long)(tp[4] - tp[0]));
-#endif
       }
     }
   }
@@ -1548,13 +1480,6 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
   const uint32_t bi = b0 + blockIdx.x;
   const BlockInfo blk = blocks[bi];
   const uint32_t isize = blk.isize;
-#ifdef HBAM_HUFF_PROBE
-  // clock probes (developer builds): cycles per stage of this workgroup-round
-  uint64_t pt = clock64(), pstage = 0, pctl = 0, pspec = 0, psync = 0, pscan = 0, pemit = 0, npass = 0;
-#define HP_MARK(acc) do { const uint64_t t_ = clock64(); acc += t_ - pt; pt = t_; } while (0)
-#else
-#define HP_MARK(acc) do { } while (0)
-#endif
   if (isize == 0) {  // inflate(buf,off,0) returns 0 without reading: nothing to validate
     if (tid == 0 && round == 0) { hout[bi].ntok = 0; hout[bi].status = kOk; }
     return;
@@ -1583,10 +1508,11 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
     const uint4* __restrict__ tsrc = reinterpret_cast<const uint4*>(tables + (uint64_t)blockIdx.x * kTableImage);
     uint4* sdst = s_in + q0;
     uint4* tdst = reinterpret_cast<uint4*>(&L);
-#if HBAM_STAGE_GLDS
     // global -> LDS without registers (global_load_lds_dwordx4): each wave
     // instruction moves 64 consecutive 16 B units to LDS base + lane x 16, all
-    // of a workgroup's copies in flight at once (__syncthreads drains them)
+    // of a workgroup's copies in flight at once (__syncthreads drains them;
+    // phase A 8.52 -> 8.00 ms per C2 pass against register staging with 4-10
+    // loads in flight per thread)
     typedef __attribute__((address_space(3))) void* lds_vp;
     typedef __attribute__((address_space(1))) void* gbl_vp;
     const uint32_t wv = tid >> 6, ln = tid & 63;
@@ -1594,27 +1520,8 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
       if (u0 + ln < nq) __builtin_amdgcn_global_load_lds((gbl_vp)(src + u0 + ln), (lds_vp)(sdst + u0), 16, 0, 0);
     for (uint32_t u0 = 64 * wv; u0 < nt; u0 += kHuffThreads)
       if (u0 + ln < nt) __builtin_amdgcn_global_load_lds((gbl_vp)(tsrc + u0 + ln), (lds_vp)(tdst + u0), 16, 0, 0);
-#else
-    constexpr int kStageBatch = HBAM_STAGE_BATCH;
-    for (uint32_t i0 = tid; i0 < nq + nt; i0 += kStageBatch * kHuffThreads) {
-      uint4 v[kStageBatch];
-#pragma unroll
-      for (int k = 0; k < kStageBatch; ++k) {
-        const uint32_t i = i0 + k * kHuffThreads;
-        if (i < nq) v[k] = src[i];
-        else if (i < nq + nt) v[k] = tsrc[i - nq];
-      }
-#pragma unroll
-      for (int k = 0; k < kStageBatch; ++k) {
-        const uint32_t i = i0 + k * kHuffThreads;
-        if (i < nq) sdst[i] = v[k];
-        else if (i < nq + nt) tdst[i - nq] = v[k];
-      }
-    }
-#endif
   }
   __syncthreads();
-  HP_MARK(pstage);
   // compressed bits: the LDS copy, or (unstaged) the file in HBM
   const uint32_t* __restrict__ W =
       STAGE ? reinterpret_cast<const uint32_t*>(s_in) : reinterpret_cast<const uint32_t*>(file + abase);
@@ -1827,7 +1734,6 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
       if (lane == 0) C.act = act;
     }
     __syncthreads();
-    HP_MARK(pctl);
     if (C.act != kActDecode) break;
 
     // ---- all-lane decode of this DEFLATE block's symbols
@@ -1840,19 +1746,12 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
     uint32_t mj = 0, x, nt, nb;
     uint32_t ev = lane_decode<LD_SPEC>(L, W, a, stop, E, x, nt, nb, mp, mj, nullptr, 0, 0);
     const uint32_t sx = x, snt = nt, snb = nb, sev = ev;
-#ifdef HBAM_HUFF_PROBE
-    bool first_sync = true;
-#endif
     for (;;) {  // sync: restart each slice from its predecessor's exit
       if (lane == 63) {
         C.xx[wave] = x;
         C.xe[wave] = ev;
       }
       __syncthreads();
-#ifdef HBAM_HUFF_PROBE
-      if (first_sync) HP_MARK(pspec);
-      first_sync = false;
-#endif
       uint32_t px = __shfl_up(x, 1, 64), pev = __shfl_up(ev, 1, 64);
       if (lane == 0 && wave > 0) {
         px = C.xx[wave - 1];
@@ -1878,21 +1777,15 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
         }
       }
     }
-    HP_MARK(psync);
     const uint32_t lend0 = wg_min(ev != EV_STOP ? tid : 0xffffffffu, C.red);
     const uint32_t lend = lend0 == 0xffffffffu ? (uint32_t)kHuffThreads - 1 : lend0;
     const bool valid = tid <= lend;
     uint32_t toff, boff;
     wg_excl_scan2(valid ? nt : 0u, valid ? nb : 0u, C.red, toff, boff);
-    HP_MARK(pscan);
     uint32_t x3 = a, nt3 = 0, nb3 = 0, ev3 = EV_STOP;
     if (valid)
       ev3 = lane_decode<LD_EMIT>(L, W, a, stop, E, x3, nt3, nb3, mp, mj, tok_out + tok0 + toff, out0 + boff, isize);
     const uint32_t m3 = wg_min((valid && ev3 != EV_STOP) ? tid : 0xffffffffu, C.red);
-    HP_MARK(pemit);
-#ifdef HBAM_HUFF_PROBE
-    ++npass;
-#endif
     const uint32_t f = m3 != 0xffffffffu ? m3 : lend;
     if (tid == f) {
       C.fe = ev3;
@@ -1903,14 +1796,6 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
     }
     __syncthreads();
   }
-#ifdef HBAM_HUFF_PROBE
-  if (tid == 0 && (blockIdx.x & 4095) == 17)
-    printf("huffprobe r%u b%u stage %u passes %u stage_cyc %llu ctl %llu spec %llu sync %llu scan %llu emit %llu\n",
-           round, blockIdx.x, (unsigned)STAGE, (unsigned)npass, (unsigned long long)pstage, (unsigned long long)pctl,
-           (unsigned long long)pspec, (unsigned long long)psync, (unsigned long long)pscan,
-           (unsigned long long)pemit);
-#endif
-#undef HP_MARK
   if (tid == 0) {
     if (wave == 0 && pending && err == kOk) {
       hout[bi] = HuffOut{ntok, kHuffPending, resume_bit, outpos};
@@ -1930,7 +1815,7 @@ __global__ __launch_bounds__(kHuffThreads, kHuffWavesPerSimd) void k_inflate_huf
     const uint8_t* __restrict__ file, const BlockInfo* __restrict__ blocks, uint32_t b0, uint64_t chunk_ustart,
     uint32_t* __restrict__ tokens, HuffOut* __restrict__ hout, const uint8_t* __restrict__ tables,
     const HuffTableInfo* __restrict__ tinfo, uint32_t round, uint32_t defer) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kHuffStageMaxLds];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kHuffStageCap + kHuffStaticBytes];
   const BlockInfo& b = blocks[b0 + blockIdx.x];
   const uint64_t abase = (b.coff + 18) & ~15ull;
   const uint32_t need = (uint32_t)(((b.coff + b.csize - abase + 15) >> 4) + 1) * 16u;  // huff_stage_bytes
@@ -1959,14 +1844,6 @@ constexpr uint32_t kMapMax = 65280;
 constexpr uint32_t kLitTag = 0xFF00u;
 constexpr int kLzRing = 4;  // phase-B fill: 64-token groups loaded ahead (4 vs 8 measured equal)
 constexpr int kLzTokGroups = 32;  // token groups a wave keeps in registers (32 K tokens per block)
-#ifndef HBAM_LZ_JUMP
-#define HBAM_LZ_JUMP 1
-#endif
-// 1: every lane stores at every chase step, branch-free (0: only the lanes
-// still chasing, exec-masked: 5.70 vs 5.43 ms per C2 pass)
-#ifndef HBAM_LZ_JUMP_ALL
-#define HBAM_LZ_JUMP_ALL 1
-#endif
 #ifndef HBAM_LZ_CHASE
 #define HBAM_LZ_CHASE 2
 #endif
@@ -2050,12 +1927,6 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
   const BlockInfo blk = blocks[b0 + blockIdx.x];
   const HuffOut ho = hout[b0 + blockIdx.x];
   if (ho.status != kOk || blk.isize == 0) return;
-#ifdef HBAM_LZ_PROBE
-  uint64_t lzt[6] = {(uint64_t)clock64(), 0, 0, 0, 0, 0};
-#define LZP(k) do { lzt[k] = clock64(); } while (0)
-#else
-#define LZP(k) do { } while (0)
-#endif
   const uint32_t isize = blk.isize;
   const uint32_t o0 = (uint32_t)(blk.ustart & 15);
   const uint32_t* tk = tokens + (blk.ustart - chunk_ustart);
@@ -2117,7 +1988,6 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
   for (int d = 32; d > 0; d >>= 1) wsum += __shfl_xor(wsum, d, 64);
   if (lane == 0) scratch[wid] = wsum;
   __syncthreads();
-  LZP(1);
   uint32_t P = 0;
 #pragma unroll
   for (int w = 0; w < kLzWaves; ++w) P += (uint32_t)w < wid ? scratch[w] : 0u;
@@ -2162,7 +2032,6 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
     }
   }
   __syncthreads();
-  LZP(2);
 
   // 3. match bodies: every 0 entry belongs to the match whose distance is the
   //    nearest non-zero entry before it that is not a literal, so a
@@ -2226,7 +2095,6 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
     }
   }
   __syncthreads();
-  LZP(3);
 
   // 4. resolve, increasing positions first; results written back in place
   //    (path compression).  Each chase step is one dependent LDS load, so a
@@ -2256,26 +2124,19 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
       }
 #pragma unroll
       for (int k = 0; k < kLzChase; ++k) v[k] = un[k] ? n[k] : v[k];
-#if HBAM_LZ_JUMP
       // pointer jumping: every step stores how far the chase got, so a lane
       // whose chain runs through this position skips the hops already made
       // (a run of dist-1 matches resolves in ~log2(len) steps instead of
       // len).  Any stored value is a position holding the same byte, or the
       // byte itself, so racing stores keep every entry valid.  The last step
       // of a chase stores its byte, so nothing is written after the loop.
+      // Every lane stores, branch-free (exec-masked stores of only the lanes
+      // still chasing: 5.70 vs 5.43 ms per C2 pass).
 #pragma unroll
-      for (int k = 0; k < kLzChase; ++k)
-        if (HBAM_LZ_JUMP_ALL || un[k]) m[at[k]] = (uint16_t)v[k];
-#endif
+      for (int k = 0; k < kLzChase; ++k) m[at[k]] = (uint16_t)v[k];
     }
-#if !HBAM_LZ_JUMP
-#pragma unroll
-    for (int k = 0; k < kLzChase; ++k)
-      if (q + k * kLzThreads < isize) m[q + k * kLzThreads] = (uint16_t)v[k];
-#endif
   }
   __syncthreads();
-  LZP(4);
 
   // 5. 16 B stores; low bytes of 16 entries packed with v_perm
   for (uint32_t s = tid; s < nseg; s += kLzThreads) {
@@ -2296,16 +2157,6 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
       }
     }
   }
-#ifdef HBAM_LZ_PROBE
-  __syncthreads();
-  LZP(5);
-  if (tid == 0 && (blockIdx.x & 4095) == 17)
-    printf("lzprobe b%u ntok %u tokens %llu heads %llu bodies %llu resolve %llu store %llu total %llu\n", blockIdx.x,
-           ntok, (unsigned long long)(lzt[1] - lzt[0]), (unsigned long long)(lzt[2] - lzt[1]),
-           (unsigned long long)(lzt[3] - lzt[2]), (unsigned long long)(lzt[4] - lzt[3]),
-           (unsigned long long)(lzt[5] - lzt[4]), (unsigned long long)(lzt[5] - lzt[0]));
-#endif
-#undef LZP
 }
 
 // ---------------------------------------------------------------------------
@@ -2539,7 +2390,7 @@ __device__ bool record_invalid(const ChainEnv& E, uint64_t q, int32_t bs, bool s
 
 // record_invalid by a whole wave, for records with long cigars (ONT-like
 // reads carry thousands of operators; one lane walking them serially set the
-// pace of k_rec_check: 2.0 ms per C4 pass).  Same rules, same result: the
+// pace of the record check: 2.0 ms per C4 pass).  Same rules, same result: the
 // per-operator rules become a lane-per-operator pass over chunks of 64, the
 // running state becomes scans --
 //   qlen / rlen            wrapping u32 sums (as the serial u32 accumulators)
@@ -2895,11 +2746,14 @@ __global__ void k_rec_count(ChainEnv E, const uint64_t* __restrict__ entry, uint
     uint64_t q = e;
     bool first = (MODE == kReader) && (e == E.p0);  // reader: first record follows a seek
     while (q < lim) {
-      if (!first && is_dead(E, q)) break;  // readInt at an exhausted block + empty block: EOF
+      if (!first && is_dead(E, q)) {  // readInt at an exhausted block + empty block: EOF
+        st = kStopClean;
+        break;
+      }
       first = false;
       const uint64_t avail = E.e_true - q;
       if (avail < 4) {
-        if (MODE == kIndexer && avail > 0) st = kErrIO;  // "less than 4 bytes long"
+        st = MODE == kIndexer && avail > 0 ? kErrIO : kStopClean;  // "less than 4 bytes long" / EOF
         break;
       }
       if (q + 4 > E.e_inf) { atomicMax(need, (unsigned long long)(q + 4)); break; }
@@ -3135,11 +2989,11 @@ __global__ void k_rec_decode(const uint8_t* __restrict__ u, const uint64_t* __re
 //                  ~records-per-block steps instead of a wave per block.
 //   k_rec_linkfix  max-scan link check; blocks whose list is off the chain are
 //                  re-walked from their true entry (usually zero or a few).
-//   k_rec_check    one wave per block: the reader / indexer rules of
-//                  k_rec_count for every listed record at once; the first stop
-//                  gives count, status and the bytes still to inflate.
-//   k_rec_out      one wave per block: positions, voffs and (reader) the fused
-//                  decode + key at the block's scanned base.
+//   k_rec_check_out  one wave per block: the reader / indexer rules of
+//                  k_rec_count for every listed record at once (the first stop
+//                  gives count, status and the bytes still to inflate), then
+//                  positions, voffs and (reader) the fused decode + key at the
+//                  block's scanned base.
 // k_rec_cand: one wave per block, each lane testing kCandPos consecutive
 // positions per step (512 per step): refID and mate refID of its 8 positions
 // come from 5 aligned 8 B loads, and only the rare position that passes that
@@ -3515,148 +3369,22 @@ __device__ __forceinline__ void check_listed_h(const ChainEnv& E, uint64_t q, ui
     }
   }
 }
-template <int MODE>
-__device__ __forceinline__ void check_listed(const ChainEnv& E, uint64_t q, uint64_t lim, bool first, bool light,
-                                             bool* stop, bool* counted, int* s, uint64_t* nd, bool* long_cigar) {
-  check_listed_h<MODE>(E, q, lim, first, light, stop, counted, s, nd, long_cigar, load_head(E.u, q));
-}
-
-// One block's listed records checked by its wave: *count = the records before
-// the first stop (plus that record when it counts), *st = the stop's status,
-// *need = the largest position a stopped record needs past the inflated range
-// (0: none); returns whether records before the stop left long cigars to
-// record_invalid_wave.
-template <int MODE>
-__device__ __forceinline__ bool check_block(const ChainEnv& E, uint32_t i, uint64_t e, const uint32_t* __restrict__ wcnt,
-                                            const uint16_t* __restrict__ list, uint32_t* count, int* st,
-                                            uint64_t* need) {
-  const uint32_t lane = lane_id();
-  *count = 0;
-  *st = kOk;
-  *need = 0;
-  bool long_cigar = false;  // a record before the stop left to record_invalid_wave (lane-local)
-  if (e == kNone) return false;
-  const BlockInfo b = E.blocks[E.k0 + i];
-  const uint64_t lim = min(b.ustart + b.isize, E.q_end);
-  const uint32_t wc = wcnt[i];
-  const uint32_t n = min(wc & kListCountMask, kListCap);
-  // a plausible() list on fully inflated data already satisfies every rule
-  // that reads the record (block_size >= 32, refID / mate refID in range,
-  // record inside the stream): only span end and dead positions remain
-  const bool light = (wc & kListPlausible) && E.e_inf == E.e_true && (MODE != kReader || E.validate == 0);
-  const uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
-  *count = n;
-  for (uint32_t r0 = 0; r0 < n; r0 += 64) {
-    const uint32_t r = r0 + lane;
-    bool stop = false, counted = false;
-    int s = kOk;
-    uint64_t nd = 0;
-    if (r < n) {
-      const uint64_t q = b.ustart + L[r];
-      check_listed<MODE>(E, q, lim, r == 0 && q == E.p0, light, &stop, &counted, &s, &nd, &long_cigar);
-    }
-    const uint64_t m = __ballot(stop);
-    if (m) {
-      const uint32_t f = (uint32_t)__ffsll((long long)m) - 1;
-      *count = r0 + f + (uint32_t)__shfl((int)counted, (int)f, 64);
-      *st = __shfl(s, (int)f, 64);
-      *need = shfl_u64(nd, f);
-      break;
-    }
-  }
-  return __ballot(long_cigar) != 0;
-}
-
-// The k_rec_count rules, one lane per listed record.
-template <int MODE>
-__global__ __launch_bounds__(64) void k_rec_check(ChainEnv E, const uint64_t* __restrict__ entry,
-                                                  const uint32_t* __restrict__ wcnt,
-                                                  const uint16_t* __restrict__ list, uint32_t* __restrict__ cnt,
-                                                  int32_t* __restrict__ err, unsigned long long* __restrict__ need,
-                                                  uint8_t* __restrict__ has_long) {
-  const uint32_t i = blockIdx.x;
-  uint32_t count;
-  int st;
-  uint64_t nd;
-  const bool any_long = check_block<MODE>(E, i, entry[i], wcnt, list, &count, &st, &nd);
-  if (lane_id() == 0) {
-    if (nd) atomicMax(need, (unsigned long long)nd);
-    cnt[i] = count;
-    err[i] = st;
-    if (MODE == kReader) {
-      has_long[i] = any_long;
-      if (any_long) has_long[gridDim.x] = 1;  // tells the host to launch k_rec_check_long
-    }
-  }
-}
-
-// The records k_rec_check left unvalidated (cigars longer than kWaveCigarOps
-// operators), one wave per record in list order, up to the block's stop: the
-// first invalid one becomes the stop (SAMFormatException).  A separate kernel
-// keeps k_rec_check's registers those of the per-lane rules.
-__global__ __launch_bounds__(64) void k_rec_check_long(ChainEnv E, const uint16_t* __restrict__ list,
-                                                       const uint8_t* __restrict__ has_long,
-                                                       uint32_t* __restrict__ cnt, int32_t* __restrict__ err) {
-  const uint32_t i = blockIdx.x;
-  if (!has_long[i]) return;
-  const uint32_t lane = lane_id();
-  const BlockInfo b = E.blocks[E.k0 + i];
-  const uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
-  const uint32_t n = cnt[i];
-  for (uint32_t r0 = 0; r0 < n; r0 += 64) {
-    const uint32_t r = r0 + lane;
-    const uint64_t q = r < n ? b.ustart + L[r] : 0;
-    const bool lg = r < n && (ldu32(E.u, q + 16) & 0xffffu) > kWaveCigarOps;
-    for (uint64_t wm = __ballot(lg); wm; wm &= wm - 1) {
-      const uint32_t src = (uint32_t)__ffsll((long long)wm) - 1;
-      const uint64_t qq = shfl_u64(q, src);
-      if (record_invalid_wave(E, qq, (int32_t)ldu32(E.u, qq), E.validate == 2)) {
-        if (lane == 0) {
-          cnt[i] = r0 + src;
-          err[i] = kErrFormat;
-        }
-        return;
-      }
-    }
-  }
-}
-
-template <int MODE, bool DECODE>
-__global__ __launch_bounds__(64) void k_rec_out(ChainEnv E, const uint32_t* __restrict__ cnt,
-                                                const uint64_t* __restrict__ base, const uint16_t* __restrict__ list,
-                                                uint64_t* __restrict__ rec_pos, uint64_t* __restrict__ rec_voff,
-                                                Columns col) {
-  const uint32_t i = blockIdx.x;
-  const uint32_t n = cnt[i];
-  if (n == 0) return;
-  const BlockInfo b = E.blocks[E.k0 + i];
-  const uint64_t o0 = base[i];
-  const uint16_t* __restrict__ L = list + (uint64_t)i * kListCap;
-  for (uint32_t r = lane_id(); r < n; r += 64) {
-    const uint32_t off = L[r];
-    const uint64_t q = b.ustart + off, o = o0 + r;
-    rec_pos[o] = q;
-    rec_voff[o] = (b.coff << 16) | off;
-    if (DECODE) decode_record(E.u, q, o, col);
-  }
-}
-
 // Record check and output in one pass (the list path of decode_span_pos):
-// k_rec_check + k_rec_check_long + k_rec_out, one wave per block, so a
-// block's records are read from HBM once after inflate and written out while
-// they are in L2.  A block writes its records at base[i], the exclusive scan
-// of the lists' counts: the true offsets whenever every block before the
-// first one that stops early (a failure, the span end, the window end) keeps
-// its whole list -- the normal case, with no wait on other blocks.  The
-// launch reports what the host needs to check that:
+// the record rules, the long-cigar validation and the output, one wave per
+// block, so a block's records are read from HBM once after inflate and
+// written out while they are in L2.  A block writes its records at base[i],
+// the exclusive scan of the lists' counts: the true offsets for every block
+// up to the first one that stops early, since every block before it keeps
+// its whole list.  A stop ends the reader's iteration (a failure, EOF at an
+// empty block, the end of the stream or of the span) and the indexer's, so
+// the span's records are exactly those up to the first stop, and what later
+// blocks write lies past them.  The launch reports:
 //   bad[0]   min over blocks that stop early or fail of (i << 40 | base[i] +
 //            count): the first such block and the records up to its stop
-//   flags[0] the first failing block (k_first_error_i32), flags[1] the last
-//            block with records + 1
-// The offsets hold iff no block after the first early stop has records, or
-// that block failed (the records after it are dropped); otherwise the host
-// rescans the counts written to cnt[] and writes the outputs again
-// (k_rec_out).  cnt[] / err[] / need are k_rec_check's.
+//   flags[0] the first failing block (its status is the span's when it is
+//            the first stop), flags[1] the last block with records + 1
+//   cnt[] / err[] per block, need = the bytes a stopped record needs past
+//            the inflated range.
 constexpr int kBadShift = 40;
 
 template <int MODE, bool DECODE>
@@ -4211,18 +3939,6 @@ hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s) 
                            a.x, a.wcnt, a.list, a.counters + 2, validate);
       break;
     }
-    case kStageCheckLong:  // records with long cigars, a wave each (after kStageCheck flagged them)
-      hipLaunchKernelGGL(k_rec_check_long, dim3(nb), dim3(64), 0, s, E, a.list, a.has_long, a.cnt, a.err);
-      break;
-    case kStageCheck:  // per-record check
-      if (mode == kReader) {
-        hipLaunchKernelGGL(k_rec_check<kReader>, dim3(nb), dim3(64), 0, s, E, a.entry, a.wcnt, a.list, a.cnt, a.err,
-                           a.need, a.has_long);
-      } else {
-        hipLaunchKernelGGL(k_rec_check<kIndexer>, dim3(nb), dim3(64), 0, s, E, a.entry, a.wcnt, a.list, a.cnt,
-                           a.err, a.need, a.has_long);
-      }
-      break;
     default:
       return hipErrorInvalidValue;
   }
@@ -4278,35 +3994,6 @@ hipError_t launch_rec_check_out(const ChainArgs& a, int mode, bool decode, const
   else if (mode == kReader) HBAM_CO(kReader, false);
   else HBAM_CO(kIndexer, false);
 #undef HBAM_CO
-  return hipGetLastError();
-}
-
-hipError_t launch_rec_out(const ChainArgs& a, int mode, bool decode, const Columns& col, hipStream_t s) {
-  ChainEnv E;
-  E.u = a.u;
-  E.blocks = a.blocks;
-  E.e_inf = a.e_inf;
-  E.e_true = a.e_true;
-  E.p0 = a.p0;
-  E.q_end = a.q_end;
-  E.dead = a.dead;
-  E.ndead = a.ndead;
-  E.n_ref = a.n_ref;
-  E.k0 = a.k0;
-  E.k1 = a.k1;
-  E.validate = a.validate;
-  E.ref_len = a.ref_len;
-  const uint32_t nb = a.k1 - a.k0;
-  if (nb == 0) return hipSuccess;
-  if (mode == kReader && decode)
-    hipLaunchKernelGGL((k_rec_out<kReader, true>), dim3(nb), dim3(64), 0, s, E, a.cnt, a.base, a.list, a.rec_pos,
-                       a.rec_voff, col);
-  else if (mode == kReader)
-    hipLaunchKernelGGL((k_rec_out<kReader, false>), dim3(nb), dim3(64), 0, s, E, a.cnt, a.base, a.list, a.rec_pos,
-                       a.rec_voff, col);
-  else
-    hipLaunchKernelGGL((k_rec_out<kIndexer, false>), dim3(nb), dim3(64), 0, s, E, a.cnt, a.base, a.list, a.rec_pos,
-                       a.rec_voff, col);
   return hipGetLastError();
 }
 

@@ -33,7 +33,6 @@ struct ChainArgs {
   uint32_t* wcnt;       // records listed per block
   uint16_t* list;       // kListCap u16 offsets (from ustart) per block
   uint32_t* counters;   // [0] hard link violations, [1] blocks to re-walk, [2] list overflow
-  uint8_t* has_long;    // check stage: the block has records left to k_rec_check_long; [nb]: any block
   // fused check + output (launch_rec_check_out)
   uint64_t* fuse_bad;    // = ~0: min (i << kFusedBadShift | records up to i's stop) over blocks that stop early
   uint32_t* fuse_flags;  // [0] first failing block = ~0, [1] last block with records + 1 = 0
@@ -50,8 +49,6 @@ enum ChainStage : int {
   kStageLinkCheck = 6,   // max-scan link check with re-walk requests
   kStageRewalk = 7,      // re-walk the requested blocks (entries validated)
   kStageRewalkAll = 8,   // re-walk every block off the serial link's entry[]
-  kStageCheck = 9,       // per-record check of the lists -> cnt / err / need (has_long[nb]: long cigars left)
-  kStageCheckLong = 10,  // the long-cigar records kStageCheck left, a wave each
 };
 
 // candidates in [lo, hi); file + buf_base is the (aligned) device buffer start
@@ -92,13 +89,11 @@ inline uint32_t huff_stage_bytes(const BlockInfo& b) {
 hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb, uint64_t chunk_ustart,
                                const uint32_t* tokens, const HuffOut* hout, uint8_t* u, hipStream_t s);
 hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s);
-// positions, voffs and (decode) the SoA columns off the per-block lists, one wave per block
-hipError_t launch_rec_out(const ChainArgs& a, int mode, bool decode, const Columns& col, hipStream_t s);
 // a.cnt[i] = the records block i's list holds (0 off the chain): scanned into
 // a.base, the offsets launch_rec_check_out writes at
 hipError_t launch_list_counts(const ChainArgs& a, hipStream_t s);
-// kStageCheck + kStageCheckLong + launch_rec_out in one launch
-// (k_rec_check_out): cnt / err / need as the check, outputs at a.base[i] (the
+// the record rules, long-cigar validation and output of the listed records
+// (k_rec_check_out): cnt / err / need per block, outputs at a.base[i] (the
 // scanned list counts), a.fuse_bad / a.fuse_flags as documented there; cap =
 // the rec_pos / rec_voff / column capacity
 hipError_t launch_rec_check_out(const ChainArgs& a, int mode, bool decode, const Columns& col, uint64_t cap,

@@ -61,7 +61,7 @@ Pipeline::Pipeline(int device) : device_(device) {
   stage_.owner = &stage_owner_;
   own(own_file_, own_spare_, dblocks_, ref_len_, du_, tokens_[0], tokens_[1], hout_, tables_[0], tables_[1],
       tinfo_[0], tinfo_[1], g_, x_, x2_, entry_, base_arr_, summary_, dead_, cand_, sorted_, isz_, ust_, cnt_, flags_,
-      errv_, need_, rec_pos_, rec_voff_, rcand_, force_, wcnt_, counters_, list_, hlong_, scan_tmp_, cols_, long_rec_,
+      errv_, need_, rec_pos_, rec_voff_, rcand_, force_, wcnt_, counters_, list_, scan_tmp_, cols_, long_rec_,
       long_n_, wbuf_, woffs_, wbad_, scalars_, fuse_);
   for (auto& e : ev_) (void)hipEventCreate(&e);
   for (auto& e : sync_ev_) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
@@ -767,16 +767,6 @@ int Pipeline::decode_span(uint64_t vstart, uint64_t vend, ChainMode mode, bool d
   return decode_span_pos((uint64_t)sp, vend, mode, decode, out);
 }
 
-// HBAM_FUSED_RECORDS=0: the list path as separate launches (check, first
-// error, count scan, output), for A/B measurement
-static bool fused_record_pass() {
-  static const bool on = [] {
-    const char* e = getenv("HBAM_FUSED_RECORDS");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool decode, SpanDev* out) {
   HIPCHK(hipSetDevice(device_));
   *out = SpanDev();
@@ -835,7 +825,6 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
     HIPCHK(force_.reserve(nb));
     HIPCHK(wcnt_.reserve(nb));
     HIPCHK(list_.reserve((uint64_t)nb * kListCap));
-    HIPCHK(hlong_.reserve(nb + 1));
     HIPCHK(base_arr_.reserve(nb + 1));
     HIPCHK(counters_.reserve(4));
     size_t lsb = 0;
@@ -853,7 +842,6 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
     a.force = force_.p;
     a.wcnt = wcnt_.p;
     a.list = list_.p;
-    a.has_long = hlong_.p;
     a.counters = counters_.p;
     a.base = base_arr_.p;
     a.scan_tmp = scan_tmp_.p;
@@ -943,7 +931,11 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
     }
     bound = last_base + last_cnt;
     lists = ovf == 0;
-    fused = lists && fused_record_pass();
+    // a list overflowed (indexer mode: records shorter than 36 bytes): the
+    // per-block walks count and emit the records instead (k_rec_count,
+    // k_rec_emit)
+    fused = lists;
+    if (!lists) ++record_fallbacks_;
     if (fused) {
       // outputs sized by the lists' records, then check + positions + voffs +
       // fields + keys in one launch, each block at its scanned list offset
@@ -971,18 +963,19 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
       if (bad == ~0ull) {
         fused_total = bound;  // every block kept its whole list
       } else {
+        // the span ends at the first block that stops: its records stand at
+        // their final offsets, later blocks' records lie past them and are
+        // dropped, and that block's status (if any) is the span's -- a
+        // failure in a later block is never reached (k_rec_check_out)
         const uint64_t k = bad >> kFusedBadShift;
-        if (fl[1] <= k + 1 || fl[0] == k) fused_total = bad & ((1ull << kFusedBadShift) - 1);
-        else fused = false;  // records after an early stop: the counts are rescanned (k_rec_out)
+        fused_total = bad & ((1ull << kFusedBadShift) - 1);
+        if (fl[0] != k) fused_first = 0xffffffffu;
+        if (fl[1] > k + 1) ++records_after_stop_;
       }
     } else {
-      uint8_t long_left = 0;
-      HIPCHK(hipMemsetAsync(hlong_.p + nb, 0, 1, stream_));
-      HIPCHK(launch_chain(a, mode, lists ? kStageCheck : kStageCount, stream_));  // count + validate
+      HIPCHK(launch_chain(a, mode, kStageCount, stream_));  // count + validate by walking
       HIPCHK(rb(&need, need_.p, 8, stream_));
-      HIPCHK(rb(&long_left, hlong_.p + nb, 1, stream_));
       HIPCHK(rb_sync(stream_));
-      if (long_left) HIPCHK(launch_chain(a, mode, kStageCheckLong, stream_));  // long cigars, a wave each
     }
     const uint64_t final_pos = sm[0];
     const bool stopped = sm[1] != 0;
@@ -1011,11 +1004,15 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
     HIPCHK(rb(&first, flags_.p + 3, 4, stream_));
     HIPCHK(rb_sync(stream_));
   }
+  int32_t code = 0;
   if (first != none) {
-    int32_t code = 0;
     HIPCHK(rb(&code, errv_.p + first, 4, stream_));
     HIPCHK(rb_sync(stream_));
+    // (k_rec_count) the first block that stops, with or without an error:
+    // the iteration ends there
     if (!fused) HIPCHK(launch_truncate_counts(cnt_.p, nb, flags_.p + 3, stream_));
+  }
+  if (first != none && code != kStopClean) {
     out->status = code;
     const BlockInfo& b = hblocks_[k0 + first];
     const char* what = code == kErrFormat ? "Invalid record (SAMFormatException)"
@@ -1051,10 +1048,7 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
   out->rec_pos = rec_pos_.p;
   out->rec_voff = rec_voff_.p;
   if (dec) out->col = c;
-  if (!fused && lists) {  // positions + voffs (+ decode) off the per-block lists, after the count scan
-    if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
-    HIPCHK(launch_rec_out(a, mode, dec, c, stream_));
-  } else if (!fused) {  // a block listed more starts than kListCap: per-block walks
+  if (!fused) {  // a block listed more starts than kListCap: per-block walks
     HIPCHK(launch_chain(a, mode, kStageEmit, stream_));
     if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
     if (dec) HIPCHK(launch_rec_decode(du_.p, rec_pos_.p, total, c, stream_));

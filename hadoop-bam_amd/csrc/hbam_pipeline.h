@@ -250,6 +250,8 @@ class Pipeline {
 
   uint64_t link_fallbacks() const { return link_fallbacks_; }
   uint64_t link_rewalks() const { return link_rewalks_; }
+  uint64_t record_fallbacks() const { return record_fallbacks_; }
+  uint64_t records_after_stop() const { return records_after_stop_; }
   uint64_t inflate_launches() const { return inflate_launches_; }
   StageTimes times;
   bool timing = false;  // record per-stage HIP event times
@@ -307,6 +309,8 @@ class Pipeline {
   uint32_t n_ref_len_ = 0;
   uint64_t link_fallbacks_ = 0;
   uint64_t link_rewalks_ = 0;      // re-walk rounds of the parallel link
+  uint64_t record_fallbacks_ = 0;  // spans whose lists overflowed: records counted and emitted by walks
+  uint64_t records_after_stop_ = 0;  // spans that stopped early with records listed in later blocks (dropped)
   uint64_t inflate_launches_ = 0;  // phase A/B launch pairs so far
 
   DevBuf<uint8_t> du_;
@@ -331,7 +335,6 @@ class Pipeline {
   DevBuf<uint64_t> rcand_, force_;  // chain v2
   DevBuf<uint32_t> wcnt_, counters_;
   DevBuf<uint16_t> list_;
-  DevBuf<uint8_t> hlong_;  // check stage: blocks with records for k_rec_check_long
   DevBuf<uint32_t> fuse_;  // k_rec_check_out: [0..1] early-stop key (u64), [2] first failing block, [3] last block with records + 1
   DevBuf<uint8_t> scan_tmp_;
   DevBuf<uint8_t> cols_;  // SoA backing store

@@ -63,7 +63,7 @@ class GpuStats(C.Structure):
                 ("ms_lz77", C.c_float), ("ms_chain", C.c_float), ("ms_decode", C.c_float),
                 ("ms_total", C.c_float), ("status", i32), ("link_fallbacks", i32),
                 ("inflate_launches", i32), ("link_rewalks", i32), ("windows", i32), ("ms_tables", C.c_float),
-                ("reserved", i32), ("key_digest", u64), ("voff_digest", u64)]
+                ("record_fallbacks", i32), ("key_digest", u64), ("voff_digest", u64)]
 
 
 def _sig(name, res, args):
@@ -89,6 +89,7 @@ _sig("hbam_ref", C.c_int, [P, i32, C.POINTER(C.c_char_p), C.POINTER(i32)])
 _sig("hbam_decode_span", C.c_int, [P, u64, u64, u64, C.POINTER(Batch)])
 _sig("hbam_decode_span_device", C.c_int, [P, u64, u64, i32, C.POINTER(GpuStats)])
 _sig("hbam_reader_position", C.c_int, [P, u64, C.POINTER(u64)])
+_sig("hbam_pipeline_counters", C.c_int, [P, C.POINTER(u64)])
 _sig("hbam_file_stats", C.c_int, [P, C.POINTER(u64), C.POINTER(u64)])
 _sig("hbam_bytes_read", C.c_int, [P, C.POINTER(u64)])
 _sig("hbam_prefetch", C.c_int, [P, u64, u64])
@@ -96,6 +97,7 @@ _sig("hbam_splitting_index_for_records", C.c_int, [C.POINTER(Opts), P, u64, i32,
 _sig("hbam_build_splitting_index", C.c_int, [P, i32, C.POINTER(P), C.POINTER(u64)])
 _sig("hbam_splitting_entries", C.c_int, [P, u64, u64, i32, u64, C.POINTER(P), C.POINTER(u64), C.POINTER(u64)])
 _sig("hbam_guess_record_starts", C.c_int, [P, P, P, u64, P])
+_sig("hbam_guess_record_starts_hdr", C.c_int, [P, i32, P, P, u64, P])
 _sig("hbam_guess_bgzf_block_starts", C.c_int, [P, P, P, u64, P])
 _sig("hbam_get_splits", C.c_int, [P, P, P, u64, P, u64, P, P, C.POINTER(u64)])
 _sig("hbam_get_splits_bai", C.c_int, [P, P, P, u64, P, u64, P, u64, P, P, C.POINTER(u64)])
@@ -294,12 +296,15 @@ class Codec:
 
 def reader_callback(read):
     """hbam_read_fn over a Python positioned read: read(offset, n) -> bytes
-    (fewer than n only at the end of the file); an exception is an I/O error
-    (-1).  Keep the returned object alive as long as the ctx."""
+    (fewer than n only at the end of the file); an exception, or more than n
+    bytes (which would overrun the library's page-locked buffer), is an I/O
+    error (-1).  Keep the returned object alive as long as the ctx."""
     def cb(user, off, dst, n):
         try:
             b = read(int(off), int(n))
         except Exception:
+            return -1
+        if b is None or len(b) > n:
             return -1
         if b:
             C.memmove(dst, b, len(b))
@@ -323,6 +328,8 @@ class BamFile:
         self._h = P()
         o = _opts(device, check_crc, stringency, window_bytes, parallel_reads, batch_records)
         if reader is not None:
+            if size is None:
+                raise ValueError("BamFile(reader=...) needs size= (the file length)")
             self._cb = reader_callback(reader)
             rc = _L.hbam_open_reader(size, self._cb, None, C.byref(o), C.byref(self._h))
             self.size = size
@@ -399,6 +406,16 @@ class BamFile:
         if rc != OK:
             raise self._err(rc)
         return v.value
+
+    def pipeline_counters(self):
+        """Cumulative path counters of the ctx (hbam_pipeline_counters)."""
+        v = (u64 * 5)()
+        rc = _L.hbam_pipeline_counters(self._h, v)
+        if rc != OK:
+            raise self._err(rc)
+        return dict(zip(("link_fallbacks", "link_rewalks", "record_fallbacks", "inflate_launches",
+                         "records_after_stop"),
+                        (int(x) for x in v)))
 
     def decode_span_device(self, vstart, vend, timing=False, decode=True, digest=True):
         """The span decoded with the records left in HBM: stats dict."""
@@ -507,12 +524,19 @@ class BamFile:
             _L.hbam_free(p)
         return nr.value, ent
 
-    def guess_record_starts(self, begs, ends):
+    def guess_record_starts(self, begs, ends, header_n_ref=None):
+        """BAMSplitGuesser.guessNextBAMRecordStart for many split points;
+        header_n_ref: the sequence count of a header read from another stream
+        (the three-argument constructor), None = the file's own header."""
         n = len(begs)
         b = np.ascontiguousarray(begs, np.uint64)
         e = np.ascontiguousarray(ends, np.uint64)
         out = np.zeros(max(n, 1), np.uint64)
-        rc = _L.hbam_guess_record_starts(self._h, b.ctypes.data, e.ctypes.data, n, out.ctypes.data)
+        if header_n_ref is None:
+            rc = _L.hbam_guess_record_starts(self._h, b.ctypes.data, e.ctypes.data, n, out.ctypes.data)
+        else:
+            rc = _L.hbam_guess_record_starts_hdr(self._h, int(header_n_ref), b.ctypes.data, e.ctypes.data, n,
+                                                 out.ctypes.data)
         if rc != OK:
             raise self._err(rc)
         return [int(x) for x in out[:n]]
@@ -568,6 +592,67 @@ class BamFile:
         if rc != OK:
             raise self._err(rc)
         return buf.raw[:length]
+
+
+class BAMSplitGuesser:
+    """BAMSplitGuesser (BAMSplitGuesser.java:80-235) over a seekable stream,
+    as java/.../GpuBAMSplitGuesser.java: the stream is read through
+    hbam_open_reader by positioned reads (seek + read under a lock, one at a
+    time), so only the bytes a guess needs are read; the BGZF block search,
+    inflate and record checks run on the GPU (hbam_guess.hip).
+      BAMSplitGuesser(ss)                  the two-argument constructor: the
+                                           header comes from ss, whose first
+                                           four bytes must be the BGZF magic
+      BAMSplitGuesser(ss, header_stream)   the three-argument one: refIDs are
+                                           bounded by header_stream's sequence
+                                           dictionary (a seekable BAM stream)
+    ss / header_stream: binary file objects with seek / read."""
+
+    BGZF_MAGIC = b"\x1f\x8b\x08\x04"
+
+    def __init__(self, ss, header_stream=None, device=0):
+        import threading
+        lock = threading.Lock()
+
+        def positioned(stream):
+            def read(off, n):
+                with lock:
+                    stream.seek(off)
+                    return stream.read(n)
+            return read
+
+        def size_of(stream):
+            with lock:
+                return stream.seek(0, os.SEEK_END)
+
+        self._n_ref = None
+        if header_stream is not None and header_stream is not ss:
+            with BamFile(reader=positioned(header_stream), size=size_of(header_stream), device=device,
+                         stringency=SILENT) as hf:
+                self._n_ref = hf.header()["n_ref"]
+        self._f = BamFile(reader=positioned(ss), size=size_of(ss), device=device, stringency=SILENT)
+        if header_stream is None:  # :86-90 the secondary magic check
+            with lock:
+                ss.seek(0)
+                m = ss.read(4)
+            if m != self.BGZF_MAGIC:
+                self.close()
+                raise HbamError(E_FORMAT, "Does not seem like a BAM file")
+
+    def guessNextBAMRecordStart(self, beg, end):
+        """The virtual offset of the first BAM record in [beg, end), or end."""
+        return self._f.guess_record_starts([beg], [end], self._n_ref)[0]
+
+    def close(self):
+        if self._f is not None:
+            self._f.close()
+            self._f = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
 
 class Gpu:

@@ -51,7 +51,7 @@ extern "C" {
 #define HBAM_E_STATE 6
 #define HBAM_E_NOMEM 7
 
-#define HBAM_ABI_VERSION 5
+#define HBAM_ABI_VERSION 6
 
 /* htsjdk ValidationStringency, as util/SAMHeaderReader.java:45-46 reads it */
 #define HBAM_STRICT 0  /* htsjdk's default: SAMRecord.isValid errors -> SAMFormatException */
@@ -184,6 +184,13 @@ int hbam_splitting_index_for_records(const hbam_opts *opts, const uint64_t *voff
  * out[i] == ends[i] when no record start is found, as in the reference. */
 int hbam_guess_record_starts(hbam_ctx *ctx, const uint64_t *begs, const uint64_t *ends, uint64_t n,
                              uint64_t *out);
+/* The same with the header read from another stream than the data
+ * (BAMSplitGuesser(SeekableStream, InputStream headerStream, Configuration),
+ * BAMSplitGuesser.java:93-103): header_n_ref = that header's sequence
+ * dictionary size, which bounds the refIDs a guessed record may hold
+ * (record.setHeaderStrict(header), :185); < 0 = the data file's header. */
+int hbam_guess_record_starts_hdr(hbam_ctx *ctx, int32_t header_n_ref, const uint64_t *begs, const uint64_t *ends,
+                                 uint64_t n, uint64_t *out);
 
 /* util/BGZFSplitGuesser.guessNextBGZFBlockStart(beg, end)
  * (util/BGZFSplitGuesser.java:64-112) for n split points at once: the first
@@ -282,7 +289,8 @@ typedef struct hbam_gpu_stats {
   int32_t link_rewalks;       /* parallel-link re-walk rounds of this run */
   int32_t windows;            /* HBM windows the span was decoded in */
   float ms_tables;            /* k_huff_tables (ms_huff: k_inflate_huff, ms_lz77: k_inflate_lz77) */
-  int32_t reserved;
+  int32_t record_fallbacks;   /* windows whose record lists overflowed (indexer mode, records < 36 bytes):
+                               * per-block walks counted and emitted the records instead of the fused pass */
   /* order-sensitive digests (flags bit2): sum over the span's records i of
    * fmix64(x_i) * P^(n-1-i) mod 2^64, x = key / voff, P = HBAM_DIGEST_P;
    * the digests of consecutive spans A, B compose as D(A) * P^|B| + D(B) */
@@ -294,6 +302,16 @@ typedef struct hbam_gpu_stats {
  * digests (flags bit2) and per-stage timings (flags bit0) only; flags bit1
  * skips the field decode (chain + voffs only). */
 int hbam_decode_span_device(hbam_ctx *ctx, uint64_t vstart, uint64_t vend, int32_t flags, hbam_gpu_stats *st);
+
+/* Cumulative counters of the ctx's decode pipeline since the open, over every
+ * call (reader, indexer, device decodes): out[0] spans that took the exact
+ * serial link, out[1] parallel-link re-walk rounds, out[2] windows whose
+ * record lists overflowed, so that per-block walks counted and emitted the
+ * records (hbam_gpu_stats.record_fallbacks), out[3] inflate launch pairs,
+ * out[4] spans that stopped early (an error, EOF at an empty block) with
+ * records listed in later blocks, which the stop drops.  Diagnostics: tests
+ * assert which path a decode took. */
+int hbam_pipeline_counters(hbam_ctx *ctx, uint64_t out[5]);
 
 /* The sharded SplittingBAMIndexer.index (SplittingBAMIndexer.java:262-287,
  * SURVEY 8e step 3): the records of FileVirtualSplit [vstart, vend) read

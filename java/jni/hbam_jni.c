@@ -100,14 +100,28 @@ struct jreader {
 static struct jreader *g_readers = NULL; /* the readers of open ctxs, freed by close */
 static pthread_mutex_t g_readers_mu = PTHREAD_MUTEX_INITIALIZER;
 
-/* hbam_read_fn: called from library threads, attached here as daemons (a
- * thread the library keeps, e.g. its staging thread, stays attached) */
+/* A library thread that calls a reader is attached here as a daemon, and
+ * detached when it exits: the thread-specific value below holds its JavaVM,
+ * and the key's destructor runs DetachCurrentThread at thread exit (the JNI
+ * rule: a native thread detaches before it exits).  The library starts a
+ * staging thread per window and its copy pool threads live as long as the
+ * process; both exit through the destructor. */
+static pthread_key_t g_attach_key;
+static pthread_once_t g_attach_once = PTHREAD_ONCE_INIT;
+static void detach_at_exit(void *vm) {
+  if (vm) (*(JavaVM *)vm)->DetachCurrentThread((JavaVM *)vm);
+}
+static void make_attach_key(void) { (void)pthread_key_create(&g_attach_key, detach_at_exit); }
+
+/* hbam_read_fn: called from library threads */
 static int64_t jreader_read(void *user, uint64_t off, void *dst, uint64_t len) {
   struct jreader *r = (struct jreader *)user;
   JNIEnv *env = NULL;
-  if ((*r->vm)->GetEnv(r->vm, (void **)&env, JNI_VERSION_1_6) != JNI_OK &&
-      (*r->vm)->AttachCurrentThreadAsDaemon(r->vm, (void **)&env, NULL) != JNI_OK)
-    return -1;
+  if ((*r->vm)->GetEnv(r->vm, (void **)&env, JNI_VERSION_1_6) != JNI_OK) {
+    if ((*r->vm)->AttachCurrentThreadAsDaemon(r->vm, (void **)&env, NULL) != JNI_OK) return -1;
+    (void)pthread_once(&g_attach_once, make_attach_key);
+    (void)pthread_setspecific(g_attach_key, r->vm); /* detached by detach_at_exit */
+  }
   uint64_t done = 0;
   while (done < len) { /* direct buffers hold < 2 GiB */
     const uint64_t n = len - done < (1u << 30) ? len - done : (1u << 30);
@@ -271,7 +285,7 @@ JNIEXPORT jbyteArray FN(splittingIndexForRecords)(JNIEnv *env, jclass c, jint de
   return a;
 }
 
-JNIEXPORT jlongArray FN(guessRecordStarts)(JNIEnv *env, jclass c, jlong h, jlongArray begs, jlongArray ends) {
+static jlongArray guess_starts(JNIEnv *env, jlong h, jint header_n_ref, jlongArray begs, jlongArray ends) {
   jsize n, m;
   uint64_t *b = from_longs(env, begs, &n);
   if (!b) return NULL;
@@ -285,7 +299,7 @@ JNIEXPORT jlongArray FN(guessRecordStarts)(JNIEnv *env, jclass c, jlong h, jlong
     throw_for(env, HBAM_E_ARG, "begs and ends differ in length");
   } else {
     uint64_t *out = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(n ? n : 1));
-    int rc = out ? hbam_guess_record_starts(CTX(h), b, e, (uint64_t)n, out) : HBAM_E_NOMEM;
+    int rc = out ? hbam_guess_record_starts_hdr(CTX(h), header_n_ref, b, e, (uint64_t)n, out) : HBAM_E_NOMEM;
     if (rc != HBAM_OK) throw_for(env, rc, hbam_last_error(CTX(h)));
     else r = to_longs(env, out, n);
     free(out);
@@ -293,6 +307,15 @@ JNIEXPORT jlongArray FN(guessRecordStarts)(JNIEnv *env, jclass c, jlong h, jlong
   free(b);
   free(e);
   return r;
+}
+
+JNIEXPORT jlongArray FN(guessRecordStarts)(JNIEnv *env, jclass c, jlong h, jlongArray begs, jlongArray ends) {
+  return guess_starts(env, h, -1, begs, ends);
+}
+
+JNIEXPORT jlongArray FN(guessRecordStartsHdr)(JNIEnv *env, jclass c, jlong h, jint header_n_ref, jlongArray begs,
+                                              jlongArray ends) {
+  return guess_starts(env, h, header_n_ref, begs, ends);
 }
 
 JNIEXPORT jlongArray FN(getSplits)(JNIEnv *env, jclass c, jlong h, jlongArray starts, jlongArray lengths,

@@ -3,16 +3,21 @@
 // BAMRecordReader on the MI355X read path (libhbam.so through HbamNative).
 // Same contract as BAMRecordReader (BAMRecordReader.java:63-233): key =
 // getKey(record) (refIdx << 32 | alignmentStart0, MurmurHash3 branch for
-// unmapped reads), value = a LazyBAMRecord in a SAMRecordWritable, records
+// unmapped reads), value = a BAMRecord in a SAMRecordWritable, records
 // of the FileVirtualSplit [vStart, vEnd) in file order, getProgress from the
 // stream position htsjdk's iterator would stand at.
 //
 // What moves to the GPU: BGZF block discovery, inflate, the record chain, the
 // htsjdk validation rules of the configured stringency and the 11 fixed
 // fields + key + voff of every record (hbam_decode_span, in batches).  What
-// stays here: building the LazyBAMRecord of each record from the batch's
+// stays here: building the record object of each record from the batch's
 // columns, exactly the arguments htsjdk's BAMRecordCodec.decode passes to
-// LazyBAMRecordFactory.createBAMRecord (LazyBAMRecordFactory.java:37-50).
+// SAMRecordFactory.createBAMRecord.  The reference's reader opens its
+// SamReader with no record factory (BAMRecordReader.java:186-200), so its
+// values are htsjdk's DefaultSAMRecordFactory BAMRecords, and so are these
+// (class and reference-name resolution included); the writable codec keeps
+// LazyBAMRecordFactory (LazyBAMRecordFactory.java:37-50), as
+// SAMRecordWritable's readFields does (SAMRecordWritable.java:47-48).
 // With hadoopbam.gpu.encode-writables the values are GpuSAMRecordWritables
 // that also carry their SAMRecordWritable.write bytes, encoded per batch on
 // the GPU (hbam_encode_writables).
@@ -25,8 +30,10 @@
 // native methods of HbamNative exactly as declared there.
 package org.seqdoop.hadoop_bam;
 
+import htsjdk.samtools.DefaultSAMRecordFactory;
 import htsjdk.samtools.SAMFileHeader;
 import htsjdk.samtools.SAMRecord;
+import htsjdk.samtools.SAMRecordFactory;
 import htsjdk.samtools.ValidationStringency;
 import java.io.IOException;
 import java.nio.ByteBuffer;
@@ -48,7 +55,8 @@ public class GpuBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
   public static final String WINDOW_BYTES_PROPERTY = "hadoopbam.gpu.window-bytes";
 
   private final LongWritable key = new LongWritable();
-  private final LazyBAMRecordFactory factory = new LazyBAMRecordFactory();
+  // SamReaderFactory.makeDefault()'s factory: BAMRecordReader.createSamReader sets none
+  private final SAMRecordFactory factory = DefaultSAMRecordFactory.getInstance();
   // a GpuSAMRecordWritable carrying its record's writable bytes when
   // hadoopbam.gpu.encode-writables is set (GpuSAMRecordWritable.java)
   private SAMRecordWritable record = new SAMRecordWritable();
@@ -134,7 +142,7 @@ public class GpuBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
     n = cols[HbamNative.KEY].capacity() / 8;
     i = 0;
     // hbam_encode_writables encodes the last decodeSpan batch: now, before the next call
-    encoded = encode && n > 0 ? GpuSAMRecordWritable.EncodedBatch.of(ctx, n) : null;
+    if (encode && n > 0) encoded = GpuSAMRecordWritable.EncodedBatch.of(ctx, n, encoded);  // reuses its buffer
   }
 
   @Override
@@ -198,11 +206,12 @@ public class GpuBAMRecordReader extends RecordReader<LongWritable, SAMRecordWrit
   }
 
   /**
-   * The LazyBAMRecord htsjdk's BAMRecordCodec.decode builds for record j of a
-   * batch (decodeSpan or decodeWritables columns); header null as
-   * SAMRecordWritable's lazyCodec (SAMRecordWritable.java:47-48).
+   * The record htsjdk's BAMRecordCodec.decode builds with factory for record
+   * j of a batch (decodeSpan or decodeWritables columns): the reader's
+   * default-factory BAMRecord, or the writable codec's LazyBAMRecord with
+   * header null as SAMRecordWritable's lazyCodec (SAMRecordWritable.java:47-48).
    */
-  static SAMRecord recordAt(ByteBuffer[] cols, int j, SAMFileHeader header, LazyBAMRecordFactory factory) {
+  static SAMRecord recordAt(ByteBuffer[] cols, int j, SAMFileHeader header, SAMRecordFactory factory) {
     final ByteBuffer data = cols[HbamNative.DATA];
     final long off = cols[HbamNative.REST_OFF].getLong(8 * j);
     final int len = cols[HbamNative.REST_LEN].getInt(4 * j);

@@ -11,10 +11,13 @@
 //       of each record, back to back), and hands out values that carry their
 //       record's slice of that buffer.  write copies the slice: the bytes are
 //       those the reference's codec writes for the record as read.  A value
-//       whose record was replaced with set(...) encodes through htsjdk, as the
-//       reference does.  The property is for jobs whose mappers pass the
-//       reader's records on without changing them in place (sort, partition,
-//       filter): a record mutated in place would still write its bytes as read.
+//       whose record was replaced with set(...), or changed in place since it
+//       was read, encodes through htsjdk, as the reference does: write
+//       compares the record's fixed fields with the encoded ones, and htsjdk's
+//       BAMRecord drops its variable-length bytes (getVariableBinaryRepresentation
+//       returns null) once a setter touches the read name, cigar, bases,
+//       qualities or tags.  The batch buffer is one direct buffer per reader,
+//       grown when a batch needs more and reused across batches.
 //   readFields(DataInput) :66-68
 //       one value at a time from a stream: the reference's codec (there is no
 //       batch to hand to a device).
@@ -49,15 +52,45 @@ public class GpuSAMRecordWritable extends SAMRecordWritable {
       this.offs = offs;
     }
 
-    /** The last decodeSpan batch of ctx (n records), encoded. */
-    static EncodedBatch of(long ctx, int n) throws IOException {
+    /**
+     * The last decodeSpan batch of ctx (n records), encoded into prev's
+     * direct buffer when it is large enough (the reader's previous batch:
+     * its values are dead once the next batch is decoded), else into a new
+     * one with room to spare.  Direct buffers are freed only by GC, so one per
+     * reader keeps a long split from churning direct memory.
+     */
+    static EncodedBatch of(long ctx, int n, EncodedBatch prev) throws IOException {
       final long total = HbamNative.encodeWritables(ctx, null, null);  // sizes only
       if (total > Integer.MAX_VALUE)  // the largest direct ByteBuffer: lower hadoopbam.gpu.batch-records
         throw new IOException("encoded batch of " + total + " bytes exceeds a ByteBuffer");
-      final ByteBuffer b = ByteBuffer.allocateDirect((int) total);
-      final long[] offs = new long[n + 1];
+      ByteBuffer b = prev != null ? prev.bytes : null;
+      if (b == null || b.capacity() < total)
+        b = ByteBuffer.allocateDirect((int) Math.min(Integer.MAX_VALUE, Math.max(total, total + total / 4)));
+      b.clear();
+      final long[] offs = prev != null && prev.offs.length >= n + 1 ? prev.offs : new long[n + 1];
       HbamNative.encodeWritables(ctx, b, offs);
-      return new EncodedBatch(b, offs);
+      final EncodedBatch e = new EncodedBatch(b, offs);
+      e.scratch = prev != null ? prev.scratch : e.scratch;
+      return e;
+    }
+
+    /**
+     * Whether r still encodes to record i's bytes: its fixed fields equal
+     * the encoded ones (BAMRecordCodec.encode's order after block_size:
+     * refID, pos, bin_mq_nl, flag_nc, l_seq, next_refID, next_pos, tlen) and
+     * htsjdk still holds its variable-length bytes as read.
+     */
+    boolean encodes(int i, SAMRecord r) {
+      if (r.getVariableBinaryRepresentation() == null) return false;  // a setter made them stale
+      final ByteBuffer b = bytes.duplicate().order(ByteOrder.LITTLE_ENDIAN);
+      final int o = (int) offs[i] + 4;
+      final int ref = b.getInt(o), pos = b.getInt(o + 4), binMqNl = b.getInt(o + 8), flagNc = b.getInt(o + 12);
+      final Integer bin = r.getIndexingBin();
+      return r.getReferenceIndex() == ref && r.getAlignmentStart() - 1 == pos
+          && r.getMappingQuality() == ((binMqNl >>> 8) & 0xff) && r.getFlags() == (flagNc >>> 16)
+          && r.getMateReferenceIndex() == b.getInt(o + 20) && r.getMateAlignmentStart() - 1 == b.getInt(o + 24)
+          && r.getInferredInsertSize() == b.getInt(o + 28)
+          && (ref < 0 || bin == null || bin == (binMqNl >>> 16));
     }
 
     /** Record i's bytes to out: what SAMRecordWritable.write writes for it. */
@@ -89,10 +122,10 @@ public class GpuSAMRecordWritable extends SAMRecordWritable {
     batch = null;
   }
 
-  /** As SAMRecordWritable.write (:55-65); the batch's bytes when they encode this record. */
+  /** As SAMRecordWritable.write (:55-65); the batch's bytes when they encode this record as it is now. */
   @Override
   public void write(DataOutput out) throws IOException {
-    if (batch != null && get() == encodedRecord) batch.write(index, out);
+    if (batch != null && get() == encodedRecord && batch.encodes(index, encodedRecord)) batch.write(index, out);
     else super.write(out);
   }
 

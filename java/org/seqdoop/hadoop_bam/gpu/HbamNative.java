@@ -129,6 +129,15 @@ public final class HbamNative {
   public static native long[] guessRecordStarts(long ctx, long[] begs, long[] ends) throws IOException;
 
   /**
+   * hbam_guess_record_starts_hdr: the same with the header read from another
+   * stream than the data (BAMSplitGuesser(SeekableStream, InputStream,
+   * Configuration)); headerNRef = its sequence dictionary size (-1: the data
+   * file's own header).
+   */
+  public static native long[] guessRecordStartsHdr(long ctx, int headerNRef, long[] begs, long[] ends)
+      throws IOException;
+
+  /**
    * hbam_get_splits_bai: the FileVirtualSplits of one file's FileSplits, from
    * the .splitting-bai (sbi), else -- when hadoopbam.bam.enable-bai-splitter
    * is set and the file has a .bai (bai) -- the BAI split calculator, else

@@ -1131,6 +1131,14 @@ static int decode_verify(gz_reader *g, int32_t n_ref) {
 }
 
 int orc_guess_record_start(orc_stream *s, const uint8_t *file, uint64_t flen, uint64_t beg, uint64_t end, uint64_t *out) {
+  return orc_guess_record_start_hdr(s, file, flen, s->n_ref, beg, end, out);
+}
+
+/* BAMSplitGuesser(ss, headerStream, conf) (BAMSplitGuesser.java:93-103): the
+ * record checks bound refIDs by the header stream's dictionary (n_ref), the
+ * first record of beg == 0 still comes from the data (:115-123) */
+int orc_guess_record_start_hdr(orc_stream *s, const uint8_t *file, uint64_t flen, int32_t n_ref, uint64_t beg,
+                               uint64_t end, uint64_t *out) {
   if (beg == 0) { /* :115-123 header parse -> first record voff */
     *out = orc_first_record_voff(s);
     return ORC_OK;
@@ -1151,7 +1159,7 @@ int orc_guess_record_start(orc_stream *s, const uint8_t *file, uint64_t flen, ui
     if (gz_seek(&g, cp0Virt) != GZ_OK) continue; /* catch Throwable */
     for (int32_t up = 0;; ++up) {
       int fatal;
-      const int32_t up0 = up = guess_next_bam_pos(&g, cp0Virt, up, psize, s->n_ref, &fatal);
+      const int32_t up0 = up = guess_next_bam_pos(&g, cp0Virt, up, psize, n_ref, &fatal);
       if (fatal) { gz_free(&g); return set_err(s, ORC_E_FORMAT, "exception escaped guessNextBAMPos"); }
       if (up0 < 0) break;
       if (gz_seek(&g, cp0Virt | (uint64_t)up0) != GZ_OK) continue;
@@ -1159,7 +1167,7 @@ int orc_guess_record_start(orc_stream *s, const uint8_t *file, uint64_t flen, ui
       int b = 0;
       uint64_t prevCP = (uint64_t)cp0;
       while (b < 3) {
-        int dr = decode_verify(&g, s->n_ref);
+        int dr = decode_verify(&g, n_ref);
         if (dr == DEC_NULL) break;
         if (dr == DEC_REJECT) { accept = 0; break; }
         if (dr == DEC_TRUNC || dr == DEC_EOF) {  /* FileTruncated / RuntimeEOF */

@@ -119,6 +119,10 @@ int orc_guess_bgzf_pos(const uint8_t *arr, uint64_t alen, int32_t p, int32_t end
 /* BAMSplitGuesser.guessNextBAMRecordStart (BAMSplitGuesser.java:108-235). */
 int orc_guess_record_start(orc_stream *s, const uint8_t *file, uint64_t flen,
                            uint64_t beg, uint64_t end, uint64_t *out);
+/* the same with the refIDs bounded by another header's dictionary size
+ * (BAMSplitGuesser(ss, headerStream, conf), BAMSplitGuesser.java:93-103) */
+int orc_guess_record_start_hdr(orc_stream *s, const uint8_t *file, uint64_t flen, int32_t n_ref, uint64_t beg,
+                               uint64_t end, uint64_t *out);
 
 /* BGZFSplitGuesser.guessNextBGZFBlockStart (util/BGZFSplitGuesser.java:64-112)
  * restated for the TestBGZFSplitGuesser pins. */

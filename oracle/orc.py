@@ -48,6 +48,7 @@ def lib():
         L.orc_get_key.argtypes = [i32, i32, C.c_uint16, P, u32]
         L.orc_get_key.restype = i64
         L.orc_guess_record_start.argtypes = [P, P, u64, u64, u64, C.POINTER(u64)]
+        L.orc_guess_record_start_hdr.argtypes = [P, P, u64, C.c_int32, u64, u64, C.POINTER(u64)]
         L.orc_guess_next_bgzf_block_start.argtypes = [P, u64, u64, u64]
         L.orc_guess_next_bgzf_block_start.restype = i64
         L.orc_get_splits.argtypes = [P, P, u64, P, P, u64, P, u64, P, P, C.POINTER(u64)]
@@ -137,6 +138,15 @@ class Stream:
         n = L.orc_data_len(self._h)
         return C.string_at(L.orc_data(self._h), n) if n else b""
 
+    def data_array(self):
+        """The inflated stream as a uint8 array over the oracle's buffer (no
+        copy; valid while the Stream lives; any size, string_at stops at 2 GiB)."""
+        L = lib()
+        n = L.orc_data_len(self._h)
+        if not n:
+            return np.zeros(0, np.uint8)
+        return np.ctypeslib.as_array((C.c_uint8 * n).from_address(L.orc_data(self._h)))
+
     @property
     def data_len(self):
         return lib().orc_data_len(self._h)
@@ -194,10 +204,14 @@ class Stream:
         L.orc_free(p)
         return b
 
-    def guess_record_start(self, beg, end):
+    def guess_record_start(self, beg, end, header_n_ref=None):
         L = lib()
         out = C.c_uint64()
-        rc = L.orc_guess_record_start(self._h, self._buf, len(self.file), beg, end, C.byref(out))
+        if header_n_ref is None:
+            rc = L.orc_guess_record_start(self._h, self._buf, len(self.file), beg, end, C.byref(out))
+        else:
+            rc = L.orc_guess_record_start_hdr(self._h, self._buf, len(self.file), header_n_ref, beg, end,
+                                              C.byref(out))
         if rc != 0:
             raise OracleError(rc, L.orc_error(self._h).decode())
         return out.value

@@ -23,7 +23,7 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch
   > /dev/null 2> $OUT/fetch.err || { echo "FETCH_SIZE pass failed"; tail -5 $OUT/fetch.err; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $PMCB \
   > /dev/null 2> $OUT/write.err || { echo "WRITE_SIZE pass failed"; tail -5 $OUT/write.err; exit 1; }
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT \
-  SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $OUT/sq -o run -- $PMCB \
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
+  SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq -o run -- $PMCB \
   > /dev/null 2> $OUT/sq.err || { echo "SQ pass failed"; tail -5 $OUT/sq.err; exit 1; }
 python3 $R/profiles/summarize.py $OUT > $OUT/summary.json && cat $OUT/summary.json

@@ -184,6 +184,12 @@ def main():
                 e[cn] = v
         if "SQ_LDS_BANK_CONFLICT" in c and c.get("SQ_INSTS_LDS"):
             e["lds_bank_conflict_per_lds_inst"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_INSTS_LDS"]
+        if "SQ_LDS_IDX_ACTIVE" in c and c.get("SQ_INSTS_LDS"):
+            e["lds_cycles_per_lds_inst"] = c["SQ_LDS_IDX_ACTIVE"] / c["SQ_INSTS_LDS"]
+        for pre in ("", "main:"):
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs; one LDS array per CU (256)
+            if c.get(pre + "SQ_LDS_IDX_ACTIVE") is not None and c.get(pre + "GRBM_GUI_ACTIVE"):
+                e[pre.replace(":", "_") + "lds_frac"] = c[pre + "SQ_LDS_IDX_ACTIVE"] / (256 * c[pre + "GRBM_GUI_ACTIVE"] / 8)
         if c.get("SQ_ACTIVE_INST_VALU") is not None and c.get("SQ_WAVE_CYCLES"):
             e["valu_active_frac_of_wave_cycles"] = c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"]
         res[k] = e

@@ -78,13 +78,21 @@ for s in $STEPS; do
       grep -E "^(mapped|resident)" $OUT/ordertrace.log | cut -c1-200 ;;
     variants)
       # stage times + overlapped wall time per pass: the default build, the
-      # in-tree experiment builds (lib/variants), the unfused record pass
+      # in-tree experiment builds (lib/variants)
       timeout -k 10 400 python -u scripts/probe_inflate.py 10000000 hadoop-bam_amd/lib/libhbam.so \
         $(ls hadoop-bam_amd/lib/variants/*.so 2>/dev/null) > $OUT/variants.log 2>&1 \
         || { echo "variants failed"; tail -30 $OUT/variants.log; exit 5; }
-      HBAM_FUSED_RECORDS=0 timeout -k 10 200 python -u scripts/probe_inflate.py 10000000 >> $OUT/variants.log 2>&1 \
-        || { echo "unfused probe failed"; tail -30 $OUT/variants.log; exit 5; }
       cat $OUT/variants.log ;;
+    gaps)
+      # kernel trace of production-order passes (no events): overlap and idle time of the last pass
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/gaps -o run \
+        -- python3 $R/scripts/probe_inflate.py 10000000 > $OUT/gaps_probe.log 2>&1) || { echo "gaps trace failed"; tail -20 $OUT/gaps_probe.log; exit 11; }
+      python3 scripts/pass_gaps.py $OUT/gaps > $OUT/gaps.txt 2>&1 || { echo "gaps analysis failed"; cat $OUT/gaps.txt; exit 11; }
+      cat $OUT/gaps.txt ;;
+    pmcab)
+      # SQ issue / LDS counters of the inflate kernels per build (default + lib/variants)
+      timeout -k 10 900 bash scripts/pmc_ab.sh $TAG > $OUT/pmcab.log 2>&1 || { echo "pmc a/b failed"; tail -20 $OUT/pmcab.log; exit 10; }
+      cat $OUT/pmcab.log ;;
     dtrace)
       # host-side timeline of the drop-in 1 M-batch loop (window copies, decode
       # steps, batch issues, serial-link fallbacks)

@@ -20,7 +20,7 @@ def test_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert hbam.lib().hbam_abi_version() == 5
+    assert hbam.lib().hbam_abi_version() == 6
 
 
 def test_struct_layouts_match_header(tmp_path):

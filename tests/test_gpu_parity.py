@@ -1,6 +1,7 @@
 """GPU parity: libhbam (gfx950 kernels, through the C ABI) vs the oracle and
 the committed golden vectors.  Bit-exact everywhere (integer/byte work)."""
 import hashlib
+import zlib
 
 import numpy as np
 import pytest
@@ -11,6 +12,7 @@ from conftest import golden_path
 from hbam import synth
 
 pytestmark = pytest.mark.gpu
+ALL = (1 << 64) - 1
 
 FIELDS = ["ref_id", "pos", "l_seq", "next_ref_id", "next_pos", "tlen", "l_read_name", "mapq", "bin",
           "n_cigar", "flag", "key", "voff", "rest_len"]
@@ -214,8 +216,11 @@ def test_record_errors_match_oracle(rec, off, val, code):
 
 def test_c2_full_size_vs_oracle():
     """BASELINE config C2 at full size (10 M records, 1.41 GB BGZF): every key
-    and voff of the device pipeline and the .splitting-bai (g = 4096) through
-    the SplittingBAMIndexer entry point, bit-exact against the oracle."""
+    and voff of the device pipeline, the .splitting-bai (g = 4096) through
+    the SplittingBAMIndexer entry point, and through the reader entry point
+    (hbam_decode_span in 2 M-record batches) all 11 fixed-field columns, the
+    rest lengths and every rest byte (CRC-32 of all rests in record order),
+    bit-exact against the oracle."""
     data, info = synth.make_bam(10_000_000, as_numpy=True)
     raw = data.tobytes()
     g = hbam.Gpu(0)
@@ -230,9 +235,27 @@ def test_c2_full_size_vs_oracle():
     np.testing.assert_array_equal(voffs, want["voff"])
     np.testing.assert_array_equal(keys, want["key"])
     want_sbi = s.splitting_index(4096)
-    del want, s
-    with hbam.BamFile(raw) as f:
+    # the oracle's rests: the inflated records without their 36-byte heads
+    # (records are back to back from the first one to the last one's end)
+    u = s.data_array()
+    off = want["offset"].astype(np.int64)
+    lo, hi = int(off[0]), int(off[-1]) + 36 + int(want["rest_len"][-1])
+    head = np.zeros(hi - lo, bool)
+    for j in range(36):
+        head[off - lo + j] = True
+    want_crc = zlib.crc32(u[lo:hi][~head])
+    del head, u, s
+    with hbam.BamFile(raw, batch_records=1 << 21) as f:
         assert f.splitting_index(4096) == want_sbi
+        parts, crc = {k: [] for k in FIELDS}, 0
+        for b in f.iter_batches(f.header()["first_record_voff"], ALL, 1 << 21):
+            assert b["status"] == 0
+            for k in FIELDS:
+                parts[k].append(b[k])
+            crc = zlib.crc32(b["data"], crc)
+    for k in FIELDS:
+        np.testing.assert_array_equal(np.concatenate(parts[k]), want[k], err_msg=k)
+    assert crc == want_crc
 
 
 def test_c4_long_reads_vs_oracle():

@@ -85,8 +85,11 @@ def test_reader_mirrors_the_reference_reader_surface():
                  "public LongWritable getCurrentKey()", "public SAMRecordWritable getCurrentValue()",
                  "public void close()"):
         assert meth in src, meth
-    # the record is built with the codec's argument order (LazyBAMRecordFactory.java:37-50)
+    # the record is built with the codec's argument order (LazyBAMRecordFactory.java:37-50), by
+    # the factory the reference's SamReader uses: none is set (BAMRecordReader.java:186-200), so
+    # htsjdk's default BAMRecords
     assert "factory.createBAMRecord(" in src
+    assert "SAMRecordFactory factory = DefaultSAMRecordFactory.getInstance()" in src
 
 
 REF_INDEXER = "/root/reference/src/main/java/org/seqdoop/hadoop_bam/SplittingBAMIndexer.java"
@@ -130,6 +133,27 @@ def test_write_time_indexer_keeps_o1_state():
 
 
 REF = "/root/reference/src/main/java/org/seqdoop/hadoop_bam"
+
+
+def test_gpu_guesser_has_the_reference_guesser_api():
+    """GpuBAMSplitGuesser offers BAMSplitGuesser's public entry points
+    (BAMSplitGuesser.java:80-108, 340): both constructors, the guess and main,
+    on the same base class; it reads through a positioned reader over the
+    SeekableStream and guesses through hbam_guess_record_starts_hdr."""
+    src = _strip_comments(open(os.path.join(JAVA, "GpuBAMSplitGuesser.java")).read())
+    assert "class GpuBAMSplitGuesser extends BaseSplitGuesser" in src
+    ref_file = os.path.join(REF, "BAMSplitGuesser.java")
+    if os.path.exists(ref_file):
+        ref = _public_signatures(_strip_comments(open(ref_file).read()))
+        ref = {("GpuBAMSplitGuesser" if n == "BAMSplitGuesser" else n, t) for n, t in ref}
+    else:  # the reference's list, as read from the file above when it was present
+        ref = {("GpuBAMSplitGuesser", ("SeekableStream", "Configuration")),
+               ("GpuBAMSplitGuesser", ("SeekableStream", "InputStream", "Configuration")),
+               ("guessNextBAMRecordStart", ("long", "long")), ("main", ("String[]",))}
+    have = _public_signatures(src)
+    assert ref <= have, ref - have
+    assert "HbamNative.openReader(" in src and "HbamNative.guessRecordStartsHdr(" in src
+    assert "SAMHeaderReader.readSAMHeaderFrom(headerStream, conf)" in src
 
 
 def test_writable_and_writer_mirror_the_reference_surface():
