@@ -100,26 +100,60 @@ __global__ __launch_bounds__(256) void k_bgzf_scan(const uint8_t* __restrict__ b
 #ifndef HBAM_SCAN_U
 #define HBAM_SCAN_U 4
 #endif
+#ifndef HBAM_SCAN_PIPE
+#define HBAM_SCAN_PIPE 1
+#endif
+#ifndef HBAM_SCAN_GRID
+#define HBAM_SCAN_GRID 8192
+#endif
   constexpr int kU = HBAM_SCAN_U;
+  // Candidates are collected per workgroup in LDS and reserved in cand[] by
+  // one global atomic per workgroup: every candidate's own atomicAdd on one
+  // device-scope counter serialized across the 8 XCDs.
+  constexpr uint32_t kWgCand = 256;
+  __shared__ uint64_t s_cand[kWgCand];
+  __shared__ uint32_t s_n, s_base;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
   const uint64_t nc = (len + 15) / 16;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * kU;
   const uint32_t lane = lane_id();
   const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * kU;
-  for (uint64_t c0 = wave0; c0 < nc; c0 += stride) {
-    uint4 vv[kU];
+  // the iteration's kU chunks per lane and the last lane's 4 bytes past them
+  // (buf is zero padded past len)
+  auto fetch = [&](uint64_t c0, uint4* vv, uint32_t& tail) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const uint64_t c = c0 + 64 * u + lane;
       vv[u] = c < nc ? reinterpret_cast<const uint4*>(buf)[c] : make_uint4(0, 0, 0, 0);
     }
-    const uint64_t clast = c0 + 64 * (kU - 1) + 63;  // (buf is zero padded past len)
-    const uint32_t tail = lane == 63 && clast < nc ? *reinterpret_cast<const uint32_t*>(buf + 16 * clast + 16) : 0u;
+    const uint64_t clast = c0 + 64 * (kU - 1) + 63;
+    tail = lane == 63 && clast < nc ? *reinterpret_cast<const uint32_t*>(buf + 16 * clast + 16) : 0u;
+  };
+#if HBAM_SCAN_PIPE
+  // software-pipelined: the next iteration's loads are in flight while this
+  // one's chunks are tested
+  uint4 nv[kU];
+  uint32_t ntail = 0;
+  if (wave0 < nc) fetch(wave0, nv, ntail);
+#endif
+  for (uint64_t c0 = wave0; c0 < nc; c0 += stride) {
+    uint4 vv[kU];
+    uint32_t tail;
+#if HBAM_SCAN_PIPE
+#pragma unroll
+    for (int u = 0; u < kU; ++u) vv[u] = nv[u];
+    tail = ntail;
+    if (c0 + stride < nc) fetch(c0 + stride, nv, ntail);
+#else
+    fetch(c0, vv, tail);
+#endif
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
     const uint64_t c = c0 + 64 * u + lane;  // the wave stays converged through the shuffle
     const uint4 v = vv[u];
     uint32_t nx = (uint32_t)__shfl_down((int)v.x, 1, 64);
-    // the wave's last lane: the next step's first chunk (lane 0), or memory
+    // the wave's last lane: the next step's first chunk (lane 0), or the tail
     const uint32_t next0 = u + 1 < kU ? (uint32_t)__shfl((int)vv[u + 1 < kU ? u + 1 : u].x, 0, 64) : 0u;
     if (lane == 63) nx = u + 1 < kU ? next0 : tail;
     const uint32_t w[5] = {v.x, v.y, v.z, v.w, nx};
@@ -137,16 +171,28 @@ __global__ __launch_bounds__(256) void k_bgzf_scan(const uint8_t* __restrict__ b
         const uint32_t xlen = ldu32(buf, p + 10) & 0xffffu;
         const uint32_t sub = ldu32(buf, p + 12);
         if (xlen != 6 || sub != 0x00024342u) continue;
-        const uint32_t i = atomicAdd(count, 1u);
-        if (i < cap) cand[i] = base + p;
+        const uint32_t j = atomicAdd(&s_n, 1u);
+        if (j < kWgCand) {
+          s_cand[j] = base + p;
+        } else {  // (more than kWgCand block headers in one workgroup's range: tiny blocks)
+          const uint32_t i = atomicAdd(count, 1u);
+          if (i < cap) cand[i] = base + p;
+        }
       }
     }
     }
   }
+  __syncthreads();
+  const uint32_t nw = min(s_n, kWgCand);
+  if (threadIdx.x == 0) s_base = nw ? atomicAdd(count, nw) : 0u;
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < nw; t += blockDim.x)
+    if (s_base + t < cap) cand[s_base + t] = s_cand[t];
 }
 
 // Verify the sorted candidate chain and fill BlockInfo.  flags[0] |= 1 on any
-// break (fallback), flags[1] = first block index with ISIZE > 64 KiB.
+// break (fallback), flags[1] = first block index with ISIZE > 64 KiB,
+// flags[3] += the empty blocks (ISIZE 0: candidates for dead positions).
 // partial (streamed upload, bytes past hi not there yet): a last candidate
 // whose block runs past hi is the incomplete tail -> flags[2] = 1, not a break.
 __global__ void k_bgzf_verify(const uint8_t* __restrict__ file, uint64_t lo, uint64_t hi,
@@ -175,6 +221,7 @@ __global__ void k_bgzf_verify(const uint8_t* __restrict__ file, uint64_t lo, uin
   b.isize = ldu32(file, next - 4);
   b.flags = 0;
   if (b.isize > kMaxIsize) atomicMin(&flags[1], i);
+  if (b.isize == 0) atomicAdd(&flags[3], 1u);
   blocks[i] = b;
 }
 
@@ -2617,6 +2664,32 @@ __device__ __forceinline__ bool plausible(const ChainEnv& E, uint64_t q) {
   return E.u[q + 36 + lrn - 1] == 0;
 }
 
+// plausible() split for a software-pipelined walk: plausible_head decides
+// from q's head h alone (1: plausible, 0: not, 2: the read-name end byte at
+// q + 36 + lrn - 1 decides: *name_at = its position), so that a walk can
+// load that byte together with the next record's head (q + 4 + block_size):
+// one dependent memory round trip per record instead of two.  Same result
+// as plausible(E, q) when h = load_head(E.u, q).
+__device__ __forceinline__ int plausible_head(const ChainEnv& E, uint64_t q, const RecHead& h, uint64_t* name_at) {
+  if (q + 36 > E.e_inf) return E.e_inf < E.e_true && q + 4 <= E.e_inf && (int32_t)h.at(0) >= 32;
+  int32_t bs = (int32_t)h.at(0);
+  int32_t ref = (int32_t)h.at(1);
+  int32_t pos = (int32_t)h.at(2);
+  uint32_t lrn = h.at(3) & 0xffu;
+  uint32_t ncig = h.at(4) & 0xffffu;
+  int32_t lseq = (int32_t)h.at(5);
+  int32_t nref = (int32_t)h.at(6);
+  int32_t npos = (int32_t)h.at(7);
+  if (ref < -1 || ref >= E.n_ref || nref < -1 || nref >= E.n_ref) return 0;
+  if (pos < -1 || npos < -1 || lrn < 1 || lseq < 0) return 0;
+  int64_t need = 32 + (int64_t)lrn + 4 * (int64_t)ncig + (int64_t)lseq + ((int64_t)lseq + 1) / 2;
+  if ((int64_t)bs < need) return 0;
+  if (q + 4 + (uint64_t)bs > E.e_true) return 0;
+  if (q + 36 + lrn > E.e_inf) return E.e_inf < E.e_true;
+  *name_at = q + 36 + lrn - 1;
+  return 2;
+}
+
 // plausible() at q and at the record after it (or the end / unreadable data):
 // a cheap second check that removes most false candidates inside long records.
 __device__ __forceinline__ bool plausible2(const ChainEnv& E, uint64_t q) {
@@ -3146,27 +3219,34 @@ __global__ __launch_bounds__(256) void k_rec_walk(ChainEnv E, const uint64_t* __
     } else {
       const uint64_t c = cand[i];
       if (c < bend) {  // c == kNone (no candidate): nothing to walk
-        uint64_t q = c;
+        // software-pipelined: record q's read-name end byte and the next
+        // record's head are loaded together (plausible_head), one dependent
+        // round trip per record.  Loads past the inflated range read the
+        // stream's padding and are not used (plausible_head's rules).
+        uint64_t q = c, exitq = c;
         uint32_t m = 0;
         bool valid = true;
-        while (q < bend) {
-          if (!plausible(E, q)) { valid = false; break; }
-          if (m < kListCap) L[m] = (uint16_t)(q - b.ustart);
-          ++m;
-          q += 4 + (uint64_t)(int32_t)ldu32(E.u, q);
-        }
-        // the chain must go on plausibly past the block end for a few records
-        // (or reach the end / unreadable data): a false start one or two bytes
-        // before a true one reads a huge block_size and lands at random, and a
-        // single landing check passes too often (~1 in 2000 blocks on C2)
-        if (valid) {
-          uint64_t y = q;
-          for (int k = 0; k < kGuessLookahead; ++k) {
-            if (y == E.e_true || y + 36 > E.e_inf) break;
-            if (!plausible(E, y)) { valid = false; break; }
-            y += 4 + (uint64_t)(int32_t)ldu32(E.u, y);
+        RecHead h = load_head(E.u, q);
+        int left = kGuessLookahead;  // plausible records required past the block end
+        for (;;) {
+          const bool inside = q < bend;
+          if (!inside && (left-- <= 0 || q == E.e_true || q + 36 > E.e_inf)) break;
+          uint64_t na = q;
+          const int ph = plausible_head(E, q, h, &na);
+          const uint64_t q2 = q + 4 + (uint64_t)(int32_t)h.at(0);
+          const uint8_t nb = E.u[na];
+          // (q2 may lie anywhere: its head is loaded when its block_size is
+          // inflated; reads reach 40 bytes past it, inside the stream's pad)
+          h = load_head(E.u, q2 + 4 <= E.e_inf ? q2 : q);
+          if (ph == 0 || (ph == 2 && nb != 0)) { valid = false; break; }
+          if (inside) {
+            if (m < kListCap) L[m] = (uint16_t)(q - b.ustart);
+            ++m;
+            exitq = q2;  // the first record start past the block (the walk's exit)
           }
+          q = q2;
         }
+        q = exitq;
         if (valid) {
           g = c;
           x = q;
@@ -3808,7 +3888,7 @@ hipError_t launch_bgzf_scan(const uint8_t* file, uint64_t buf_base, uint64_t lo,
   (void)buf_base;
   const uint64_t a = lo & ~15ull;
   const uint64_t nc = (hi - a + 15) / 16;  // 16 B per lane and step, 4 steps per iteration
-  hipLaunchKernelGGL(k_bgzf_scan, dim3(grid_for((nc + 3) / 4, 256, 8192)), dim3(256), 0, s, file + a, hi - a, a, lo,
+  hipLaunchKernelGGL(k_bgzf_scan, dim3(grid_for((nc + 3) / 4, 256, HBAM_SCAN_GRID)), dim3(256), 0, s, file + a, hi - a, a, lo,
                      cand, cap, count);
   return hipGetLastError();
 }
@@ -3854,10 +3934,10 @@ hipError_t launch_huff_tables(const uint8_t* file, const BlockInfo* blocks, uint
 }
 // phase A proper; the chunk's tables must be built (launch_huff_tables).
 hipError_t launch_inflate_huff_prebuilt(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                                        uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
+                                        uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout,
                                         const uint8_t* tables, const HuffTableInfo* tinfo, uint32_t round,
                                         uint32_t defer, hipStream_t s) {
-  (void)max_stage;  // every workgroup decides for its own block (k_inflate_huff)
+  // (every workgroup decides for its own block whether it stages it, k_inflate_huff)
   if (nb == 0) return hipSuccess;
   hipLaunchKernelGGL(k_inflate_huff, dim3(nb), dim3(kHuffThreads), 0, s, file, blocks, b0, chunk_ustart, tokens,
                      hout, tables, tinfo, round, defer);

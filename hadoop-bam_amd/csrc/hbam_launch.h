@@ -77,15 +77,9 @@ hipError_t launch_huff_tables(const uint8_t* file, const BlockInfo* blocks, uint
 // (defer: stop a block before its next DEFLATE header, kHuffPending, for
 // the next round; the last round decodes every remaining header inline)
 hipError_t launch_inflate_huff_prebuilt(const uint8_t* file, const BlockInfo* blocks, uint32_t b0, uint32_t nb,
-                                        uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout, uint32_t max_stage,
+                                        uint64_t chunk_ustart, uint32_t* tokens, HuffOut* hout,
                                         const uint8_t* tables, const HuffTableInfo* tinfo, uint32_t round,
                                         uint32_t defer, hipStream_t s);
-// LDS bytes phase A stages for a block: its cdata from the 16 B-aligned start,
-// footer included, plus one 16 B pad (must match k_inflate_huff).
-inline uint32_t huff_stage_bytes(const BlockInfo& b) {
-  const uint64_t abase = (b.coff + 18) & ~15ull;
-  return (uint32_t)(((b.coff + b.csize - abase + 15) >> 4) + 1) * 16u;
-}
 hipError_t launch_inflate_lz77(const BlockInfo* blocks, uint32_t b0, uint32_t nb, uint64_t chunk_ustart,
                                const uint32_t* tokens, const HuffOut* hout, uint8_t* u, hipStream_t s);
 hipError_t launch_chain(const ChainArgs& a, int mode, int stage, hipStream_t s);

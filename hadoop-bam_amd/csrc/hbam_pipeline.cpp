@@ -342,12 +342,13 @@ int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_sta
   const uint32_t cap = (uint32_t)std::min<uint64_t>(len / 1024 + 4096, 0x7fffffffu);
   const uint32_t walk_cap = (uint32_t)std::min<uint64_t>(len / 26 + 16, 0x7fffffffu);
   HIPCHK(cand_.reserve(cap));
-  HIPCHK(flags_.reserve(4));
-  // {0, 0, 0xffffffff, 0} by fill kernels: a small pageable H2D can wait
+  HIPCHK(flags_.reserve(5));
+  // {0, 0, 0xffffffff, 0, 0} by fill kernels: a small pageable H2D can wait
   // behind other contexts' or the drop-in batches' copies on the DMA engines
-  HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags_.p), 0, 4, s));
+  HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags_.p), 0, 5, s));
   HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags_.p + 2), -1, 1, s));
-  // flags_[0] = candidate count, [1] = chain break, [2] = first big ISIZE, [3] = cut tail
+  // flags_[0] = candidate count, [1] = chain break, [2] = first big ISIZE, [3] = cut tail,
+  // [4] = empty blocks
   HIPCHK(launch_bgzf_scan(fbase, base_, lo, hi, cand_.p, cap, flags_.p, s));
   uint32_t count = 0;
   HIPCHK(rb(&count, flags_.p, 4, s));
@@ -370,11 +371,12 @@ int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_sta
       lo = starts[0];
     }
     HIPCHK(launch_bgzf_verify(fbase, lo, hi, sorted_.p, n, dblocks_.p + nprev, flags_.p + 1, partial ? 1u : 0u, s));
-    uint32_t fl[3];
+    uint32_t fl[4];
     uint64_t last = 0;
-    HIPCHK(rb(fl, flags_.p + 1, 12, s));
+    HIPCHK(rb(fl, flags_.p + 1, 16, s));
     HIPCHK(rb(&last, sorted_.p + n - 1, 8, s));
     HIPCHK(rb_sync(s));
+    if (!fl[0] && empty_blocks_ != kEmptyUnknown) empty_blocks_ += fl[3];
     if (fl[0]) serial = true;
     else if (fl[1] != 0xffffffffu) return fail(kErrFormat, "BGZF block with ISIZE > 65536 (unsupported on device)");
     else if (fl[2]) {  // the last candidate's block is cut by hi: next range
@@ -383,6 +385,7 @@ int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_sta
     }
   }
   if (serial) {
+    empty_blocks_ = kEmptyUnknown;  // (the walk does not count them)
     uint32_t out[4];
     HIPCHK(dblocks_.grow(nprev + walk_cap + 1));
     if (starts.empty()) starts.push_back(lo);
@@ -429,10 +432,18 @@ int Pipeline::finish_blocks() {
   HIPCHK(hipMemsetAsync(du_.p + total_u_, 0, kUPad, stream_));
   inflated_.resize(n, 0);
   HIPCHK(hout_.grow(n + 1));
-  // dead positions: [htsjdk] an empty block right after an exhausted one
+  // dead positions: [htsjdk] an empty block right after an exhausted one.
+  // The verify kernel counted the empty blocks: with none, or only the EOF
+  // block at the end, no walk over the block table (1.7 MB for C2, read
+  // while the GPU waits) is needed.
   std::vector<uint64_t> dead;
-  for (uint32_t k = 1; k < n; ++k)
-    if (hblocks_[k].isize == 0 && (dead.empty() || dead.back() != hblocks_[k].ustart)) dead.push_back(hblocks_[k].ustart);
+  if (empty_blocks_ == 1 && n >= 2 && hblocks_[n - 1].isize == 0) {
+    dead.push_back(hblocks_[n - 1].ustart);
+  } else if (empty_blocks_ != 0) {
+    for (uint32_t k = 1; k < n; ++k)
+      if (hblocks_[k].isize == 0 && (dead.empty() || dead.back() != hblocks_[k].ustart))
+        dead.push_back(hblocks_[k].ustart);
+  }
   HIPCHK(dead_.reserve(dead.size() + 1));
   if (!dead.empty())
     HIPCHK(hipMemcpyAsync(dead_.p, dead.data(), dead.size() * 8, hipMemcpyHostToDevice, stream_));
@@ -446,6 +457,7 @@ int Pipeline::locate(bool free_start) {
   if (timing) HIPCHK(hipEventRecord(ev_[0], stream_));
   hblocks_.clear();
   inflated_.clear();
+  empty_blocks_ = 0;
   uint32_t n = 0;
   uint64_t tail = 0;
   int rc = locate_range(base_, base_ + flen_, !at_eof_, free_start, 0, 0, stream_, &n, &tail);
@@ -496,6 +508,7 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
   if (int rc0 = queue_copy(0)) return rc0;
   hblocks_.clear();
   inflated_.clear();
+  empty_blocks_ = 0;
   total_u_ = 0;
   uint64_t lo = base_;
   uint32_t nb = 0, queued = 0;  // blocks located / handed to inflate
@@ -568,15 +581,20 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
   hipStream_t sB = serial ? stream_ : stream_b_, sT = serial ? stream_ : stream_t_;
   struct Chunk { uint32_t b, e; };
   std::vector<Chunk> chunks;
+  // (the GPU is idle here: the common case -- nothing of [b0, b1) inflated
+  // yet -- is planned without a walk over the blocks)
+  const bool fresh = force || std::find(inflated_.begin() + b0, inflated_.begin() + b1, (uint8_t)1) ==
+                                  inflated_.begin() + b1;
   uint32_t b = b0;
   while (b < b1) {
-    if (!force && inflated_[b]) { ++b; continue; }
+    if (!fresh && inflated_[b]) { ++b; continue; }
     // even chunks (a short last chunk would pay a whole wave tail for few blocks)
     const uint32_t left = b1 - b;
     const uint32_t nchunks = (left + kInflateChunkBlocks - 1) / kInflateChunkBlocks;
     const uint32_t per = (left + nchunks - 1) / nchunks;
     uint32_t e = b;
-    while (e < b1 && e - b < per && (force || !inflated_[e])) ++e;
+    if (fresh) e = std::min(b1, b + per);
+    else while (e < b1 && e - b < per && !inflated_[e]) ++e;
     chunks.push_back({b, e});
     b = e;
   }
@@ -614,8 +632,6 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
     const uint32_t cb = chunks[j].b, ce = chunks[j].e;
     const int par = serial ? 0 : (int)(j & 1);
     const uint64_t cu = hblocks_[cb].ustart;
-    uint32_t max_stage = 0;
-    for (uint32_t k = cb; k < ce; ++k) max_stage = std::max(max_stage, huff_stage_bytes(hblocks_[k]));
     if (!serial && j >= 2) {
       HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + par], 0));  // B(j-2) released the token buffer
       HIPCHK(hipStreamWaitEvent(stream_t_, hdone_ev_[par], 0));   // A(j-2) released the table buffer
@@ -632,7 +648,7 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
         HIPCHK(hipStreamWaitEvent(stream_, tab_ev_[par], 0));
       }
       HIPCHK(mark());
-      HIPCHK(launch_inflate_huff_prebuilt(fbase, dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, max_stage,
+      HIPCHK(launch_inflate_huff_prebuilt(fbase, dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p,
                                           tables_[par].p, tinfo_[par].p, r, r + 1 < kInflateRounds ? 1u : 0u,
                                           stream_));
       HIPCHK(mark());
@@ -646,7 +662,7 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
     HIPCHK(launch_inflate_lz77(dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, du_.p, sB));
     HIPCHK(mark());
     if (!serial) HIPCHK(hipEventRecord(sync_ev_[2 + par], stream_b_));
-    for (uint32_t k = cb; k < ce; ++k) inflated_[k] = 1;
+    std::fill(inflated_.begin() + cb, inflated_.begin() + ce, (uint8_t)1);
     ++inflate_launches_;
   }
   if (any && !serial) {  // everything after this call on stream_ sees phase B done

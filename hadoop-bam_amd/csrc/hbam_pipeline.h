@@ -303,6 +303,9 @@ class Pipeline {
   std::vector<BlockInfo> hblocks_;
   uint64_t total_u_ = 0;
   uint32_t ndead_ = 0;
+  // empty blocks among hblocks_ (counted by the verify kernel), or unknown
+  static constexpr uint32_t kEmptyUnknown = 0xffffffffu;
+  uint32_t empty_blocks_ = kEmptyUnknown;
   int32_t n_ref_ = 0;
   int stringency_ = kStrict;
   DevBuf<int32_t> ref_len_;
