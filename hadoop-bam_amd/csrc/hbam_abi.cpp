@@ -130,9 +130,20 @@ int decode_device(BamFile& f, uint64_t vstart, uint64_t vend, int32_t flags, hba
   bool cont = false;
   int rc = HBAM_OK;
   bool first = true;
+  // Windows read from the host ramp up (SpanCursor::ramp_window: 32 MiB,
+  // doubling to the full window), so that decoding starts after the first
+  // small copy instead of a whole 4 GiB window's (C3 from the mapped file);
+  // a span already in HBM decodes in full windows.
+  const uint64_t span_end = std::min<uint64_t>(f.file_size(), vend == ~0ull ? ~0ull : (vend >> 16) + 0x20000);
+  const bool ramp = !f.window_explicit() && !f.resident(vstart >> 16, span_end);
+  uint64_t nwin = 0;
   for (;;) {
     Step step;
-    rc = f.decode_step(c, vend, hbam::kReader, decode, cont, &step);
+    rc = ramp ? f.decode_step(c, vend, hbam::kReader, decode, cont, &step,
+                              hadoop_bam::SpanCursor::ramp_window(f.window_bytes(), nwin),
+                              hadoop_bam::SpanCursor::ramp_window(f.window_bytes(), nwin + 1))
+              : f.decode_step(c, vend, hbam::kReader, decode, cont, &step);
+    ++nwin;
     if (rc != HBAM_OK) {
       *err = f.error();
       break;

@@ -122,6 +122,9 @@ class BamFile {
   uint64_t file_size() const { return src_.size; }
   uint64_t bytes_read() const { return src_.bytes_read; }
   uint64_t window_bytes() const { return window_bytes_; }
+  bool window_explicit() const { return window_explicit_; }
+  // file bytes [lo, hi) already in HBM (prefetch, or a device copy)
+  bool resident(uint64_t lo, uint64_t hi) const { return src_.dev.p && lo >= src_.dev_lo && hi <= src_.dev_hi; }
   void set_window_bytes(uint64_t w) { window_bytes_ = w < (1ull << 16) ? (1ull << 16) : w; }
 
   // [htsjdk] BAMFileReader.readHeader results
@@ -358,6 +361,9 @@ int fetch_span(hbam::Pipeline& p, const SpanDev& s, uint64_t k, uint64_t m, Host
 // the split in one owning HostBatch (several windows appended).
 class SpanCursor {
  public:
+  // window id of a split read from the host: 32 MiB, doubling up to `full`
+  // (HBAM_DROPIN_RAMP="first MiB,growth"), so decoding starts after a small copy
+  static uint64_t ramp_window(uint64_t full, uint64_t id);
   SpanCursor() = default;
   SpanCursor(const SpanCursor&) = delete;
   SpanCursor& operator=(const SpanCursor&) = delete;
@@ -408,7 +414,6 @@ class SpanCursor {
   };
   int ensure_streams(hbam::Pipeline& p, std::string* err);
   int decode_window(BamFile& f, Carry from, bool cont, uint64_t m, Window* w, std::string* err);
-  static uint64_t ramp_window(uint64_t full, uint64_t id);
   int issue(const Window& w, uint64_t k, uint64_t m, Slot* s, std::string* err);
   // m capped so that the batch's rest bytes fit a Java direct buffer (an int
   // capacity and int positions: GpuBAMRecordReader.recordAt): the largest

@@ -3462,7 +3462,7 @@ __device__ __forceinline__ void check_listed_h(const ChainEnv& E, uint64_t q, ui
 //   bad[0]   min over blocks that stop early or fail of (i << 40 | base[i] +
 //            count): the first such block and the records up to its stop
 //   flags[0] the first failing block (its status is the span's when it is
-//            the first stop), flags[1] the last block with records + 1
+//            the first stop)
 //   cnt[] / err[] per block, need = the bytes a stopped record needs past
 //            the inflated range.
 constexpr int kBadShift = 40;
@@ -3554,8 +3554,20 @@ __global__ __launch_bounds__(64, 6) void k_rec_check_out(ChainEnv E, const uint6
     if (count < listed || st != kOk)
       atomicMin(bad, ((unsigned long long)i << kBadShift) | (unsigned long long)(o0 + count));
     if (st != kOk) atomicMin(&flags[0], i);
-    if (count) atomicMax(&flags[1], i + 1);
+    // (no per-block atomic on a shared word here: 52 K of them on one address
+    // serialize across the XCDs; k_records_after answers for the rare stop)
   }
+}
+
+// *flag = 1 when a block after block k has records (a span cut at an early
+// stop dropped them: a diagnostic, hbam_pipeline_counters)
+__global__ void k_records_after(const uint32_t* __restrict__ cnt, uint32_t nb, uint32_t k, uint32_t* __restrict__ flag) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > k && i < nb && cnt[i]) *flag = 1u;
+}
+hipError_t launch_records_after(const uint32_t* cnt, uint32_t nb, uint32_t k, uint32_t* flag, hipStream_t s) {
+  hipLaunchKernelGGL(k_records_after, dim3((nb + 255) / 256), dim3(256), 0, s, cnt, nb, k, flag);
+  return hipGetLastError();
 }
 
 // first block (index) whose status is non-zero -> *first (atomicMin), status -> code[]

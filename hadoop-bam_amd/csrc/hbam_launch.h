@@ -35,7 +35,7 @@ struct ChainArgs {
   uint32_t* counters;   // [0] hard link violations, [1] blocks to re-walk, [2] list overflow
   // fused check + output (launch_rec_check_out)
   uint64_t* fuse_bad;    // = ~0: min (i << kFusedBadShift | records up to i's stop) over blocks that stop early
-  uint32_t* fuse_flags;  // [0] first failing block = ~0, [1] last block with records + 1 = 0
+  uint32_t* fuse_flags;  // [0] first failing block = ~0
 };
 constexpr uint32_t kListCap = 2048;              // >= 65536 / 36 + 2: every reader-mode record start
 constexpr uint64_t kForceEmpty = ~0ull - 1;      // force[]: the block holds no record start
@@ -97,6 +97,7 @@ hipError_t link_scan_bytes(uint32_t nb, size_t* bytes);
 hipError_t launch_rec_decode(const uint8_t* u, const uint64_t* rec_pos, uint64_t n, const Columns& col,
                              hipStream_t s);
 hipError_t launch_first_error_hout(const HuffOut* hout, uint32_t b0, uint32_t nb, uint32_t* first, hipStream_t s);
+hipError_t launch_records_after(const uint32_t* cnt, uint32_t nb, uint32_t k, uint32_t* flag, hipStream_t s);
 hipError_t launch_first_error_i32(const int32_t* err, uint32_t nb, uint32_t* first, hipStream_t s);
 hipError_t launch_truncate_counts(uint32_t* cnt, uint32_t nb, const uint32_t* cut, hipStream_t s);
 // .splitting-bai entries of records with global ordinals o0 .. o0+n-1

@@ -817,6 +817,7 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
   uint32_t fused_first = 0xffffffffu;
   for (int it = 0;; ++it) {
     if (it >= kMaxChainIters) return fail(kErrState, "record chain did not converge");
+    after_stop_pending_ = false;  // (only the last iteration's stop counts)
     int rc = inflate(k0, inf_end);
     if (timing) {
       infl_ms += times.inflate;
@@ -962,7 +963,6 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
         if (rc != kOk) return rc;
       }
       HIPCHK(hipMemsetAsync(fuse_.p, 0xff, 12, stream_));  // early-stop key, first failing block: none
-      HIPCHK(hipMemsetAsync(fuse_.p + 3, 0, 4, stream_));   // last block with records + 1: none
       a.fuse_bad = reinterpret_cast<uint64_t*>(fuse_.p);
       a.fuse_flags = fuse_.p + 2;
       a.rec_pos = rec_pos_.p;
@@ -973,7 +973,7 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
       uint32_t fl[2] = {0, 0};
       HIPCHK(rb(&need, need_.p, 8, stream_));
       HIPCHK(rb(&bad, fuse_.p, 8, stream_));
-      HIPCHK(rb(fl, fuse_.p + 2, 8, stream_));
+      HIPCHK(rb(fl, fuse_.p + 2, 4, stream_));
       HIPCHK(rb_sync(stream_));
       fused_first = fl[0];
       if (bad == ~0ull) {
@@ -986,7 +986,12 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
         const uint64_t k = bad >> kFusedBadShift;
         fused_total = bad & ((1ull << kFusedBadShift) - 1);
         if (fl[0] != k) fused_first = 0xffffffffu;
-        if (fl[1] > k + 1) ++records_after_stop_;
+        // (diagnostic) records listed after the stop, which it drops: read
+        // with the span's last readback, no round trip of its own
+        HIPCHK(hipMemsetAsync(fuse_.p + 3, 0, 4, stream_));
+        HIPCHK(launch_records_after(cnt_.p, nb, (uint32_t)k, fuse_.p + 3, stream_));
+        HIPCHK(rb(&after_stop_flag_, fuse_.p + 3, 4, stream_));
+        after_stop_pending_ = true;
       }
     } else {
       HIPCHK(launch_chain(a, mode, kStageCount, stream_));  // count + validate by walking
@@ -1076,6 +1081,9 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
   HIPCHK(rb(&out->next_pos, scalars_.p, 8, stream_));
   if (timing) HIPCHK(hipEventRecord(ev_[2], stream_));
   HIPCHK(rb_sync(stream_));
+  if (after_stop_pending_ && after_stop_flag_) ++records_after_stop_;
+  after_stop_pending_ = false;
+  after_stop_flag_ = 0;
   if (timing) {
     float all = 0, dcd = 0;
     (void)hipEventElapsedTime(&all, ev_[0], ev_[1]);

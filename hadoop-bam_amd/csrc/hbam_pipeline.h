@@ -314,6 +314,8 @@ class Pipeline {
   uint64_t link_rewalks_ = 0;      // re-walk rounds of the parallel link
   uint64_t record_fallbacks_ = 0;  // spans whose lists overflowed: records counted and emitted by walks
   uint64_t records_after_stop_ = 0;  // spans that stopped early with records listed in later blocks (dropped)
+  uint32_t after_stop_flag_ = 0;     // (read back with a span's last readback)
+  bool after_stop_pending_ = false;
   uint64_t inflate_launches_ = 0;  // phase A/B launch pairs so far
 
   DevBuf<uint8_t> du_;

@@ -41,9 +41,11 @@ for s in $STEPS; do
       # after hbam_gpu_run_streamed (the slowed next context)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace \
         --output-format csv -d $OUT/qtrace -- python3 $R/scripts/dropin_probe2.py 10000000 --torch \
-        --smi --steps none,run_streamed,none,none > $OUT/qtrace.log 2>&1) \
+        --steps none,run_streamed,none,none > $OUT/qtrace.log 2>&1) \
         || { echo "qtrace failed"; tail -30 $OUT/qtrace.log; exit 4; }
-      grep -E "^(mapped|resident|SMI)" $OUT/qtrace.log | cut -c1-300 ;;
+      grep -E "^(mapped|resident)" $OUT/qtrace.log | cut -c1-300
+      python3 scripts/qtrace_summary.py $OUT > $OUT/qtrace_summary.json 2>&1 || true
+      python3 -c "import json; d=json.load(open('$OUT/qtrace_summary.json')); [print(k, json.dumps(v.get('overlap'))) for k, v in d.items() if isinstance(v, dict) and 'overlap' in v]" || true ;;
     dropin_ab)
       # the drop-in 1 M-batch loop under window ramps (HBAM_DROPIN_RAMP="first MiB,growth"; 0 = none)
       for r in ${RAMPS:-0 32,2}; do
@@ -83,6 +85,15 @@ for s in $STEPS; do
         $(ls hadoop-bam_amd/lib/variants/*.so 2>/dev/null) > $OUT/variants.log 2>&1 \
         || { echo "variants failed"; tail -30 $OUT/variants.log; exit 5; }
       cat $OUT/variants.log ;;
+    engines)
+      # HIP log at level 4 (all categories; the copy lines name their engine): which DMA engine each copy of the drop-in loop
+      # took, before and after hbam_gpu_run_streamed (the slowed next context)
+      AMD_LOG_LEVEL=4 AMD_LOG_MASK=0x7fffffff timeout -k 10 400 python -u scripts/dropin_probe2.py 10000000 --torch \
+        --steps none,run_streamed,none > $OUT/engines.log 2>&1 || { echo "engines probe failed"; tail -20 $OUT/engines.log; exit 12; }
+      python3 scripts/engine_summary.py $OUT/engines.log > $OUT/engines.txt 2>&1
+      grep -i "copy" $OUT/engines.log | head -c 2000000 > $OUT/engines_copylines.txt || true
+      gzip -f $OUT/engines.log
+      cat $OUT/engines.txt ;;
     gaps)
       # kernel trace of production-order passes (no events): overlap and idle time of the last pass
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/gaps -o run \

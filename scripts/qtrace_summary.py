@@ -71,7 +71,41 @@ def main():
                 c["ns"] += int(r["End_Timestamp"]) - s
                 c["bytes"] += int(col(r, "Bytes", "Size", "Copy_Bytes") or 0)
                 c["streams"][col(r, "Stream_Id", "Stream_ID") or "?"] += 1
+        # the copies' own timeline: time each direction is in flight, time both
+        # are, and each direction's rate alone vs beside the other
+        iv = collections.defaultdict(list)
+        for r in copy:
+            s0 = int(r["Start_Timestamp"])
+            if b <= s0 <= e:
+                iv[col(r, "Direction", "Kind") or "?"].append((s0, int(r["End_Timestamp"]),
+                                                               int(col(r, "Bytes", "Size", "Copy_Bytes") or 0)))
+        out_ov = {}
+        dirs = sorted(iv)
+        if len(dirs) >= 2:
+            ev = sorted([(s0, 1, d) for d in dirs for s0, _, _ in iv[d]] + [(e0, -1, d) for d in dirs for _, e0, _ in iv[d]])
+            run = collections.Counter()
+            last = ev[0][0] if ev else 0
+            acc = collections.Counter()
+            for t, dd, d in ev:
+                act = tuple(x for x in dirs if run[x] > 0)
+                acc[act] += t - last
+                run[d] += dd
+                last = t
+            out_ov["ms_active"] = {"+".join(k) if k else "none": round(v / 1e6, 2) for k, v in acc.items()}
+            for d in dirs:
+                others = [x for o in dirs if o != d for x in iv[o]]
+                alone = [0, 0]
+                beside = [0, 0]
+                for s0, e0, nb in iv[d]:
+                    hit = any(os_ < e0 and oe > s0 for os_, oe, _ in others)
+                    tgt = beside if hit else alone
+                    tgt[0] += nb
+                    tgt[1] += e0 - s0
+                out_ov[d] = {"GBps_alone": round(alone[0] / alone[1], 2) if alone[1] else None,
+                             "GBps_beside_other": round(beside[0] / beside[1], 2) if beside[1] else None,
+                             "GB_alone": round(alone[0] / 1e9, 3), "GB_beside": round(beside[0] / 1e9, 3)}
         out[rep] = {
+            "overlap": out_ov,
             "seconds": round((e - b) / 1e9, 4),
             "kernels": {n: {"n": v["n"], "mean_us": round(v["ns"] / v["n"] / 1e3, 1), "queues": dict(v["queues"]),
                             "streams": dict(v["streams"])} for n, v in sorted(ks.items(), key=lambda x: -x[1]["ns"])},
