@@ -1889,6 +1889,10 @@ constexpr int kLzThreads = 1024;
 constexpr int kLzWaves = kLzThreads / 64;
 constexpr uint32_t kMapMax = 65280;
 constexpr uint32_t kLitTag = 0xFF00u;
+// map entries: 128 KiB, so that the 16 waves' 8 rows of 64 eight-entry chunks
+// (step 3) cover it exactly and need no bounds (o0 + ISIZE <= 65295)
+constexpr uint32_t kMapEntries = 65536;
+static_assert(kMapEntries == kLzWaves * 8 * 64 * 8 && kMapMax + 15 < kMapEntries, "phase-B map geometry");
 constexpr int kLzRing = 4;  // phase-B fill: 64-token groups loaded ahead (4 vs 8 measured equal)
 constexpr int kLzTokGroups = 32;  // token groups a wave keeps in registers (32 K tokens per block)
 #ifndef HBAM_LZ_CHASE
@@ -1969,7 +1973,7 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
                                                              const HuffOut* __restrict__ hout,
                                                              uint8_t* __restrict__ u) {
   // map index = o0 + position, so 16-byte output segments read 32 B-aligned LDS
-  __shared__ __attribute__((aligned(16))) uint16_t map[kMapMax + 32];
+  __shared__ __attribute__((aligned(16))) uint16_t map[kMapEntries];
   __shared__ uint32_t scratch[kLzWaves];
   const BlockInfo blk = blocks[b0 + blockIdx.x];
   const HuffOut ho = hout[b0 + blockIdx.x];
@@ -2001,7 +2005,7 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
   }
 
   // 0. empty map: 0 marks a position no token writes (inside a match)
-  for (uint32_t c = tid; c < (kMapMax + 32) / 8; c += kLzThreads)
+  for (uint32_t c = tid; c < kMapEntries / 8; c += kLzThreads)
     reinterpret_cast<uint4*>(map)[c] = make_uint4(0u, 0u, 0u, 0u);
 
   // 1. wave w expands tokens [w*TW, (w+1)*TW); its output range starts at
@@ -2059,11 +2063,28 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
       }
     }
   };
+  // one token's entries, branch-free selects and two predicated stores
+  auto head_at = [&](uint32_t t, uint32_t len, uint32_t pos) {
+    const bool mt = (t >> 31) != 0;
+    const uint32_t e0 = mt ? ((t >> 16) & 0x7fffu) + 1u : (kLitTag | (t & 0xffu));  // dist <= pos: checked in phase A
+    if ((len != 0) & (pos < whi)) m[pos] = (uint16_t)e0;
+    if ((len == 2) & !mt & (pos + 1 < whi)) m[pos + 1] = (uint16_t)(kLitTag | ((t >> 8) & 0xffu));
+  };
   if (inreg) {
+    // two groups of 64 tokens per scan: their lengths packed in 16-bit
+    // halves (a group's bytes <= 64 x 258 < 2^16)
 #pragma unroll
-    for (int k = 0; k < kLzTokGroups; ++k) {
-      if (tw0 + 64u * k >= tw1) break;  // wave-uniform
-      head(tr[k]);
+    for (int j = 0; j < kLzTokGroups / 2; ++j) {
+      if (tw0 + 128u * j >= tw1) break;  // wave-uniform
+      const uint32_t t0 = tr[2 * j], t1 = tr[2 * j + 1];
+      const uint32_t l0 = tok_len(t0), l1 = tok_len(t1);
+      const uint32_t incl = wave_incl_scan_dpp(l0 | (l1 << 16));
+      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      const uint32_t p0 = P + (incl & 0xffffu) - l0;
+      const uint32_t p1 = P + (tot & 0xffffu) + (incl >> 16) - l1;
+      P += (tot & 0xffffu) + (tot >> 16);
+      head_at(t0, l0, p0);
+      head_at(t1, l1, p1);
     }
   } else {
     uint32_t ring[kLzRing];  // tokens of the next kLzRing groups (L2 hits after step 1)
@@ -2090,13 +2111,12 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
   //    waves (LDS) find the nearest non-zero entry before each chunk.
   {
     constexpr uint32_t kRowChunks = 64, kWaveChunks = 8 * kRowChunks;
-    const uint32_t nchunk = (o0 + isize + 7) >> 3;
     uint4* mc = reinterpret_cast<uint4*>(map);
     uint4 rows[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const uint32_t c = wid * kWaveChunks + r * kRowChunks + lane;
-      rows[r] = c < nchunk ? mc[c] : make_uint4(0u, 0u, 0u, 0u);
+      rows[r] = mc[c];  // (every chunk: entries past the block are zero or unused)
     }
     uint32_t key[8], kmax = 0;
 #pragma unroll
@@ -2124,21 +2144,19 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
       uint32_t cur = max(carry, excl) & 0xffffu;
       carry = max(carry, (uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
       const uint32_t c = wid * kWaveChunks + r * kRowChunks + lane;
-      if (c < nchunk) {
-        // position of entry 0 of this chunk, relative to the block (index - o0)
-        const uint32_t q0 = 8u * c - o0;
-        uint32_t w4[4] = {rows[r].x, rows[r].y, rows[r].z, rows[r].w};
+      // position of entry 0 of this chunk, relative to the block (index - o0)
+      const uint32_t q0 = 8u * c - o0;
+      uint32_t w4[4] = {rows[r].x, rows[r].y, rows[r].z, rows[r].w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          uint32_t lo = w4[j] & 0xffffu, hi = w4[j] >> 16;
-          cur = lo ? lo : cur;
-          lo = (cur != 0 && cur < kLitTag) ? (q0 + 2u * j - cur) & 0xffffu : lo;
-          cur = hi ? hi : cur;
-          hi = (cur != 0 && cur < kLitTag) ? (q0 + 2u * j + 1u - cur) & 0xffffu : hi;
-          w4[j] = lo | (hi << 16);
-        }
-        mc[c] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      for (int j = 0; j < 4; ++j) {
+        uint32_t lo = w4[j] & 0xffffu, hi = w4[j] >> 16;
+        cur = lo ? lo : cur;
+        lo = (cur != 0 && cur < kLitTag) ? (q0 + 2u * j - cur) & 0xffffu : lo;
+        cur = hi ? hi : cur;
+        hi = (cur != 0 && cur < kLitTag) ? (q0 + 2u * j + 1u - cur) & 0xffffu : hi;
+        w4[j] = lo | (hi << 16);
       }
+      mc[c] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
     }
   }
   __syncthreads();
