@@ -2004,15 +2004,16 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
     return;
   }
 
-  // 0. empty map: 0 marks a position no token writes (inside a match)
-  for (uint32_t c = tid; c < kMapEntries / 8; c += kLzThreads)
-    reinterpret_cast<uint4*>(map)[c] = make_uint4(0u, 0u, 0u, 0u);
-
   // 1. wave w expands tokens [w*TW, (w+1)*TW); its output range starts at
   //    the byte total of the waves before it.  Up to kLzTokGroups groups of
   //    64 tokens stay in registers from this load to step 2 (all loads in
   //    flight at once); a wave with more re-reads them (L2) through a ring.
   const uint32_t wid = tid >> 6, lane = tid & 63;
+  // 0. empty map: 0 marks a position no token writes (inside a match)
+  auto zero_map = [&]() {
+    for (uint32_t c = tid; c < kMapEntries / 8; c += kLzThreads)
+      reinterpret_cast<uint4*>(map)[c] = make_uint4(0u, 0u, 0u, 0u);
+  };
   const uint32_t TW = (ntok + kLzWaves - 1) / kLzWaves;
   const uint32_t tw0 = min(wid * TW, ntok), tw1 = min(tw0 + TW, ntok);
   const bool inreg = TW <= 64u * kLzTokGroups;  // uniform over the workgroup
@@ -2024,9 +2025,11 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
       const uint32_t i = tw0 + lane + 64u * k;
       tr[k] = i < tw1 ? tk[i] : 0u;  // 0 = a literal token of length 0
     }
+    zero_map();  // (while the loads are in flight)
 #pragma unroll
     for (int k = 0; k < kLzTokGroups; ++k) wsum += tok_len(tr[k]);
   } else {
+    zero_map();
     for (uint32_t i0 = tw0 + lane; i0 < tw1 + lane; i0 += 8 * 64) {  // 8 loads in flight
       uint32_t tv[8];
 #pragma unroll
@@ -2149,12 +2152,15 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
       uint32_t w4[4] = {rows[r].x, rows[r].y, rows[r].z, rows[r].w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        uint32_t lo = w4[j] & 0xffffu, hi = w4[j] >> 16;
+        // inside the block a 0 entry follows its match's head, so every
+        // entry becomes cur (a literal, or 0 before the block) or, when cur
+        // is a distance, its source position
+        const uint32_t lo = w4[j] & 0xffffu, hi = w4[j] >> 16;
         cur = lo ? lo : cur;
-        lo = (cur != 0 && cur < kLitTag) ? (q0 + 2u * j - cur) & 0xffffu : lo;
+        const uint32_t olo = cur - 1u < kLitTag - 1u ? q0 + 2u * j - cur : cur;
         cur = hi ? hi : cur;
-        hi = (cur != 0 && cur < kLitTag) ? (q0 + 2u * j + 1u - cur) & 0xffffu : hi;
-        w4[j] = lo | (hi << 16);
+        const uint32_t ohi = cur - 1u < kLitTag - 1u ? q0 + 2u * j + 1u - cur : cur;
+        w4[j] = (olo & 0xffffu) | (ohi << 16);
       }
       mc[c] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
     }
@@ -2166,8 +2172,8 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
   //    thread chases kLzChase positions 1024 apart at once (their loads
   //    overlap).  Any visiting order is correct: entries always point to
   //    smaller positions and a chase ends at a literal, resolved or not.
-  // Branch-free steps: a resolved lane re-reads its own entry and keeps its
-  // value (a select, not an exec-masked read).
+  // Branch-free steps: a resolved lane re-reads its own entry (no select,
+  // no exec-masked read).
   for (uint32_t q = tid; q < isize; q += kLzChase * kLzThreads) {
     uint32_t v[kLzChase], at[kLzChase];
 #pragma unroll
@@ -2180,15 +2186,12 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
 #pragma unroll
       for (int k = 0; k < kLzChase; ++k) more |= v[k] < kLitTag;
       if (!__builtin_amdgcn_ballot_w64(more)) break;
-      uint32_t n[kLzChase];
-      bool un[kLzChase];
+      // min(v, at): an unresolved v is a smaller position than at; a
+      // resolved lane (v >= kLitTag > at) re-reads its own entry, which
+      // holds v (the literal it first read, or its last store below: only
+      // this lane writes m[at]) -- so the value read is the new v either way
 #pragma unroll
-      for (int k = 0; k < kLzChase; ++k) {
-        un[k] = v[k] < kLitTag;
-        n[k] = m[un[k] ? v[k] : at[k]];
-      }
-#pragma unroll
-      for (int k = 0; k < kLzChase; ++k) v[k] = un[k] ? n[k] : v[k];
+      for (int k = 0; k < kLzChase; ++k) v[k] = m[min(v[k], at[k])];
       // pointer jumping: every step stores how far the chase got, so a lane
       // whose chain runs through this position skips the hops already made
       // (a run of dist-1 matches resolves in ~log2(len) steps instead of
