@@ -347,6 +347,10 @@ enum : uint32_t { K_LIT = 0, K_LEN = 1, K_EOB = 2, K_LONG = 3, K_BAD = 4, K_SLOW
 constexpr uint32_t kBadEntry = K_BAD << 26;
 constexpr uint32_t kLongTag = 0xF0000000u;  // build-time mark: kLongTag | (max len - root)
 constexpr uint32_t kKindLit = 1u << 26;  // e < kKindLit  <=>  literal entry
+// a root entry that points to a sub-table (kind K_LONG) also carries bit 31,
+// so the decode loop tests it with one signed compare
+constexpr uint32_t kLongEntry = 0x80000000u | (K_LONG << 26);
+__device__ __forceinline__ bool is_long(uint32_t e) { return (int32_t)e < 0; }
 
 __constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
                                       31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -519,7 +523,7 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
       if (lane >= (uint32_t)d) inc += v;
     }
     const uint32_t base = used + inc - sz;
-    if (mk) tab[i] = base + sz <= (uint32_t)subcap ? ((K_LONG << 26) | (bits << 16) | base) : (K_SLOW << 26);
+    if (mk) tab[i] = base + sz <= (uint32_t)subcap ? (kLongEntry | (bits << 16) | base) : (K_SLOW << 26);
     used += (uint32_t)__shfl(inc, 63, 64);
   }
   const uint32_t nused = min(used, (uint32_t)subcap);
@@ -530,7 +534,7 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
     if ((int)l > root) {
       const uint32_t rev = L.rev_of[s];
       const uint32_t e = tab[rev & rmask];
-      if ((e >> 26) == K_LONG) {
+      if (is_long(e)) {
         const uint32_t b = e & 0xffffu, sb = (e >> 16) & 15u;
         const uint32_t ent = make_entry(mode, (uint32_t)s, l);
         for (uint32_t k = rev >> root; k < (1u << sb); k += 1u << (l - root)) sub[b + k] = ent;
@@ -672,7 +676,7 @@ __device__ __attribute__((noinline)) int build_table_r(HuffLds& L, const uint8_t
       const uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)t, j) & 15u;
       const uint32_t sz = 1u << bits;
       if ((int)lane == j)
-        tab[64 * c + lane] = used + sz <= (uint32_t)subcap ? ((K_LONG << 26) | (bits << 16) | used) : (K_SLOW << 26);
+        tab[64 * c + lane] = used + sz <= (uint32_t)subcap ? (kLongEntry | (bits << 16) | used) : (K_SLOW << 26);
       used += sz;
     }
   }
@@ -687,7 +691,7 @@ __device__ __attribute__((noinline)) int build_table_r(HuffLds& L, const uint8_t
       const int s = 64 * g + (int)lane;
       const uint32_t rev = revv[g];
       const uint32_t e = tab[rev & rmask];
-      if ((e >> 26) == K_LONG) {
+      if (is_long(e)) {
         const uint32_t b = e & 0xffffu, sb = (e >> 16) & 15u;
         const uint32_t ent = make_entry(mode, (uint32_t)s, l);
         for (uint32_t k = rev >> root; k < (1u << sb); k += 1u << (l - root)) sub[b + k] = ent;
@@ -746,11 +750,10 @@ template <bool UNIFORM>
 __device__ __forceinline__ uint32_t lit_lookup(const HuffLds& L, uint64_t b) {
   uint32_t e = L.lit[(uint32_t)b & ((1u << kLitRoot) - 1)];
   if (UNIFORM) e = rfl(e);
-  const uint32_t k = e >> 26;
-  if (k == K_LONG) {
+  if (is_long(e)) {
     e = L.litsub[(e & 0xffffu) + ((uint32_t)(b >> kLitRoot) & ((1u << ((e >> 16) & 15u)) - 1))];
     if (UNIFORM) e = rfl(e);
-  } else if (k == K_SLOW) {
+  } else if ((e >> 26) == K_SLOW) {
     e = canon_decode<UNIFORM>(b, L.cnt_lit, L.sort_lit, 0);
   }
   return e;
@@ -759,11 +762,10 @@ template <bool UNIFORM>
 __device__ __forceinline__ uint32_t dist_lookup(const HuffLds& L, uint64_t b) {
   uint32_t d = L.dist[(uint32_t)b & ((1u << kDistRoot) - 1)];
   if (UNIFORM) d = rfl(d);
-  const uint32_t k = d >> 26;
-  if (k == K_LONG) {
+  if (is_long(d)) {
     d = L.distsub[(d & 0xffffu) + ((uint32_t)(b >> kDistRoot) & ((1u << ((d >> 16) & 15u)) - 1))];
     if (UNIFORM) d = rfl(d);
-  } else if (k == K_SLOW) {
+  } else if ((d >> 26) == K_SLOW) {
     d = canon_decode<UNIFORM>(b, L.cnt_dist, L.sort_dist, 1);
   }
   return d;
@@ -898,7 +900,7 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
       const uint32_t hi = __builtin_amdgcn_alignbit(w2, w1, sh);
       uint32_t e = L.lit[lo & ((1u << kLitRoot) - 1)];
       {  // a code longer than the root (rare): every lane reads, long ones keep it
-        const bool lg = (e >> 26) == K_LONG;
+        const bool lg = is_long(e);
         if (__builtin_amdgcn_ballot_w64(lg)) {
           const uint32_t es = L.litsub[min((e & 0xffffu) + __builtin_amdgcn_ubfe(lo, kLitRoot, (e >> 16) & 15u),
                                            (uint32_t)kLitSubCap - 1)];  // in bounds for the lanes that drop it
@@ -915,7 +917,7 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
       const uint32_t b2 = __builtin_amdgcn_alignbit(hi, lo, c1);
       uint32_t d = L.dist[b2 & ((1u << kDistRoot) - 1)];
       {
-        const bool lg = (d >> 26) == K_LONG;
+        const bool lg = is_long(d);
         if (__builtin_amdgcn_ballot_w64(lg)) {
           const uint32_t ds = L.distsub[min((d & 0xffffu) + __builtin_amdgcn_ubfe(b2, kDistRoot, (d >> 16) & 15u),
                                             (uint32_t)kDistSubCap - 1)];
@@ -925,11 +927,12 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
       const uint32_t dn = (d >> 16) & 31, dx = (d >> 21) & 15;
       const uint32_t dist = (d & 0x7fff) + __builtin_amdgcn_ubfe(b2, dn, dx);
       // not taken here (the slow path decodes that symbol): an EOB / invalid /
-      // canonical-decode entry (e >= 2 << 26), an invalid distance code for a
-      // length (d >= 1 << 26), (EMIT) a distance before the block start
-      uint32_t bad = (e >> 27) | (isl & (d >> 26));
-      if (EMIT) bad |= isl & ((out0 + nb - dist) >> 31);
-      const bool upd = act & (bad == 0);
+      // canonical-decode entry (e >= 2 << 26), an invalid or canonical-decode
+      // distance entry for a length (d >= 1 << 26: kinds K_BAD and K_SLOW),
+      // (EMIT) a distance before the block start
+      bool bad = (e >= (2u << 26)) | ((isl != 0) & (d >= kKindLit));
+      if (EMIT) bad |= (isl != 0) & (out0 + nb < dist);
+      const bool upd = act & !bad;
       const uint32_t tm = 0x80000000u | ((dist - 1) << 16) | len, tl = e & 0x0300ffffu;
       const uint32_t t = tl ^ ((tm ^ tl) & (0u - isl));
       const uint32_t npos = pos + c1 + ((dn + dx) & (0u - isl));

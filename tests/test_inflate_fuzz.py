@@ -97,3 +97,69 @@ def test_isize_exactly_short_by_one_symbol():
     got_rc, got = _status_and_bytes_hbam(bad)
     assert got_rc == want_rc == hbam.OK
     assert got == want
+
+
+def _fixed_block_with_distance_code(dcode, nlit=400):
+    """One BGZF block: a fixed-Huffman DEFLATE block of nlit literals, a
+    length-3 match with distance code dcode (30 and 31 are invalid in
+    DEFLATE), nlit more literals and the end-of-block code.  The match lies
+    thousands of bits before the end, in the decoder's fast region."""
+    import zlib
+    bits, nbits = 0, 0
+
+    def put(v, n):  # n bits, LSB first
+        nonlocal bits, nbits
+        bits |= v << nbits
+        nbits += n
+
+    def put_code(c, n):  # a Huffman code, MSB first
+        put(int(format(c, "0%db" % n)[::-1], 2), n)
+
+    def lit(v):
+        if v < 144:
+            put_code(0x30 + v, 8)
+        else:
+            put_code(0x190 + v - 144, 9)
+
+    rng = np.random.default_rng(dcode)
+    body = bytes(rng.integers(65, 91, nlit, dtype=np.uint8))
+    put(1, 1)  # BFINAL
+    put(1, 2)  # fixed Huffman
+    for b in body:
+        lit(b)
+    put_code(1, 7)  # length code 257: length 3
+    put_code(dcode, 5)  # distance code, 5 bits (no extra bits for 0-3; 30/31 invalid)
+    if dcode >= 4:
+        put(0, (dcode - 2) // 2)
+    for b in body:
+        lit(b)
+    put_code(0, 7)  # end of block
+    cdata = bits.to_bytes((nbits + 7) // 8, "little")
+    out = body + (body[-4:-1] if dcode == 3 else b"...") + body  # (only the length matters for ISIZE)
+    isize = len(out)
+    hdr = bytes([31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0]) + struct.pack("<H", len(cdata) + 25)
+    blk = hdr + cdata + struct.pack("<II", zlib.crc32(out) & 0xffffffff, isize)
+    eof = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+    return blk + eof
+
+
+@pytest.mark.parametrize("dcode", [30, 31])
+def test_invalid_distance_code_in_fast_region(dcode):
+    """zlib rejects distance codes 30 and 31 ("invalid distance code" ->
+    E_IO); the GPU decoder must too, also when the code is decoded by the
+    branch-free fast path (the kind of a K_BAD distance entry has bit 0
+    clear, which the fast path's test once missed)."""
+    data = _fixed_block_with_distance_code(dcode)
+    want_rc, _ = _status_and_bytes_oracle(data)
+    got_rc, _ = _status_and_bytes_hbam(data)
+    assert want_rc == hbam.E_IO
+    assert got_rc == want_rc
+
+
+def test_valid_distance_code_fixture_decodes():
+    """The same construction with a valid distance code decodes to zlib's bytes."""
+    data = _fixed_block_with_distance_code(3)
+    want_rc, want = _status_and_bytes_oracle(data)
+    got_rc, got = _status_and_bytes_hbam(data)
+    assert want_rc == got_rc
+    assert got == want
