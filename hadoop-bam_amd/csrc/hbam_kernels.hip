@@ -2155,14 +2155,15 @@ __global__ __launch_bounds__(kLzThreads) void k_inflate_lz77(const BlockInfo* __
       uint32_t w4[4] = {rows[r].x, rows[r].y, rows[r].z, rows[r].w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        // inside the block a 0 entry follows its match's head, so every
-        // entry becomes cur (a literal, or 0 before the block) or, when cur
-        // is a distance, its source position
+        // inside the block a 0 entry follows its match's head, so a literal
+        // stays and every other entry (a head's distance, or 0 in its body)
+        // becomes q - cur, cur = the last non-zero entry (past the block the
+        // values are unused)
         const uint32_t lo = w4[j] & 0xffffu, hi = w4[j] >> 16;
         cur = lo ? lo : cur;
-        const uint32_t olo = cur - 1u < kLitTag - 1u ? q0 + 2u * j - cur : cur;
+        const uint32_t olo = lo < kLitTag ? q0 + 2u * j - cur : lo;
         cur = hi ? hi : cur;
-        const uint32_t ohi = cur - 1u < kLitTag - 1u ? q0 + 2u * j + 1u - cur : cur;
+        const uint32_t ohi = hi < kLitTag ? q0 + 2u * j + 1u - cur : hi;
         w4[j] = (olo & 0xffffu) | (ohi << 16);
       }
       mc[c] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
