@@ -54,7 +54,13 @@ struct HuffOut {
 // stops there (kHuffPending); the next round's k_huff_tables parses that
 // header at high occupancy and the decode resumes with the tables prebuilt.
 constexpr int32_t kHuffPending = -2;
-constexpr uint32_t kInflateRounds = 4;  // zlib: <= 4 DEFLATE blocks of 16383 symbols per 64 KiB BGZF block
+#ifndef HBAM_INFLATE_ROUNDS
+#define HBAM_INFLATE_ROUNDS 2
+#endif
+// zlib writes <= 4 DEFLATE blocks of 16383 symbols per 64 KiB BGZF block and
+// htslib/bgzip data nearly always 2: rounds 3-4 cost ~47 us of near-empty
+// launches per chunk, so a third or fourth header is parsed inline in round 1
+constexpr uint32_t kInflateRounds = HBAM_INFLATE_ROUNDS;
 
 // Phase-A table prebuild (k_huff_tables -> k_inflate_huff), per block of a chunk.
 constexpr uint32_t kHuffTableImage = 8704;  // bytes of the LDS table image
