@@ -10,7 +10,7 @@ def main():
     path, name = sys.argv[1], sys.argv[2]
     min_ab = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     lines = open(path).read().split("\n")
-    start = next(i for i, l in enumerate(lines) if l.startswith(name) or (name in l and l.endswith(":") and l.startswith("_Z")))
+    start = next(i for i, l in enumerate(lines) if l.startswith(name) or (name in l and l.split(";")[0].strip().endswith(":") and l.startswith("_Z")))
     end = next(i for i in range(start + 1, len(lines)) if lines[i].strip().startswith(".Lfunc_end"))
     body = lines[start:end]
     labels = {}
