@@ -390,6 +390,13 @@ constexpr uint32_t kTableImage = offsetof(HuffLds, offs);
 static_assert(kTableImage % 16 == 0, "table image is copied in 16 B units");
 static_assert(kTableImage == kHuffTableImage, "hbam_device.h kHuffTableImage must match HuffLds");
 
+// A code of length l fills 2^(root - l) root entries: codes with l <= root -
+// kFillWave are filled by the whole wave together, longer ones by their lane.
+#ifndef HBAM_FILL_WAVE
+#define HBAM_FILL_WAVE 6
+#endif
+constexpr int kFillWave = HBAM_FILL_WAVE;
+
 // mode 0 litlen, 1 distance, 2 code-length codes
 __device__ __forceinline__ uint32_t make_entry(int mode, uint32_t s, uint32_t len) {
   if (mode == 0) {
@@ -491,18 +498,18 @@ __device__ __attribute__((noinline)) int build_table(HuffLds& L, const uint8_t* 
         // a code that fills fewer than 64 root entries fills them itself; the
         // wave fills the wider ones together below (a lane alone took up to
         // 2^(root - l) dependent trips, and the wave waited for the longest)
-        if ((int)l > root - 6)
+        if ((int)l > root - kFillWave)
           for (uint32_t i = rev; i < (1u << root); i += (1u << l)) tab[i] = e;
       } else {
         atomicMax(&tab[rev & rmask], kLongTag | (l - (uint32_t)root));  // widest sub-table under the prefix
         any_long = true;
       }
     }
-    for (uint64_t wm = __ballot(l != 0 && (int)l <= root - 6); wm; wm &= wm - 1) {
+    for (uint64_t wm = __ballot(l != 0 && (int)l <= root - kFillWave); wm; wm &= wm - 1) {
       const int src = __ffsll((long long)wm) - 1;
-      const uint32_t wl = (uint32_t)__shfl((int)l, src, 64);
-      const uint32_t wr = (uint32_t)__shfl((int)rev, src, 64);
-      const uint32_t we = (uint32_t)__shfl((int)e, src, 64);
+      const uint32_t wl = (uint32_t)__builtin_amdgcn_readlane((int)l, src);  // src is wave-uniform
+      const uint32_t wr = (uint32_t)__builtin_amdgcn_readlane((int)rev, src);
+      const uint32_t we = (uint32_t)__builtin_amdgcn_readlane((int)e, src);
       for (uint32_t k = lane; k < (1u << (root - (int)wl)); k += 64) tab[wr + (k << wl)] = we;
     }
   }
@@ -638,18 +645,18 @@ __device__ __attribute__((noinline)) int build_table_r(HuffLds& L, const uint8_t
         // a code that fills fewer than 64 root entries fills them itself; the
         // wave fills the wider ones together below (a lane alone took up to
         // 2^(root - l) dependent trips, and the wave waited for the longest)
-        if ((int)l > root - 6)
+        if ((int)l > root - kFillWave)
           for (uint32_t i = rev; i < (1u << root); i += (1u << l)) tab[i] = e;
       } else {
         atomicMax(&tab[rev & rmask], kLongTag | (l - (uint32_t)root));  // widest sub-table under the prefix
         any_long = true;
       }
     }
-    for (uint64_t wm = __ballot(l != 0 && (int)l <= root - 6); wm; wm &= wm - 1) {
+    for (uint64_t wm = __ballot(l != 0 && (int)l <= root - kFillWave); wm; wm &= wm - 1) {
       const int src = __ffsll((long long)wm) - 1;
-      const uint32_t wl = (uint32_t)__shfl((int)l, src, 64);
-      const uint32_t wr = (uint32_t)__shfl((int)rev, src, 64);
-      const uint32_t we = (uint32_t)__shfl((int)e, src, 64);
+      const uint32_t wl = (uint32_t)__builtin_amdgcn_readlane((int)l, src);  // src is wave-uniform
+      const uint32_t wr = (uint32_t)__builtin_amdgcn_readlane((int)rev, src);
+      const uint32_t we = (uint32_t)__builtin_amdgcn_readlane((int)e, src);
       for (uint32_t k = lane; k < (1u << (root - (int)wl)); k += 64) tab[wr + (k << wl)] = we;
     }
   }
@@ -1359,26 +1366,15 @@ __device__ int dyn_header_par(HuffLds& L, ClLds& C, const uint32_t* __restrict__
       }
     }
     const bool bad_lane = ns > kClMaxSym;
-    uint32_t incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t t = __shfl_up(incl, d, 64);
-      if (lane >= (uint32_t)d) incl += t;
-    }
+    const uint32_t incl = wave_incl_scan_dpp(cnt);  // DPP: no LDS round trips
     const uint32_t base = done + incl - cnt;
     const uint64_t reach = __ballot(done + incl >= ntot);
     const uint32_t lend = reach ? (uint32_t)__ffsll((unsigned long long)reach) - 1 : 63u;
-    // value entering each lane (for repeat codes): last defined value before it
-    uint32_t v = own, hv = has;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t v2 = __shfl_up(v, d, 64), h2 = __shfl_up(hv, d, 64);
-      if (lane >= (uint32_t)d && !hv) {
-        v = v2;
-        hv = h2;
-      }
-    }
-    uint32_t in_v = __shfl_up(v, 1, 64), in_h = __shfl_up(hv, 1, 64);
+    // value entering each lane (for repeat codes): last defined value before
+    // it, as a max-scan of (lane + 1) << 8 | value over the defining lanes
+    const uint32_t key = wave_incl_max_dpp(has ? ((lane + 1u) << 8) | own : 0u);
+    const uint32_t in_key = __shfl_up(key, 1, 64);
+    uint32_t in_v = in_key & 0xffu, in_h = in_key != 0;
     if (lane == 0 || !in_h) {
       in_v = prevv;
       in_h = have_prev;
@@ -1404,17 +1400,20 @@ __device__ int dyn_header_par(HuffLds& L, ClLds& C, const uint32_t* __restrict__
     }
     if (__ballot(bad)) return DH_TRUNC;
     if (reach) {  // this window completes the header: end = after lane lend's last used symbol
-      const uint32_t end = (uint32_t)__shfl(xe, (int)lend, 64);
+      const uint32_t end = (uint32_t)__builtin_amdgcn_readlane((int)xe, (int)lend);  // lend is wave-uniform
       if (end > E) return DH_TRUNC;
       *end_pos = rfl(end);
       break;
     }
-    const uint32_t tot = (uint32_t)__shfl(incl, 63, 64);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (tot == 0) return DH_TRUNC;  // no progress (ran past the staged window)
     done += tot;
-    prevv = (uint32_t)__shfl(v, 63, 64);
-    have_prev = (uint32_t)__shfl(hv, 63, 64) | have_prev;
-    p = rfl((uint32_t)__shfl(x, 63, 64));
+    const uint32_t k63 = (uint32_t)__builtin_amdgcn_readlane((int)key, 63);
+    if (k63) {
+      prevv = k63 & 0xffu;
+      have_prev = 1;
+    }
+    p = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
   }
   wave_sync();
   if (rfl(L.lens[256]) == 0) return DH_TRUNC;
