@@ -1295,6 +1295,7 @@ constexpr uint32_t kClSlice = 16;
 constexpr uint32_t kClMaxSym = kClSlice;  // a slice holds at most one symbol per bit
 struct ClLds {
   uint16_t ent[64][kClMaxSym];  // sym | extra << 5 | bits << 12
+  uint8_t ex[64][kClSlice];     // k_huff_tables: the slice's exit from each entry offset
 };
 static_assert(sizeof(ClLds) <= sizeof(HuffLds::lit), "ClLds aliases HuffLds::lit in k_inflate_huff");
 
@@ -1330,6 +1331,69 @@ __device__ int dyn_header_par(HuffLds& L, ClLds& C, const uint32_t* __restrict__
   for (;;) {  // windows of 64 * kClSlice bits
     const uint32_t a0 = p + lane * kClSlice, stop = a0 + kClSlice;
     uint32_t a = a0, x = a0, ns = 0;
+    if constexpr (REG) {
+      // k_huff_tables: the symbol at EVERY bit offset of the slice (16
+      // independent lookups), the slice's exit from every entry offset (a
+      // backward pass), then the entries of the 64 slices chained on the
+      // scalar unit.  The speculative decode + sync loop it replaces
+      // restarted 62 of 64 lanes per window, ~21 K cycles per header.
+      const bool live0 = a0 + 14 <= E;  // the decode stops at a field that may cross E (monotone in the offset)
+      uint64_t win = 0;
+      if (live0) win = (((uint64_t)W[(a0 >> 5) + 1] << 32) | W[a0 >> 5]) >> (a0 & 31);
+      uint32_t lenv[kClSlice];
+#pragma unroll
+      for (uint32_t j = 0; j < kClSlice; ++j) {
+        const uint32_t b = (uint32_t)(win >> j);
+        const uint32_t e = L.dist[b & 127];
+        const uint32_t nb = (e >> 16) & 31, sym = e & 0xffff;
+        const uint32_t xb = sym < 16 ? 0u : sym == 16 ? 2u : sym == 17 ? 3u : 7u;
+        const uint32_t ext = (b >> nb) & ((1u << xb) - 1);
+        lenv[j] = nb + xb;
+        C.ent[lane][j] = (uint16_t)(sym | (ext << 5) | ((nb + xb) << 12));
+      }
+      // exit offset (from the slice start) when the decode enters at j; the
+      // next slice's entry is exit - kClSlice (<= 14), 15 = stopped at E
+      uint32_t glo = 0, ghi = 0;
+#pragma unroll
+      for (int j = (int)kClSlice - 1; j >= 0; --j) {
+        const uint32_t nx = (uint32_t)j + lenv[j];
+        uint32_t exj = nx >= kClSlice ? nx : (uint32_t)C.ex[lane][min(nx, kClSlice - 1)];
+        if (a0 + (uint32_t)j + 14 > E) exj = (uint32_t)j;
+        C.ex[lane][j] = (uint8_t)exj;
+        const uint32_t g = exj >= kClSlice ? exj - kClSlice : 15u;
+        if (j < 8) glo |= g << (4 * j);
+        else ghi |= g << (4 * (j - 8));
+      }
+      uint32_t my_e = 15, ent = 0;  // ent: entry offset of slice l (wave-uniform)
+      for (uint32_t l = 0; l < 64; ++l) {
+        my_e = lane == l ? ent : my_e;
+        if (ent == 15) break;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)glo, (int)l);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)ghi, (int)l);
+        ent = ((ent < 8 ? lo >> (4 * ent) : hi >> (4 * (ent - 8)))) & 15u;
+      }
+      // walk the true symbols from the entry, compacting them to ent[lane][0..ns)
+      if (my_e != 15) {
+        uint32_t q = my_e;
+        a = a0 + q;
+        while (q < kClSlice && a0 + q + 14 <= E) {
+          const uint32_t en = C.ent[lane][q];
+          C.ent[lane][ns++] = (uint16_t)en;
+          q += en >> 12;
+        }
+        x = a0 + q;
+      }
+      // slices after the one that stopped at E start (and end) where it stopped
+      const uint64_t stopped = __ballot(my_e != 15 && x < stop);
+      if (stopped) {
+        const uint32_t sl = (uint32_t)__ffsll((unsigned long long)stopped) - 1;
+        const uint32_t xs = (uint32_t)__builtin_amdgcn_readlane((int)x, (int)sl);
+        if (lane > sl) {
+          a = x = xs;
+          ns = 0;
+        }
+      }
+    } else {
     auto decode_slice = [&]() {
       x = a;
       ns = 0;
@@ -1354,6 +1418,7 @@ __device__ int dyn_header_par(HuffLds& L, ClLds& C, const uint32_t* __restrict__
         a = px;
         decode_slice();
       }
+    }
     }
     // run lengths of this lane's symbols and its last defined value
     uint32_t cnt = 0, own = 0, has = 0;
