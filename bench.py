@@ -50,7 +50,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 SEED = 0x48424D00
 ALL = (1 << 64) - 1
 SOA_BYTES_PER_RECORD = 37  # key 8 + voff 8 + rest_off 8 + refID 4 + pos 4 + flag 2 + bin 2 + mapq 1
-INFLATE_ROUNDS = 4  # hbam_device.h kInflateRounds: k_huff_tables + k_inflate_huff launches per chunk
+INFLATE_ROUNDS = 2  # hbam_device.h kInflateRounds: k_huff_tables + k_inflate_huff launches per chunk (tests/test_bench_launch.py)
 BGZF_EOF = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
 
 

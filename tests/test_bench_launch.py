@@ -45,3 +45,13 @@ def test_failing_rank_fails_the_run():
                        capture_output=True, text=True, timeout=180,
                        env=_env(MASTER_ADDR="127.0.0.1", HBAM_BENCH_FAIL_RANK="1"))
     assert p.returncode != 0
+
+
+def test_inflate_rounds_match_the_library():
+    """bench.py divides phase A's time over INFLATE_ROUNDS launches per chunk:
+    it must be the library's kInflateRounds (HBAM_INFLATE_ROUNDS default)."""
+    import re
+    src = open(os.path.join(ROOT, "hadoop-bam_amd", "csrc", "hbam_device.h")).read()
+    rounds = int(re.search(r"#define HBAM_INFLATE_ROUNDS (\d+)", src).group(1))
+    bench = open(BENCH).read()
+    assert int(re.search(r"^INFLATE_ROUNDS = (\d+)", bench, re.M).group(1)) == rounds
