@@ -785,7 +785,11 @@ enum { LD_SPEC = 0, LD_SYNC = 1, LD_EMIT = 2 };
 
 // Boundaries of a lane's speculative walk: p[k] = bit position after symbol
 // kMergeFirst << k, b[k] = output bytes decoded up to there (~0u = not reached).
-constexpr uint32_t kMergeFirst = 4;  // power of two
+#ifndef HBAM_MERGE_FIRST
+#define HBAM_MERGE_FIRST 4
+#endif
+constexpr uint32_t kMergeFirst = HBAM_MERGE_FIRST;  // power of two
+static_assert((kMergeFirst & (kMergeFirst - 1)) == 0, "kMergeFirst: a power of two");
 struct MergePts {
   uint32_t p0, p1, p2, p3;
   uint32_t b0, b1, b2, b3;
