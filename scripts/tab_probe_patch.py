@@ -22,14 +22,12 @@ KEDITS = [  # (anchor, text, insert after the anchor?)
      "  uint64_t tb_t0 = clock64();\n", False),
     ("  if (rfl(build_tab<REG>(L, L.cl_lens, 19, 7, 2, L.dist, L.cnt_dist, L.sort_dist, nullptr, 0))) return DH_TRUNC;\n",
      "  if constexpr (REG) TBP(1);\n", True),
-    ("    decode_slice();\n    for (;;) {  // sync: restart each slice from its predecessor's exit\n",
-     "    if constexpr (REG) { TBP(10); if (lane_id() == 0 && (blockIdx.x & 63) == 0) atomicAdd(&g_tab_probe[14], 1ull); }\n", False),
-    ("      if (need) {\n        a = px;\n        decode_slice();\n      }\n    }\n",
-     "    if constexpr (REG) TBP(11);\n", True),
+    ("      // exit offset (from the slice start) when the decode enters at j; the\n", "      TBP(10);\n", False),
+    ("      // entry of slice l = F_{l-1}(0), F_l = g_l o ... o g_0: an inclusive\n", "      TBP(11);\n", False),
+    ("      // walk the true symbols from the entry, compacting them to ent[lane][0..ns)\n", "      TBP(14);\n", False),
+    ("    // run lengths of this lane's symbols and its last defined value\n", "    if constexpr (REG) TBP(15);\n", False),
     ("    // write this lane's runs\n", "    if constexpr (REG) TBP(12);\n", False),
     ("    if (__ballot(bad)) return DH_TRUNC;\n    if (reach) {", "    if constexpr (REG) TBP(13);\n", False),
-    ("        decode_slice();\n      }\n    }\n    if constexpr (REG) TBP(11);\n",
-     "        if constexpr (REG) if ((blockIdx.x & 63) == 0) atomicAdd(&g_tab_probe[15], 1ull);\n", False),
     ("  wave_sync();\n  if (rfl(L.lens[256]) == 0) return DH_TRUNC;\n", "  if constexpr (REG) TBP(2);\n", True),
     ("  if (rfl(build_tab<REG>(L, L.lens + hlit, (int)hdist, kDistRoot, 1, L.dist, L.cnt_dist, L.sort_dist, L.distsub,\n",
      "  if constexpr (REG) TBP(3);\n", False),
@@ -53,7 +51,7 @@ PEDITS = [
      "  if (any && getenv(\"HBAM_TAB_STATS\")) {\n    unsigned long long t[16];\n    HIPCHK(hipDeviceSynchronize());\n"
      "    HIPCHK(tab_probe_read(t));\n    const double n = t[8] ? (double)t[8] : 1.0;\n"
      "    fprintf(stderr, \"[tab] headers %llu, cycles per header: stage %.0f cl %.0f lens %.0f lit %.0f dist %.0f "
-     "pair %.0f est %.0f write %.0f probe %.0f (1 block in 64); lens: first-decode %.0f sync %.0f scans %.0f write %.0f windows/hdr %.2f resync-lanes/hdr %.1f\\n\", t[8], t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n, t[5] / n, t[6] / n, t[7] / n, t[9] / n, t[10] / n, t[11] / n, t[12] / n, t[13] / n, t[14] / n, t[15] / n);\n  }\n", False),
+     "pair %.0f est %.0f write %.0f probe %.0f (1 block in 64); lens: lookups %.0f backward %.0f runs+scans %.0f write %.0f chain %.0f walk %.0f\\n\", t[8], t[0] / n, t[1] / n, t[2] / n, t[3] / n, t[4] / n, t[5] / n, t[6] / n, t[7] / n, t[9] / n, t[10] / n, t[11] / n, t[12] / n, t[13] / n, t[14] / n, t[15] / n);\n  }\n", False),
 ]
 LEDITS = [("hipError_t launch_inflate_lz77(", "hipError_t tab_probe_read(unsigned long long* t);\n", False)]
 
