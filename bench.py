@@ -41,14 +41,15 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "hadoop-bam_amd"))
-# 8 hardware queues per device for the context's streams (libhbam asks for it
-# when it loads first; at N > 1 torch initializes HIP before libhbam loads)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# GPU_MAX_HW_QUEUES is left as the box sets it (4): libhbam's stream priority
+# levels keep its decode, batch and staging streams on separate queues at 4
+# (DESIGN.md 3), and the line records the value it ran at.
 
 METRIC = "uncompressed BAM decode GB/s + records/sec per GPU and 8-GPU node"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 SEED = 0x48424D00
 ALL = (1 << 64) - 1
+BOUND_MIN = 0.7  # a limit below this is not called the bound (roofline.bound = "latency")
 SOA_BYTES_PER_RECORD = 37  # key 8 + voff 8 + rest_off 8 + refID 4 + pos 4 + flag 2 + bin 2 + mapq 1
 INFLATE_ROUNDS = 2  # hbam_device.h kInflateRounds: k_huff_tables + k_inflate_huff launches per chunk (tests/test_bench_launch.py)
 BGZF_EOF = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
@@ -197,7 +198,7 @@ def pmc_traffic(path, vstart, vend, kernel):
         return None
     sys.path.insert(0, os.path.join(ROOT, "profiles"))
     import summarize
-    out = {}
+    out, tot = {}, {}
     base = tempfile.mkdtemp(prefix="hbam_pmc_", dir="/tmp")
     env = dict(os.environ, TMPDIR="/tmp")
     for sub, counters in PMC_PASSES:
@@ -215,6 +216,8 @@ def pmc_traffic(path, vstart, vend, kernel):
         if p.returncode != 0:
             return {"error": f"{sub} pass rc={p.returncode}: {err.decode(errors='replace')[-300:]}"}
         cs = summarize.counters(base, sub, merge_instances=True)
+        if sub in ("fetch", "write"):
+            tot[sub] = summarize.totals(base, sub)
         e = cs.get(kernel)
         if not e:
             return {"error": f"{sub}: no dispatch of {kernel} in the counter file"}
@@ -229,6 +232,17 @@ def pmc_traffic(path, vstart, vend, kernel):
     write = out["WRITE_SIZE"] * 1024
     res = {"bytes_per_launch": int(fetch + write), "fetch_bytes": int(fetch), "write_bytes": int(write),
            "main_dispatches": out.get("main_dispatches")}
+    # the child decodes the split once: every dispatch of its run summed is
+    # one pass's HBM traffic (+ the open's few header-read dispatches)
+    per = {}
+    for k in set(tot.get("fetch", {})) | set(tot.get("write", {})):
+        f_ = tot.get("fetch", {}).get(k, {}).get("FETCH_SIZE", 0.0) * 1024 * 2
+        w_ = tot.get("write", {}).get(k, {}).get("WRITE_SIZE", 0.0) * 1024
+        per[k] = (int(f_), int(w_))
+    res["pass_traffic"] = {"bytes": sum(a + b for a, b in per.values()),
+                           "per_kernel_GB": {k: round((a + b) / 1e9, 4) for k, (a, b) in
+                                             sorted(per.items(), key=lambda kv: -sum(kv[1]))[:12]},
+                           "kernel_bytes": {k: a + b for k, (a, b) in per.items()}}
     cyc = out.get("GRBM_GUI_ACTIVE", 0) / 8.0
     if cyc > 0 and "SQ_INSTS_VALU" in out:
         valu, salu = out["SQ_INSTS_VALU"], out.get("SQ_INSTS_SALU", 0.0)
@@ -341,6 +355,11 @@ def pinned_host_leg(path, records):
 
 C3_SEG_RECORDS = 5_000_000  # records per segment of the C3 file
 C3_BODIES = 3                # distinct body segments (each repeated an odd number of times)
+# BASELINE config 3: "30x WGS-scale BAM (~600M reads, ~60 GB)".  The C2 model's
+# unbinned qualities make ~141 B per record, which would put 600 M reads at
+# ~85 GB; with Illumina's 8-level quality binning (gen_synth_bam.c mode 2)
+# a record is ~100 B, so a ~60 GB file holds ~600 M reads: both figures.
+C3_MODE = "wgs"
 
 
 def c3_sequence(k):
@@ -369,7 +388,7 @@ def build_c3_file(path, D, target_gb, seg_records=C3_SEG_RECORDS):
     for j in range(1 + C3_BODIES):
         if j % D.world == D.rank:
             mine[j] = synth.make_bam_segment(n_model, j * seg_records, (j + 1) * seg_records,
-                                             with_header=j == 0, eof_block=False, seed=SEED + 3)
+                                             with_header=j == 0, eof_block=False, seed=SEED + 3, mode=C3_MODE)
     sizes = {}
     for part in D.all_gather({j: (int(a.nbytes), int(i["uncompressed"])) for j, (a, i) in mine.items()}):
         sizes.update(part)
@@ -471,14 +490,23 @@ def run_c3(D, target_gb, steps, warmup, host_leg=False, solo=False):
         split = shard.ShardedBamReader(f, size, first, D.rank, D.world, D.all_gather).split()
         vs, ve = split if split is not None else (0, 0)
         lo, hi = vs >> 16, min(size, (ve >> 16) + (256 << 10))
-        if host_leg and split is not None:
+        if host_leg:
+            # feed-inclusive: every rank decodes its split with the windows
+            # copied from the mapped file inside the timed call (the PCIe H2D
+            # of its own bytes included), max over ranks
+            D.barrier()
             t = time.perf_counter()
-            st = f.decode_span_device(vs, ve, timing=False, digest=False)
-            dt = time.perf_counter() - t
+            st = f.decode_span_device(vs, ve, timing=False, digest=False) if split is not None else None
+            dt_mine = time.perf_counter() - t
+            D.barrier()
+            dt = D.max_over_ranks(dt_mine)
+            recs = D.all_gather(0 if st is None else int(st["records"]))
             res["c3_streamed_from_host"] = {
                 "seconds": round(dt, 3), "uncompressed_GBps": round(meta["uncompressed_bytes"] / dt / 1e9, 3),
-                "records_per_s": round(st["records"] / dt, 1), "windows": st["windows"],
-                "note": "windows copied from the mapped file (pageable) inside the timed call"}
+                "records_per_s": round(sum(recs) / dt, 1), "windows_rank0": None if st is None else st["windows"],
+                "rank0_seconds": round(dt_mine, 3),
+                "note": "each rank's split decoded with its windows copied from the mapped file (pageable, "
+                        "through the host feed) inside the timed call; max over ranks"}
         t = time.perf_counter()
         if split is not None:
             f.prefetch(lo, hi)  # inputs resident in HBM before the timed region
@@ -763,6 +791,7 @@ def run_c2(D, args, steps, warmup, extras):
         # untimed measurement passes: every launch on one stream between its own
         # HIP events -> per-stage and per-kernel durations (the roofline)
         stats = [step(timing=True) for _ in range(3)]
+        tokens = f.inflate_token_count() if split is not None else 0  # phase A's output of that pass
         check = step(timing=args.serial, digest=True)  # untimed: the digests for the parity check
         mine = (0, 0, 0, 0) if check is None else (int(check["records"]), int(check["inflated_bytes"]),
                                                    int(check["key_digest"]), int(check["voff_digest"]))
@@ -833,11 +862,12 @@ def run_c2(D, args, steps, warmup, extras):
                 log(f"[extra] dropin_end_to_end {time.time() - t:.1f}s")
             if not args.no_pmc:
                 try:
+                    st_c = stats[-1]["compressed_bytes"]
                     tr = pmc_traffic(path, vs, ve, out["roofline"]["kernel"])
                     if tr and "bytes_per_launch" in tr:
                         rf = out["roofline"]
                         rf["traffic"] = tr["bytes_per_launch"]
-                        rf["traffic_detail"] = {k: v for k, v in tr.items() if k != "issue"}
+                        rf["traffic_detail"] = {k: v for k, v in tr.items() if k not in ("issue", "pass_traffic")}
                         rf["traffic_detail"]["source"] = "rocprofv3 --pmc child runs, this session, every " \
                                                          "full-size dispatch of the kernel"
                         rf["traffic_frac_of_alg"] = round(tr["bytes_per_launch"] / max(rf["alg_bytes_per_launch"], 1), 3)
@@ -848,11 +878,33 @@ def run_c2(D, args, steps, warmup, extras):
                                    "hbm_traffic": tr["bytes_per_launch"] / (rf["avg_launch_ms"] * 1e-3) / 1e9
                                    / HBM_PEAK_GBS}
                             rf["limits"] = {k: round(v, 4) for k, v in lim.items()}
-                            rf["bound"] = max(lim, key=lim.get).replace("hbm_traffic", "hbm")
-                            rf["bound_rule"] = ("the largest of: algorithmic HBM bytes / peak (frac), measured "
-                                                "HBM traffic / peak, VALU and SALU issue fractions and the "
-                                                "LDS-array busy fraction (issue); "
+                            top = max(lim, key=lim.get)
+                            rf["bound"] = top.replace("hbm_traffic", "hbm") if lim[top] >= BOUND_MIN else "latency"
+                            rf["bound_rule"] = (f"the largest of: algorithmic HBM bytes / peak (frac), measured "
+                                                f"HBM traffic / peak, VALU and SALU issue fractions and the "
+                                                f"LDS-array busy fraction (issue), when it is >= {BOUND_MIN}; "
+                                                f"'latency' when every limit is below {BOUND_MIN} (no unit "
+                                                f"saturated: the dependent chain sets the pace); "
                                                 "achieved / peak / frac stay the algorithmic-bytes HBM figures")
+                        pt = tr.get("pass_traffic")
+                        if pt:
+                            b_alg = rf["alg_bytes_per_launch"] * rf["launches_per_pass"]
+                            wp = rf["whole_pass"]
+                            wp["traffic"] = pt["bytes"]
+                            wp["traffic_frac_of_alg"] = round(pt["bytes"] / max(b_alg, 1), 3)
+                            wp["traffic_GBps"] = round(pt["bytes"] / (out["ms_per_step"] * 1e-3) / 1e9, 1)
+                            wp["traffic_per_kernel_GB"] = pt["per_kernel_GB"]
+                            wp["traffic_rule"] = ("FETCH_SIZE x 2 + WRITE_SIZE (KiB -> B) summed over every "
+                                                  "dispatch of a child that decodes the split once, against "
+                                                  "C + U + 37 N; traffic_GBps over the timed step")
+                            ka = pt["kernel_bytes"].get("hbam::k_inflate_huff")
+                            if ka and tokens:
+                                a_alg = st_c + 4 * tokens
+                                rf["phase_a"] = {
+                                    "traffic": ka, "alg_bytes": a_alg, "traffic_frac_of_alg": round(ka / a_alg, 3),
+                                    "tokens": tokens,
+                                    "rule": "k_inflate_huff traffic of one pass (every dispatch) against its own "
+                                            "algorithmic bytes: C read + 4 B per LZ77 token written"}
                     elif tr:
                         out["roofline"]["traffic_error"] = tr["error"]
                 except Exception as e:
@@ -995,6 +1047,8 @@ def main():
     ap.add_argument("--one-device", action="store_true", help="every rank on device 0 (rehearsal only)")
     ap.add_argument("--no-solo", action="store_true",
                     help="N > 1: skip rank 0's solo pass (the N = 1 value of the same workload)")
+    ap.add_argument("--no-feed-leg", action="store_true",
+                    help="N > 1: skip the feed-inclusive C3 decode (windows copied from the mapped file)")
     ap.add_argument("--dry-run", action="store_true",
                     help="start the ranks and rendezvous (gloo), report them, decode nothing (CPU test of the launch)")
     ap.add_argument("--pmc-child", default=None, help=argparse.SUPPRESS)
@@ -1052,7 +1106,7 @@ def main():
             log(f"[extra] c2_from_pinned_host {time.time() - t:.1f}s")
             line.setdefault("extra", {})["c2_from_pinned_host"] = ph
     else:
-        r = run_c3(D, args.c3_gb, args.steps, args.warmup, host_leg=False, solo=not args.no_solo)
+        r = run_c3(D, args.c3_gb, args.steps, args.warmup, host_leg=not args.no_feed_leg, solo=not args.no_solo)
         if D.rank == 0:
             solo = r.get("solo")
             line = {"value": r["value"], "ms_per_step": r["ms_per_step"], "records_per_s": r["records_per_s"],
@@ -1073,6 +1127,7 @@ def main():
                                "parallelism": f"FileVirtualSplit per rank x{D.world} (BAMSplitGuesser)"},
                     "parity": {"records": r["records"], "matches_oracle": r["matches_oracle"],
                                "c3": r["c3_parity"], "c5_splitting_bai_g4096": r["c5_splitting_bai_g4096"]},
+                    "feed_inclusive": r.get("c3_streamed_from_host"),
                     "stages_ms": r["stages_ms_rank0"], "windows_rank0": r["windows_rank0"],
                     "roofline": r["roofline"], "cpu_baseline": r["cpu_baseline"]}
         if D.world > 1 and not args.no_extra:

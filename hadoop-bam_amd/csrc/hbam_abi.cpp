@@ -433,6 +433,12 @@ int hbam_pipeline_counters(hbam_ctx* ctx, uint64_t out[5]) {
   return HBAM_OK;
 }
 
+int hbam_inflate_token_count(hbam_ctx* ctx, uint64_t* tokens) {
+  *tokens = 0;
+  if (!ctx || !ctx->f) return HBAM_E_STATE;
+  return ctx->f->pipe().inflate_tokens(tokens) == 0 ? HBAM_OK : HBAM_E_DEVICE;
+}
+
 int hbam_decode_span_device(hbam_ctx* ctx, uint64_t vstart, uint64_t vend, int32_t flags, hbam_gpu_stats* st) {
   if (!ctx || !ctx->f) return HBAM_E_STATE;
   ctx->cursor.reset();

@@ -322,6 +322,18 @@ int Pipeline::d2d_bandwidth(uint64_t bytes, int iters, float* gbps) {
   return kOk;
 }
 
+int Pipeline::inflate_tokens(uint64_t* n) {
+  *n = 0;
+  const size_t nb = hblocks_.size();
+  if (nb == 0) return kOk;
+  std::vector<HuffOut> h(nb);
+  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(hipStreamSynchronize(stream_b_));
+  HIPCHK(hipMemcpy(h.data(), hout_.p, nb * sizeof(HuffOut), hipMemcpyDeviceToHost));
+  for (const HuffOut& o : h) *n += o.ntok;
+  return kOk;
+}
+
 int Pipeline::set_ref_lengths(const std::vector<int32_t>& lens) {
   HIPCHK(ref_len_.reserve(lens.size() + 1));
   if (!lens.empty())

@@ -253,6 +253,9 @@ class Pipeline {
   uint64_t record_fallbacks() const { return record_fallbacks_; }
   uint64_t records_after_stop() const { return records_after_stop_; }
   uint64_t inflate_launches() const { return inflate_launches_; }
+  // LZ77 tokens phase A wrote for the window's blocks in its last inflate
+  // (the sum of HuffOut::ntok; a synchronous read, for measurements)
+  int inflate_tokens(uint64_t* n);
   StageTimes times;
   bool timing = false;  // record per-stage HIP event times
 

@@ -90,6 +90,7 @@ _sig("hbam_decode_span", C.c_int, [P, u64, u64, u64, C.POINTER(Batch)])
 _sig("hbam_decode_span_device", C.c_int, [P, u64, u64, i32, C.POINTER(GpuStats)])
 _sig("hbam_reader_position", C.c_int, [P, u64, C.POINTER(u64)])
 _sig("hbam_pipeline_counters", C.c_int, [P, C.POINTER(u64)])
+_sig("hbam_inflate_token_count", C.c_int, [P, C.POINTER(u64)])
 _sig("hbam_file_stats", C.c_int, [P, C.POINTER(u64), C.POINTER(u64)])
 _sig("hbam_bytes_read", C.c_int, [P, C.POINTER(u64)])
 _sig("hbam_prefetch", C.c_int, [P, u64, u64])
@@ -416,6 +417,15 @@ class BamFile:
         return dict(zip(("link_fallbacks", "link_rewalks", "record_fallbacks", "inflate_launches",
                          "records_after_stop"),
                         (int(x) for x in v)))
+
+    def inflate_token_count(self):
+        """LZ77 tokens phase A wrote in the last pass over the current window
+        (hbam_inflate_token_count)."""
+        v = u64()
+        rc = _L.hbam_inflate_token_count(self._h, C.byref(v))
+        if rc != OK:
+            raise self._err(rc)
+        return int(v.value)
 
     def decode_span_device(self, vstart, vend, timing=False, decode=True, digest=True):
         """The span decoded with the records left in HBM: stats dict."""

@@ -10,6 +10,9 @@ _LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
 _G = None
 
 STRATEGY = {"default": 0, "filtered": 1, "huffman": 2, "rle": 3, "fixed": 4}
+# short: C2 (150 bp paired-end, Illumina-like qualities); long: C4 (ONT-like);
+# wgs: C3 (the short-read model with Illumina's 8-level binned qualities)
+MODE = {"short": 0, "long": 1, "wgs": 2}
 
 
 class _Params(C.Structure):
@@ -36,7 +39,7 @@ def make_bam(n_records, mode="short", level=5, strategy="default", block_payload
              eof_block=True, all_unmapped=False, seed=0x48424D00, as_numpy=False):
     """Return (bam_bytes_or_uint8_array, info dict)."""
     import numpy as np
-    p = _Params(n_records, 1 if mode == "long" else 0, level, STRATEGY[strategy], block_payload,
+    p = _Params(n_records, MODE[mode], level, STRATEGY[strategy], block_payload,
                 threads or min(16, os.cpu_count() or 8), int(eof_block), int(all_unmapped), seed)
     out = C.c_void_p()
     n = C.c_uint64()
@@ -63,7 +66,7 @@ def make_bam_segment(n_records, lo, hi, with_header, eof_block, mode="short", le
     processes can each write their part of one file.  Returns (uint8 ndarray,
     info)."""
     import numpy as np
-    p = _Params(n_records, 1 if mode == "long" else 0, level, 0, block_payload,
+    p = _Params(n_records, MODE[mode], level, 0, block_payload,
                 threads or min(16, os.cpu_count() or 8), int(eof_block), int(all_unmapped), seed)
     out = C.c_void_p()
     n = C.c_uint64()

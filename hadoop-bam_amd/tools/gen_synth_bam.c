@@ -10,6 +10,11 @@
  *           aux NM:i MD:Z AS:i XS:i RG:Z.
  *   mode 1  "C4": ONT-like long reads, 10-50 kb (log-normal, median 20 kb),
  *           Q 5-30, CIGARs of 100s-1000s of ops, MM:Z + ML:B:C, 10 % unmapped.
+ *   mode 2  "C3": mode 0 with the qualities binned to the 8 levels of
+ *           Illumina's quality binning (2, 6, 15, 22, 27, 33, 37, 40), as
+ *           30x WGS BAMs from binned-quality instruments hold them: ~100 B
+ *           per record compressed, so ~600 M reads are ~60 GB, as BASELINE
+ *           config 3 names it (mode 0's unbinned qualities: ~141 B).
  * BGZF framing as htsjdk/htslib write it (1f8b0804 00000000 00ff 0600 4243 0200
  * BSIZE); raw DEFLATE at a chosen level/strategy; payload cut every
  * `block_payload` bytes regardless of record boundaries; optional EOF block.
@@ -25,7 +30,7 @@
 
 typedef struct {
   uint64_t n_records;
-  int32_t mode;           /* 0 short PE, 1 long reads */
+  int32_t mode;           /* 0 short PE, 1 long reads, 2 short PE with binned qualities */
   int32_t level;          /* zlib level (htsjdk default 5) */
   int32_t strategy;       /* Z_DEFAULT_STRATEGY(0) Z_FILTERED(1) Z_HUFFMAN_ONLY(2) Z_RLE(3) Z_FIXED(4) */
   int32_t block_payload;  /* uncompressed bytes per BGZF block (<= 65280 for stored safety) */
@@ -115,7 +120,7 @@ static uint32_t make_record(const model *m, uint64_t i, uint8_t *o) {
     if (p->all_unmapped || r < (p->mode == 1 ? 100u : 15u)) unmapped = 1;
   }
   /* read length */
-  if (p->mode == 0) {
+  if (p->mode != 1) {
     l_seq = 150;
   } else {
     /* log-normal-ish: median 20 kb, clipped 10-50 kb */
@@ -137,14 +142,14 @@ static uint32_t make_record(const model *m, uint64_t i, uint8_t *o) {
     ref = mref = -1;
     pos = mpos = -1;
   } else if (unmapped) {
-    flag = (p->mode == 0 ? (0x1 | (mate ? 0x80 : 0x40)) : 0) | 0x4;
+    flag = (p->mode != 1 ? (0x1 | (mate ? 0x80 : 0x40)) : 0) | 0x4;
     mapq = 0;
-    mref = p->mode == 0 ? ref : -1;
-    mpos = p->mode == 0 ? pos : -1;
+    mref = p->mode != 1 ? ref : -1;
+    mpos = p->mode != 1 ? pos : -1;
     if (p->mode == 1) { ref = -1; pos = -1; }
   } else {
     mapq = (uint8_t)(20 + splitmix(&s) % 41);
-    if (p->mode == 0) {
+    if (p->mode != 1) {
       flag = 0x1 | 0x2 | (mate ? 0x80 : 0x40) | (mate ? 0x10 : 0x20);
       mref = ref;
       mpos = pos + (mate ? -200 : 200);
@@ -186,7 +191,7 @@ static uint32_t make_record(const model *m, uint64_t i, uint8_t *o) {
   int nm = (int)(splitmix(&s) % 4);
   int mdl = nm ? snprintf(md, sizeof md, "%dA%dC%d", l_seq / 2, 3, l_seq - l_seq / 2 - 5) : snprintf(md, sizeof md, "%d", l_seq);
   int aux_len = 0;
-  if (p->mode == 0) {
+  if (p->mode != 1) {
     aux_len += 3 + 1;                 /* NM:C */
     aux_len += 3 + mdl + 1;           /* MD:Z */
     aux_len += 3 + 1 + 3 + 1;         /* AS:C XS:C */
@@ -244,7 +249,7 @@ static uint32_t make_record(const model *m, uint64_t i, uint8_t *o) {
    * segment indicator) -- about 3.9 bits per quality after DEFLATE, which puts
    * C2 at ~1.5 GB compressed as SURVEY 8d asks; ONT-like random walk Q5..30
    * for long reads */
-  if (p->mode == 0) {
+  if (p->mode != 1) {
     uint64_t tr = splitmix(&ms);
     const int tail = (tr % 100) < 8 ? l_seq - 5 - (int)((tr >> 8) % 40) : l_seq;
     for (int k = 0; k < l_seq; ++k) {
@@ -255,6 +260,7 @@ static uint32_t make_record(const model *m, uint64_t i, uint8_t *o) {
       if (k >= tail) q = 2;
       if (q > 41) q = 41;
       if (q < 2) q = 2;
+      if (p->mode == 2) q = q < 3 ? 2 : q < 10 ? 6 : q < 20 ? 15 : q < 25 ? 22 : q < 30 ? 27 : q < 35 ? 33 : q < 40 ? 37 : 40;
       *w++ = (uint8_t)q;
     }
   } else {
@@ -268,7 +274,7 @@ static uint32_t make_record(const model *m, uint64_t i, uint8_t *o) {
       *w++ = (uint8_t)q;
     }
   }
-  if (p->mode == 0) {
+  if (p->mode != 1) {
     memcpy(w, "NMC", 3); w[3] = (uint8_t)nm; w += 4;
     memcpy(w, "MDZ", 3); memcpy(w + 3, md, (size_t)mdl); w[3 + mdl] = 0; w += 3 + mdl + 1;
     memcpy(w, "ASC", 3); w[3] = (uint8_t)(l_seq - 5 * nm); w += 4;
@@ -375,10 +381,10 @@ int gen_bam_segment(const gen_params *p, uint64_t lo, uint64_t hi, int with_head
   const uint64_t N = p->n_records;
   if (hi > N) hi = N;
   if (lo > hi) lo = hi;
-  m.n_unplaced_start = p->mode == 0 ? N - N / 200 : N;
+  m.n_unplaced_start = p->mode != 1 ? N - N / 200 : N;
   m.n_mapped = m.n_unplaced_start;
   /* 30x local coverage of 150 bp reads: 5 bp per read */
-  m.span = p->mode == 0 ? m.n_mapped * 5 : m.n_mapped * 1500;
+  m.span = p->mode != 1 ? m.n_mapped * 5 : m.n_mapped * 1500;
   int nt = p->threads > 0 ? (p->threads > 256 ? 256 : p->threads) : 8;
   const uint64_t R = hi - lo;
   uint32_t *sizes = (uint32_t *)malloc((R + 1) * sizeof *sizes);

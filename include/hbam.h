@@ -313,6 +313,12 @@ int hbam_decode_span_device(hbam_ctx *ctx, uint64_t vstart, uint64_t vend, int32
  * assert which path a decode took. */
 int hbam_pipeline_counters(hbam_ctx *ctx, uint64_t out[5]);
 
+/* The LZ77 tokens inflate phase A wrote for the blocks of the ctx's current
+ * window in its last pass (u32 each: phase A's output bytes / 4).  A
+ * measurement helper for the bench's traffic figures (no reference
+ * counterpart); synchronous. */
+int hbam_inflate_token_count(hbam_ctx *ctx, uint64_t *tokens);
+
 /* The sharded SplittingBAMIndexer.index (SplittingBAMIndexer.java:262-287,
  * SURVEY 8e step 3): the records of FileVirtualSplit [vstart, vend) read
  * under the indexer's rules (readAlignment/fullySkip, :340-368), their count

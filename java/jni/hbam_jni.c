@@ -271,7 +271,7 @@ JNIEXPORT jbyteArray FN(splittingIndexForRecords)(JNIEnv *env, jclass c, jint de
   jsize n;
   uint64_t *v = from_longs(env, voffs, &n);
   if (!v) return NULL;
-  hbam_opts o = {device, 0, HBAM_STRICT, 0, 0};
+  hbam_opts o = {device, 0, HBAM_STRICT, 0, 0, 0};
   uint8_t *buf = NULL;
   uint64_t len = 0;
   int rc = hbam_splitting_index_for_records(&o, v, (uint64_t)n, g, (uint64_t)file_size, &buf, &len);
@@ -393,7 +393,7 @@ JNIEXPORT jlong FN(encodeWritables)(JNIEnv *env, jclass c, jlong h, jobject out,
 }
 
 JNIEXPORT jlong FN(openCodec)(JNIEnv *env, jclass c, jint device) {
-  hbam_opts o = {device, 0, HBAM_STRICT, 0, 0};
+  hbam_opts o = {device, 0, HBAM_STRICT, 0, 0, 0};
   hbam_ctx *ctx = NULL;
   int rc = hbam_open_codec(&o, &ctx);
   if (rc != HBAM_OK) {
@@ -423,7 +423,7 @@ JNIEXPORT jobjectArray FN(decodeWritables)(JNIEnv *env, jclass c, jlong h, jobje
 
 JNIEXPORT jbyteArray FN(bgzfCompress)(JNIEnv *env, jclass c, jint device, jobject payload, jintArray lens,
                                       jint level, jboolean eof) {
-  hbam_opts o = {device, 0, HBAM_STRICT, 0, 0};
+  hbam_opts o = {device, 0, HBAM_STRICT, 0, 0, 0};
   const void *p = (*env)->GetDirectBufferAddress(env, payload);
   const uint64_t plen = (uint64_t)(*env)->GetDirectBufferCapacity(env, payload);
   const jsize nb = lens ? (*env)->GetArrayLength(env, lens) : 0;

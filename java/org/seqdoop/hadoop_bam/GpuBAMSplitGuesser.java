@@ -13,7 +13,9 @@
 //       record may hold
 //   guessNextBAMRecordStart(beg, end)                                :108-235
 //       the virtual offset of the first BAM record in [beg, end), or end
-//   main(String[])                                                   :340-401
+//
+// BAMSplitGuesser.main (:340-401), a command-line probe, is not mirrored: the
+// CLI is outside the read path this class replaces.
 //
 // The stream is read through hbam_open_reader: a positioned reader over the
 // SeekableStream (seek + read, one call at a time), so any Hadoop
@@ -40,11 +42,8 @@ import java.io.InputStream;
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
 import org.apache.hadoop.conf.Configuration;
-import org.apache.hadoop.fs.Path;
-import org.apache.hadoop.util.GenericOptionsParser;
 import org.seqdoop.hadoop_bam.gpu.HbamNative;
 import org.seqdoop.hadoop_bam.util.SAMHeaderReader;
-import org.seqdoop.hadoop_bam.util.WrapSeekable;
 
 public class GpuBAMSplitGuesser extends BaseSplitGuesser implements Closeable {
   /** As BAMSplitGuesser.MAX_BYTES_READ (:72-73): 3 * 0xffff + 0xfffe. */
@@ -127,47 +126,5 @@ public class GpuBAMSplitGuesser extends BaseSplitGuesser implements Closeable {
     } finally {
       super.finalize();
     }
-  }
-
-  /** As BAMSplitGuesser.main (:340-401). */
-  public static void main(String[] args) throws IOException {
-    final GenericOptionsParser parser;
-    try {
-      parser = new GenericOptionsParser(args);
-    } catch (Exception e) {
-      System.err.printf("Error in Hadoop arguments: %s\n", e.getMessage());
-      System.exit(1);
-      return;
-    }
-    args = parser.getRemainingArgs();
-    final Configuration conf = parser.getConfiguration();
-    if (args.length < 2 || args.length > 3) {
-      System.err.println("Usage: GpuBAMSplitGuesser path-or-uri header-path-or-uri [beg]");
-      System.exit(2);
-    }
-    long beg = 0;
-    try {
-      if (args.length > 2) beg = Long.decode(args[2]);
-    } catch (NumberFormatException e) {
-      System.err.println("Invalid beg offset.");
-      if (e.getMessage() != null) System.err.println(e.getMessage());
-      System.exit(2);
-    }
-    final SeekableStream ss = WrapSeekable.openPath(conf, new Path(args[0]));
-    final SeekableStream hs = WrapSeekable.openPath(conf, new Path(args[1]));
-    final long end = beg + MAX_BYTES_READ;
-    System.out.printf("Will look for a BGZF block within: [%1$#x,%2$#x) = [%1$d,%2$d)\n"
-        + "Will then verify BAM data within:  [%1$#x,%3$#x) = [%1$d,%3$d)\n", beg, beg + 0xffff, end);
-    final long g;
-    try (GpuBAMSplitGuesser guesser = new GpuBAMSplitGuesser(ss, hs, conf)) {
-      g = guesser.guessNextBAMRecordStart(beg, end);
-    }
-    ss.close();
-    if (g == end) {
-      System.out.println("Didn't find any acceptable BAM record in any BGZF block.");
-      System.exit(1);
-    }
-    System.out.printf("Accepted BGZF block at offset %1$#x (%1$d).\n"
-        + "Accepted BAM record at offset %2$#x (%2$d) therein.\n", g >> 16, g & 0xffff);
   }
 }

@@ -158,6 +158,23 @@ def counters(d, sub, merge_instances=False):
     return out
 
 
+def totals(d, sub):
+    """Per kernel (template instances merged): each counter summed over every
+    dispatch of the run, and the dispatch count."""
+    p = _find(os.path.join(d, sub), "*counter_collection.csv")
+    out = defaultdict(lambda: defaultdict(float))
+    if not p:
+        return {}
+    seen = defaultdict(set)
+    for r in csv.DictReader(open(p)):
+        k = base_name(short(_col(r, "Kernel_Name", "KernelName")))
+        out[k][_col(r, "Counter_Name", "CounterName")] += float(_col(r, "Counter_Value", "CounterValue"))
+        seen[k].add(_col(r, "Dispatch_Id", "DispatchId", "Correlation_Id"))
+    for k, ds in seen.items():
+        out[k]["dispatches"] = len(ds)
+    return {k: dict(v) for k, v in out.items()}
+
+
 def main():
     d = sys.argv[1]
     ks = kernel_stats(d)
@@ -193,7 +210,20 @@ def main():
         if c.get("SQ_ACTIVE_INST_VALU") is not None and c.get("SQ_WAVE_CYCLES"):
             e["valu_active_frac_of_wave_cycles"] = c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"]
         res[k] = e
-    print(json.dumps({"kernels": res, "inflate_stage": inflate_stage_spans(d)}, indent=1))
+    # every dispatch of the run summed (FETCH x 2, KiB -> B); bench.py's PMC
+    # child decodes the split once, so there this is one pass's HBM traffic
+    # (plus the few header-read dispatches of the open)
+    tf, tw = totals(d, "fetch"), totals(d, "write")
+    run_total = None
+    if tf and tw:
+        per = {k: {"fetch_bytes": tf.get(k, {}).get("FETCH_SIZE", 0) * 2048,
+                   "write_bytes": tw.get(k, {}).get("WRITE_SIZE", 0) * 1024,
+                   "dispatches": int(tf.get(k, {}).get("dispatches", 0))} for k in set(tf) | set(tw)}
+        run_total = {"bytes": sum(v["fetch_bytes"] + v["write_bytes"] for v in per.values()),
+                     "per_kernel": dict(sorted(per.items(), key=lambda kv: -(kv[1]["fetch_bytes"] +
+                                                                           kv[1]["write_bytes"])))}
+    print(json.dumps({"kernels": res, "inflate_stage": inflate_stage_spans(d), "pmc_run_total": run_total},
+                     indent=1))
 
 
 if __name__ == "__main__":

@@ -123,6 +123,7 @@ SYNTH = [
     dict(n_records=500, block_payload=65536 - 1024, level=6),
     dict(n_records=3000, block_payload=65536, level=6),  # ISIZE 65536: phase-B round path
     dict(n_records=3000, block_payload=65280, level=1),  # ISIZE at the map limit
+    dict(n_records=20000, mode="wgs"),                   # C3's binned-quality model
 ]
 
 

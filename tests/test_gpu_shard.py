@@ -15,6 +15,7 @@ pytestmark = pytest.mark.gpu
     (2, 4096, dict(n_records=40000)),
     (4, 7, dict(n_records=30000, block_payload=4096)),
     (3, 3, dict(n_records=60, mode="long")),
+    (8, 4096, dict(n_records=120000)),                   # the 8-GPU node's rank count (all on cuda:0)
 ])
 def test_gpu_sharded_read_matches_whole_file(tmp_path, world, g, kw):
     """Each rank opens the file by path (split-local) and decodes its split
@@ -63,6 +64,7 @@ def _strong_worker(rank, world, port, path, outdir, granularity):
     (3, 4096, dict(n_records=50000)),
     (4, 5, dict(n_records=20000, block_payload=4096)),
     (2, 2, dict(n_records=40, mode="long")),
+    (8, 4096, dict(n_records=120000, mode="wgs")),       # 8 ranks over C3's model
 ])
 def test_gpu_strong_split_digests_and_index(tmp_path, world, g, kw):
     """One file split over the ranks (bench.py --workload c3): the ranks'

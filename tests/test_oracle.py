@@ -112,7 +112,8 @@ def test_key_edge_cases():
 
 
 @pytest.mark.parametrize("kw", [dict(n_records=1500), dict(n_records=60, mode="long"), dict(n_records=800, level=0),
-                                dict(n_records=800, strategy="fixed"), dict(n_records=400, all_unmapped=True)])
+                                dict(n_records=800, strategy="fixed"), dict(n_records=400, all_unmapped=True),
+                                dict(n_records=1500, mode="wgs")])
 def test_oracle_vs_python_synthetic(kw):
     from hbam import synth
     d, _ = synth.make_bam(**kw)

@@ -141,6 +141,8 @@ def test_merge_empty_splits_follows_reference():
     (3, 7, dict(n_records=4000, block_payload=4096)),          # many straddling records
     (4, 1, dict(n_records=1500, block_payload=8192, level=1)),
     (2, 5, dict(n_records=12, mode="long")),                     # records spanning many blocks
+    (8, 4096, dict(n_records=24000)),                            # the 8-GPU node's rank count
+    (8, 3, dict(n_records=3000, block_payload=4096)),            # 8 ranks, straddles at every split
 ])
 def test_sharded_read_matches_whole_file(tmp_path, world, g, kw):
     data, _ = synth.make_bam(**kw)
