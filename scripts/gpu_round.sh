@@ -67,6 +67,13 @@ for s in $STEPS; do
           > $OUT/dropin_env_$e.log 2>&1 || { echo "dropin probe failed"; tail -30 $OUT/dropin_env_$e.log; exit 6; }
         echo "env $e"; grep -E "^(mapped|resident)" $OUT/dropin_env_$e.log | cut -c1-140
       done ;;
+    orderenvs)
+      # the drop-in loop before and after hbam_gpu_run_streamed under each VAR=VALUE of ENVS
+      for e in ${ENVS:-NONE=0}; do
+        env $e timeout -k 10 300 python -u scripts/dropin_probe2.py 10000000 --torch --steps none,run_streamed,none,none \
+          > $OUT/orderenv_$e.log 2>&1 || { echo "order probe failed"; tail -30 $OUT/orderenv_$e.log; exit 9; }
+        echo "env $e"; grep -E "^(mapped|resident)" $OUT/orderenv_$e.log | cut -c1-110
+      done ;;
     order)
       # the drop-in loop before and after hbam_gpu_run_streamed (the pinned-host leg), clocks and link sampled
       timeout -k 10 400 python -u scripts/dropin_probe2.py 10000000 --torch --smi --steps none,run_streamed,none,none \
@@ -122,5 +129,10 @@ for s in $STEPS; do
       timeout -k 10 600 python -u bench.py --gpus 2 --dist-backend gloo --one-device --c3-gb 7 --steps 3 --warmup 1 \
         > $OUT/rehearsal.json 2> $OUT/rehearsal.err || { echo "rehearsal failed"; tail -30 $OUT/rehearsal.err; exit 3; }
       cat $OUT/rehearsal.json ;;
+    rehearsal8)
+      # the driver's 8-GPU sequence with 8 gloo ranks sharing this box's one GPU
+      timeout -k 10 900 python -u bench.py --gpus 8 --dist-backend gloo --one-device --c3-gb 4 --steps 3 --warmup 1 \
+        > $OUT/rehearsal8.json 2> $OUT/rehearsal8.err || { echo "rehearsal8 failed"; tail -30 $OUT/rehearsal8.err; exit 3; }
+      cat $OUT/rehearsal8.json ;;
   esac
 done
