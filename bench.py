@@ -270,7 +270,7 @@ def pmc_traffic(path, vstart, vend, kernel):
 # ---------------------------------------------------------------------------
 # side legs (N=1, rank 0)
 # ---------------------------------------------------------------------------
-def dropin_leg(path, first, records):
+def dropin_leg(path, first, records, short=False):
     """The call a JVM makes (hbam.h): hbam_open(path) maps the file (with
     opts.batch_records = the batch size, as GpuBAMRecordReader passes it, so
     the page-locked batch slots are pinned on a helper thread from the open
@@ -281,10 +281,11 @@ def dropin_leg(path, first, records):
     page-locked batch buffers (device blocks may come from the process cache,
     hbam_mem.h, filled by the decodes before), the second finds both cached
     -- the case of an executor that reads many splits.  seconds = the batch
-    loop; open_seconds = the hbam_open before it (header read)."""
+    loop; open_seconds = the hbam_open before it (header read).  short: the
+    1 M-record batches only (the later placements of the leg)."""
     import hbam
     res = {}
-    for label, batch in (("batches_64K", 1 << 16), ("batches_1M", 1 << 20)):
+    for label, batch in ((("batches_64K", 1 << 16),) if not short else ()) + (("batches_1M", 1 << 20),):
         for run in ("first_open", "second_open"):
             t0 = time.perf_counter()
             with hbam.BamFile(path=path, batch_records=batch) as f:
@@ -297,6 +298,8 @@ def dropin_leg(path, first, records):
                 "records": n, "batches": k, "rest_bytes_to_host": nbytes, "seconds": round(dt, 3),
                 "open_seconds": round(t - t0, 4),
                 "uncompressed_GBps": round(u / dt / 1e9, 3), "records_per_s": round(n / dt, 1)}
+    if short:
+        return res
     # the same 1 M-record loop with the file read through hbam_open_reader (a
     # positioned-read callback, as a Hadoop FSDataInputStream through JNI):
     # here os.pread in Python, one call at a time
@@ -909,6 +912,13 @@ def run_c2(D, args, steps, warmup, extras):
                         out["roofline"]["traffic_error"] = tr["error"]
                 except Exception as e:
                     out["roofline"]["traffic_error"] = repr(e)
+                if want("dropin_end_to_end"):
+                    # the same loop again after the PMC child processes (DESIGN.md 7 item 5:
+                    # some earlier GPU work slows a later drop-in loop of the process)
+                    try:
+                        extra["dropin_after_pmc"] = dropin_leg(path, first, n_all, short=True)
+                    except Exception as e:
+                        extra["dropin_after_pmc"] = {"error": repr(e)}
             if not args.no_extra:
                 # (the pinned-host leg runs last of all, in main())
                 for name, fn in (("write_path", lambda: write_legs(path, size, u_file)),
@@ -1098,6 +1108,13 @@ def main():
             try:
                 size, _ = build_shared_bam(path, 0, 1, args.records, D.all_gather, D.barrier)
                 ph = pinned_host_leg(path, args.records)
+                if args.extras is None or "dropin_end_to_end" in args.extras:
+                    # the drop-in loop once more, after hbam_gpu_run_streamed ran in this process
+                    import hbam
+                    with hbam.BamFile(path=path) as f:
+                        first = f.header()["first_record_voff"]
+                    line.setdefault("extra", {})["dropin_after_run_streamed"] = dropin_leg(path, first, args.records,
+                                                                                         short=True)
             except Exception as e:
                 ph = {"error": repr(e)}
             finally:

@@ -790,6 +790,16 @@ enum { LD_SPEC = 0, LD_SYNC = 1, LD_EMIT = 2 };
 #endif
 constexpr uint32_t kMergeFirst = HBAM_MERGE_FIRST;  // power of two
 static_assert((kMergeFirst & (kMergeFirst - 1)) == 0, "kMergeFirst: a power of two");
+// Slices shorter than this many bits (a short last DEFLATE block) take their
+// boundaries at kMergeFirst / 2 << k instead (0: never)
+#ifndef HBAM_MERGE_SHORT_BITS
+#define HBAM_MERGE_SHORT_BITS 0
+#endif
+constexpr uint32_t kMergeShortBits = HBAM_MERGE_SHORT_BITS;
+#ifndef HBAM_MERGE_TINY_BITS
+#define HBAM_MERGE_TINY_BITS 0
+#endif
+constexpr uint32_t kMergeTinyBits = HBAM_MERGE_TINY_BITS;  // ... kMergeFirst / 4 << k below this
 struct MergePts {
   uint32_t p0, p1, p2, p3;
   uint32_t b0, b1, b2, b3;
@@ -812,7 +822,7 @@ template <int MODE>
 __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t* __restrict__ W, uint32_t a,
                                                 uint32_t stop, uint32_t E, uint32_t& x, uint32_t& nt, uint32_t& nb,
                                                 MergePts& mp, uint32_t& mj, uint32_t* __restrict__ tok,
-                                                uint32_t out0, uint32_t isize) {
+                                                uint32_t out0, uint32_t isize, uint32_t mf = kMergeFirst) {
   constexpr bool EMIT = MODE == LD_EMIT;
   uint32_t wd, cnt, nx;
   uint64_t buf;
@@ -862,17 +872,17 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
     }                                                                                       \
     ++nt;                                                                                   \
     nb += (len_);                                                                           \
-    if (MODE == LD_SPEC && (nt & (nt - 1)) == 0 && nt >= kMergeFirst && nt <= 8 * kMergeFirst) { \
+    if (MODE == LD_SPEC && (nt & (nt - 1)) == 0 && nt >= mf && nt <= 8 * mf) {                   \
       /* boundaries after symbols F, 2F, 4F, 8F: the speculative walk has */                \
       /* usually joined the true path by the later ones */                                  \
-      mp.p0 = nt == kMergeFirst ? pos : mp.p0;                                              \
-      mp.b0 = nt == kMergeFirst ? nb : mp.b0;                                               \
-      mp.p1 = nt == 2 * kMergeFirst ? pos : mp.p1;                                          \
-      mp.b1 = nt == 2 * kMergeFirst ? nb : mp.b1;                                           \
-      mp.p2 = nt == 4 * kMergeFirst ? pos : mp.p2;                                          \
-      mp.b2 = nt == 4 * kMergeFirst ? nb : mp.b2;                                           \
-      mp.p3 = nt == 8 * kMergeFirst ? pos : mp.p3;                                          \
-      mp.b3 = nt == 8 * kMergeFirst ? nb : mp.b3;                                           \
+      mp.p0 = nt == mf ? pos : mp.p0;                                              \
+      mp.b0 = nt == mf ? nb : mp.b0;                                               \
+      mp.p1 = nt == 2 * mf ? pos : mp.p1;                                          \
+      mp.b1 = nt == 2 * mf ? nb : mp.b1;                                           \
+      mp.p2 = nt == 4 * mf ? pos : mp.p2;                                          \
+      mp.b2 = nt == 4 * mf ? nb : mp.b2;                                           \
+      mp.p3 = nt == 8 * mf ? pos : mp.p3;                                          \
+      mp.b3 = nt == 8 * mf ? nb : mp.b3;                                           \
     }                                                                                       \
   } while (0)
   // Fast path: while a whole symbol (<= 15+5+15+13 = 48 bits) fits before E,
@@ -903,7 +913,7 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
     const bool g0 = fast_go(pos, nb, hit0);
     merged = g0 & hit0;
     bool act = g0 & !hit0;
-    uint32_t it = 0, ucp = kMergeFirst;  // iterations of this loop, next checkpoint iteration (wave-uniform)
+    uint32_t it = 0, ucp = mf;  // iterations of this loop, next checkpoint iteration (wave-uniform)
     if (__builtin_amdgcn_ballot_w64(act)) do {
       const uint32_t wd = pos >> 5, sh = pos & 31;
       const uint32_t w0 = W[wd], w1 = W[wd + 1], w2 = W[wd + 2];
@@ -967,11 +977,11 @@ __device__ __forceinline__ uint32_t lane_decode(const HuffLds& L, const uint32_t
         // re-entered after the slow path records only where the counts
         // agree; a missing boundary costs its sync walk time, not a result.
         const bool cp = upd & (nt == it);
-        if (it == kMergeFirst) { mp.p0 = cp ? pos : mp.p0; mp.b0 = cp ? nb : mp.b0; }
-        if (it == 2 * kMergeFirst) { mp.p1 = cp ? pos : mp.p1; mp.b1 = cp ? nb : mp.b1; }
-        if (it == 4 * kMergeFirst) { mp.p2 = cp ? pos : mp.p2; mp.b2 = cp ? nb : mp.b2; }
-        if (it == 8 * kMergeFirst) { mp.p3 = cp ? pos : mp.p3; mp.b3 = cp ? nb : mp.b3; }
-        ucp = it == 8 * kMergeFirst ? 0u : 2 * it;
+        if (it == mf) { mp.p0 = cp ? pos : mp.p0; mp.b0 = cp ? nb : mp.b0; }
+        if (it == 2 * mf) { mp.p1 = cp ? pos : mp.p1; mp.b1 = cp ? nb : mp.b1; }
+        if (it == 4 * mf) { mp.p2 = cp ? pos : mp.p2; mp.b2 = cp ? nb : mp.b2; }
+        if (it == 8 * mf) { mp.p3 = cp ? pos : mp.p3; mp.b3 = cp ? nb : mp.b3; }
+        ucp = it == 8 * mf ? 0u : 2 * it;
       }
       bool hit;
       const bool g = fast_go(pos, nb, hit);
@@ -1889,7 +1899,8 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
     const uint32_t stop = tid == kHuffThreads - 1 ? Bend : min(B0 + (tid + 1) * S, Bend);
     MergePts mp;
     uint32_t mj = 0, x, nt, nb;
-    uint32_t ev = lane_decode<LD_SPEC>(L, W, a, stop, E, x, nt, nb, mp, mj, nullptr, 0, 0);
+    const uint32_t mf = S < kMergeTinyBits ? kMergeFirst / 4 : S < kMergeShortBits ? kMergeFirst / 2 : kMergeFirst;
+    uint32_t ev = lane_decode<LD_SPEC>(L, W, a, stop, E, x, nt, nb, mp, mj, nullptr, 0, 0, mf);
     const uint32_t sx = x, snt = nt, snb = nb, sev = ev;
     for (;;) {  // sync: restart each slice from its predecessor's exit
       if (lane == 63) {
@@ -1907,12 +1918,12 @@ __device__ __forceinline__ void huff_block(uint8_t* smem, const uint8_t* __restr
       if (need) {
         a = px;
         uint32_t rx, rnt, rnb;
-        const uint32_t rev = lane_decode<LD_SYNC>(L, W, a, stop, E, rx, rnt, rnb, mp, mj, nullptr, 0, 0);
+        const uint32_t rev = lane_decode<LD_SYNC>(L, W, a, stop, E, rx, rnt, rnb, mp, mj, nullptr, 0, 0, mf);
         if (rev == EV_MERGE) {  // shares the speculative walk from boundary mj on
           const uint32_t bj = mj == 0 ? mp.b0 : mj == 1 ? mp.b1 : mj == 2 ? mp.b2 : mp.b3;
           x = sx;
           ev = sev;
-          nt = rnt + snt - (kMergeFirst << mj);
+          nt = rnt + snt - (mf << mj);
           nb = rnb + snb - bj;
         } else {
           x = rx;

@@ -36,6 +36,15 @@ def main():
         e = stats[phase][(eng, etype, cls)]
         e[0] += 1
         e[1] += size
+    if not stats:  # no copy line in the expected format: show what the log holds about copies
+        from collections import Counter
+        seen = Counter()
+        for ln in open(sys.argv[1], errors="replace"):
+            if "opy" in ln or "SDMA" in ln or "engine" in ln:
+                seen[re.sub(r"0x[0-9a-fA-F]+|\d+", "#", ln.strip())[:160]] += 1
+        print("no 'HSA Copy copy_engine=' lines; most common copy-related line shapes:")
+        for shape, n in seen.most_common(25):
+            print(f"  {n:7d}  {shape}")
     for ph in order:
         if ph not in stats:
             continue

@@ -74,6 +74,18 @@ for s in $STEPS; do
           > $OUT/orderenv_$e.log 2>&1 || { echo "order probe failed"; tail -30 $OUT/orderenv_$e.log; exit 9; }
         echo "env $e"; grep -E "^(mapped|resident)" $OUT/orderenv_$e.log | cut -c1-110
       done ;;
+    concurrent)
+      # K FileVirtualSplits of C2 decoded at once by K contexts of one process (K map tasks per GPU)
+      timeout -k 10 300 python -u scripts/concurrent_probe.py 10000000 ${KS:-1,2,3,4} > $OUT/concurrent.log 2>&1 \
+        || { echo "concurrent probe failed"; tail -30 $OUT/concurrent.log; exit 13; }
+      timeout -k 10 300 python -u scripts/concurrent_probe.py 10000000 ${KS:-1,2,3,4} --procs > $OUT/concurrent_procs.log 2>&1 \
+        || { echo "concurrent probe (processes) failed"; tail -30 $OUT/concurrent_procs.log; exit 13; }
+      cat $OUT/concurrent.log $OUT/concurrent_procs.log ;;
+    fetchcalib)
+      # FETCH_SIZE against the line bytes of known sparse access shapes (scripts/fetch_calib.hip)
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fcal \
+        -o run -- $R/scripts/bin/fetch_calib > $OUT/fcal.log 2>&1) || { echo "fetch calib failed"; tail -20 $OUT/fcal.log; exit 14; }
+      python3 scripts/fetch_calib_summary.py $OUT/fcal $OUT/fcal.log | tee $OUT/fcal_summary.txt ;;
     order)
       # the drop-in loop before and after hbam_gpu_run_streamed (the pinned-host leg), clocks and link sampled
       timeout -k 10 400 python -u scripts/dropin_probe2.py 10000000 --torch --smi --steps none,run_streamed,none,none \
