@@ -793,7 +793,7 @@ static_assert((kMergeFirst & (kMergeFirst - 1)) == 0, "kMergeFirst: a power of t
 // Slices shorter than this many bits (a short last DEFLATE block) take their
 // boundaries at kMergeFirst / 2 << k instead (0: never)
 #ifndef HBAM_MERGE_SHORT_BITS
-#define HBAM_MERGE_SHORT_BITS 0
+#define HBAM_MERGE_SHORT_BITS 400
 #endif
 constexpr uint32_t kMergeShortBits = HBAM_MERGE_SHORT_BITS;
 #ifndef HBAM_MERGE_TINY_BITS

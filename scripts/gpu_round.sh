@@ -107,7 +107,8 @@ for s in $STEPS; do
     engines)
       # HIP log at level 4 (all categories; the copy lines name their engine): which DMA engine each copy of the drop-in loop
       # took, before and after hbam_gpu_run_streamed (the slowed next context)
-      AMD_LOG_LEVEL=4 AMD_LOG_MASK=0x7fffffff timeout -k 10 400 python -u scripts/dropin_probe2.py 10000000 --torch \
+      # (without torch: libhbam then loads /opt/rocm's HIP runtime, whose copy log names the engine)
+      AMD_LOG_LEVEL=4 AMD_LOG_MASK=0x7fffffff timeout -k 10 400 python -u scripts/dropin_probe2.py 10000000 \
         --steps none,run_streamed,none > $OUT/engines.log 2>&1 || { echo "engines probe failed"; tail -20 $OUT/engines.log; exit 12; }
       python3 scripts/engine_summary.py $OUT/engines.log > $OUT/engines.txt 2>&1
       grep -i "copy" $OUT/engines.log | head -c 2000000 > $OUT/engines_copylines.txt || true
