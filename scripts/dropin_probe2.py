@@ -1,6 +1,6 @@
 """Per-batch timing of the drop-in call (developer probe): hbam_decode_span in 1M-record
 batches from the mapped file and from a resident copy, every batch timed.
-usage: python scripts/dropin_probe2.py [records] [--torch] [--pinned] [--smi] [--steps a,b+c,...]"""
+usage: python scripts/dropin_probe2.py [records] [--torch] [--pinned] [--smi] [--numa] [--steps a,b+c,...]"""
 import os
 import sys
 import time
@@ -105,6 +105,34 @@ class Sampler:
 SMI = None
 
 
+def numa_summary(label):
+    """--numa: where the process's large anonymous mappings (the page-locked
+    batch slots and bounce buffers among them) have their pages, from
+    /proc/self/numa_maps (pages per node), and the GPU's node."""
+    import glob
+    gnode = "?"
+    for f in glob.glob("/sys/class/drm/card*/device/numa_node"):
+        try:
+            gnode = open(f).read().strip()
+            break
+        except OSError:
+            pass
+    rows = []
+    try:
+        for ln in open("/proc/self/numa_maps"):
+            if "anon=" not in ln and "file=/dev/shm" not in ln:
+                continue
+            nodes = {k: int(v) for k, v in (t.split("=") for t in ln.split() if t[:1] == "N" and "=" in t)}
+            kb = 2048 if "kernelpagesize_kB=2048" in ln else 4
+            tot = sum(nodes.values()) * kb
+            if tot >= 64 * 1024:
+                rows.append(f"{ln.split()[0]}:{'shm' if 'file=' in ln else 'anon'}:"
+                            + ",".join(f"{k}={v * kb // 1024}M" for k, v in sorted(nodes.items())))
+    except OSError as e:
+        rows.append(repr(e))
+    print(f"NUMA {label} gpu_node={gnode} " + " ".join(rows), flush=True)
+
+
 def batches(f, first, nrec):
     b = hbam.Batch()
     v, ts, n = first, [], 0
@@ -169,6 +197,8 @@ def main():
                 elif what == "dummy_decode":  # a context that decodes one small batch
                     with hbam.BamFile(path=path) as fd:
                         batches(fd, fd.header()["first_record_voff"], 1 << 16)
+                elif what == "rates":  # torch's own pinned H2D / D2H copy rates (4 GiB), device-wide state
+                    print("RATES", link_rates(), flush=True)
                 elif what == "release":  # every cached device / page-locked block back to HIP
                     print("released", hbam.release_cached_memory(), flush=True)
                 elif what.startswith("sleep"):  # idle seconds: a transient device state would wear off
@@ -192,6 +222,8 @@ def main():
                     del raw
             print("after", step, flush=True)
             with hbam.BamFile(path=path, batch_records=1 << 20) as f:
+                if "--numa" in sys.argv:
+                    numa_summary(f"rep{rep}_open")
                 first = f.header()["first_record_voff"]
                 mark(f"mapped{rep}_begin")
                 if SMI:
@@ -204,7 +236,12 @@ def main():
                 mark(f"mapped{rep}_end")
                 print(f"mapped rep {rep}: {m} records {dt:.3f}s {info['uncompressed'] / dt / 1e9:.1f} GB/s batches ms {ts}",
                       flush=True)
+                if "--numa" in sys.argv:
+                    numa_summary(f"rep{rep}_after_loop")
+                t = time.perf_counter()
                 f.prefetch(0, f.size)
+                dtp = time.perf_counter() - t
+                print(f"prefetch rep {rep}: {f.size / dtp / 1e9:.1f} GB/s host feed ({dtp * 1e3:.1f} ms)", flush=True)
                 t = time.perf_counter()
                 m, ts = batches(f, first, 1 << 20)
                 dt = time.perf_counter() - t

@@ -91,6 +91,21 @@ for s in $STEPS; do
       timeout -k 10 400 python -u scripts/dropin_probe2.py 10000000 --torch --smi --steps none,run_streamed,none,none \
         > $OUT/order.log 2>&1 || { echo "order probe failed"; tail -30 $OUT/order.log; exit 9; }
       grep -E "^(mapped|resident|SMI)" $OUT/order.log | cut -c1-260 ;;
+    ordernuma)
+      # the order probe with the NUMA placement of the process's large mappings before and after each loop
+      timeout -k 10 400 python -u scripts/dropin_probe2.py 10000000 --numa --steps none,run_streamed,none,none \
+        > $OUT/ordernuma.log 2>&1 || { echo "order probe failed"; tail -30 $OUT/ordernuma.log; exit 9; }
+      grep -E "^(mapped|resident|NUMA)" $OUT/ordernuma.log | cut -c1-600 ;;
+    orderrates)
+      # torch's pinned copy rates beside the order probe's loops: is the slow state device-wide?
+      timeout -k 10 400 python -u scripts/dropin_probe2.py 10000000 --torch --steps rates,run_streamed+rates,rates,rates \
+        > $OUT/orderrates.log 2>&1 || { echo "order probe failed"; tail -30 $OUT/orderrates.log; exit 9; }
+      grep -E "^(mapped|resident|RATES|prefetch)" $OUT/orderrates.log | cut -c1-300 ;;
+    ordersteps)
+      # which prior action triggers the slow mapped loop (STEPS: dropin_probe2 --steps list)
+      timeout -k 10 500 python -u scripts/dropin_probe2.py 10000000 --torch --steps ${STEPS_LIST:-none,pinned_buffer,none,reload_pinned,none,none} \
+        > $OUT/ordersteps.log 2>&1 || { echo "order probe failed"; tail -30 $OUT/ordersteps.log; exit 9; }
+      grep -E "^(after|mapped|resident|prefetch)" $OUT/ordersteps.log | cut -c1-160 ;;
     ordertrace)
       # the same with the host-side timeline (HBAM_CURSOR_TRACE) of each loop
       HBAM_CURSOR_TRACE=1 timeout -k 10 400 python -u scripts/dropin_probe2.py 10000000 --torch \
