@@ -39,6 +39,13 @@ def main():
         if k in di:
             rows.append(row("C2", f"MI355X, drop-in hbam_open(path) + hbam_decode_span 1M batches -> pinned host "
                                   f"({k.replace('_', ' ')})", "1 GPU", c2c, c2u, n, di[k]["seconds"]))
+    for leg, where in (("dropin_after_pmc", "after the PMC child runs"),
+                       ("dropin_after_run_streamed", "after hbam_gpu_run_streamed")):
+        dj = (ex.get(leg) or {}).get("batches_1M") or {}
+        for k in ("first_open", "second_open"):
+            if k in dj:
+                rows.append(row("C2", f"MI355X, drop-in 1M batches, {where} ({k.replace('_', ' ')})", "1 GPU",
+                                c2c, c2u, n, dj[k]["seconds"]))
     c4 = ex.get("c4_long_reads") or {}
     if "seconds" in c4:
         rows.append(row("C4", "MI355X, resident", "1 GPU", c4["compressed_bytes"], c4["uncompressed_bytes"],
