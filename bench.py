@@ -441,6 +441,14 @@ def compose_digests(parts):
     return n, kd, vd
 
 
+def bound_of(limits):
+    """roofline.bound from the measured limits (fractions of each unit's
+    peak): the largest one's unit when it reaches BOUND_MIN, else "latency"
+    (no unit saturated: the kernel's dependent chain sets its pace)."""
+    top = max(limits, key=limits.get)
+    return top.replace("hbm_traffic", "hbm") if limits[top] >= BOUND_MIN else "latency"
+
+
 def roofline_of(stats, world=1):
     """The roofline object of the dominant kernel from measurement passes
     (every inflate launch between its own HIP events on one stream: kernel
@@ -881,8 +889,7 @@ def run_c2(D, args, steps, warmup, extras):
                                    "hbm_traffic": tr["bytes_per_launch"] / (rf["avg_launch_ms"] * 1e-3) / 1e9
                                    / HBM_PEAK_GBS}
                             rf["limits"] = {k: round(v, 4) for k, v in lim.items()}
-                            top = max(lim, key=lim.get)
-                            rf["bound"] = top.replace("hbm_traffic", "hbm") if lim[top] >= BOUND_MIN else "latency"
+                            rf["bound"] = bound_of(lim)
                             rf["bound_rule"] = (f"the largest of: algorithmic HBM bytes / peak (frac), measured "
                                                 f"HBM traffic / peak, VALU and SALU issue fractions and the "
                                                 f"LDS-array busy fraction (issue), when it is >= {BOUND_MIN}; "

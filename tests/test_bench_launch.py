@@ -55,3 +55,17 @@ def test_inflate_rounds_match_the_library():
     rounds = int(re.search(r"#define HBAM_INFLATE_ROUNDS (\d+)", src).group(1))
     bench = open(BENCH).read()
     assert int(re.search(r"^INFLATE_ROUNDS = (\d+)", bench, re.M).group(1)) == rounds
+
+
+def test_roofline_bound_names_a_unit_only_when_it_is_near_saturation():
+    """roofline.bound: the largest measured limit's unit when it reaches 0.7,
+    "latency" when no unit is near its peak (round-5 verdict: 0.46 of the LDS
+    array is not an LDS bound)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.BOUND_MIN == 0.7
+    lim = {"hbm": 0.08, "valu_issue": 0.39, "salu_issue": 0.14, "lds": 0.46, "hbm_traffic": 0.13}
+    assert bench.bound_of(lim) == "latency"
+    assert bench.bound_of(dict(lim, lds=0.85)) == "lds"
+    assert bench.bound_of(dict(lim, hbm_traffic=0.72)) == "hbm"
+    assert bench.bound_of(dict(lim, valu_issue=0.7)) == "valu_issue"

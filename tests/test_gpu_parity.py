@@ -271,3 +271,21 @@ def test_c4_long_reads_vs_oracle():
         assert_same_records(got, want, s.data)
         for gran in (1, 5, 4096):
             assert f.splitting_index(gran) == s.splitting_index(gran)
+
+
+def test_inflate_token_count_is_consistent():
+    """hbam_inflate_token_count (the bench's phase-A traffic denominator):
+    the LZ77 tokens of the last pass lie between U / 258 (every token a
+    longest match) and U (every token one literal), and a second pass over the
+    same span writes the same number."""
+    d, _ = synth.make_bam(20000)
+    s = orc.Stream(d)
+    u = len(s.data)
+    with hbam.BamFile(d) as f:
+        first = f.header()["first_record_voff"]
+        st = f.decode_span_device(first, (1 << 64) - 1)
+        t1 = f.inflate_token_count()
+        assert st["records"] == 20000
+        assert u // 258 <= t1 <= u, (t1, u)
+        f.decode_span_device(first, (1 << 64) - 1)
+        assert f.inflate_token_count() == t1
