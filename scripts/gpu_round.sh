@@ -157,6 +157,10 @@ for s in $STEPS; do
       timeout -k 10 600 python -u bench.py --gpus 2 --dist-backend gloo --one-device --c3-gb 7 --steps 3 --warmup 1 \
         > $OUT/rehearsal.json 2> $OUT/rehearsal.err || { echo "rehearsal failed"; tail -30 $OUT/rehearsal.err; exit 3; }
       cat $OUT/rehearsal.json ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 \
+        || { echo "smoke failed"; tail -30 $OUT/smoke.log; exit 15; }
+      tail -2 $OUT/smoke.log ;;
     rehearsal8)
       # the driver's 8-GPU sequence with 8 gloo ranks sharing this box's one GPU
       timeout -k 10 900 python -u bench.py --gpus 8 --dist-backend gloo --one-device --c3-gb 4 --steps 3 --warmup 1 \
