@@ -1,12 +1,13 @@
 // dual_sim.c -- host model of phase A with 256 or 512 slices per DEFLATE
 // block (developer probe, not product; symbol walk and true path as in
 // sync_sim.c).  Per 64-lane wave (each lane walking NS/256 slices in
-// lockstep): the speculative walk's length (max over the wave), the first
-// sync iteration's (every slice re-walked from its true start until it meets
-// a boundary of its speculative walk at symbols mf, 2mf, 4mf, 8mf; mf = 2
-// under 400 bits) and the second iteration's (slices whose predecessor never
-// met its walk).  NOTE: the "round 0" row is the second DEFLATE block of a
-// BGZF block and "round 1" the first (the labels are swapped).
+// lockstep): the speculative walk's length (max over the wave), then every
+// sync iteration until no exit changes (a slice re-walks from its
+// predecessor's latest exit until it meets a boundary of its speculative walk
+// at symbols mf, 2mf, 4mf, 8mf -- mf = 2 under 400 bits -- or passes its
+// stop), each costing the wave's longest re-walk; emit = spec.
+// NOTE: the "2nd" row is the second DEFLATE block of a BGZF block's chunk
+// order as the kernel's round 0 sees it, "1st" the first (labels as printed).
 // Build: gcc -O2 -o scripts/bin/dual_sim scripts/dual_sim.c
 // Run:   scripts/bin/dual_sim <C2-like BAM> [BGZF blocks] [256|512]
 #include <stdint.h>
@@ -153,53 +154,77 @@ static void sim_block(uint64_t b0, uint64_t bend) {
 
 
 static int NSL = 256;  // slices per DEFLATE block
-static double sp_cost[2], sy_cost[2], nwaves[2], sym_tot[2], iters2[2];
+static double sp_cost[2], sy_cost[2], nwaves[2], sym_tot[2], iters[2], nblk[2];
 static int cur_round = 0;
 static int walkn(uint64_t g, uint64_t stop, uint64_t* pos, int cap) {
   int n = 0; uint64_t q = g;
   while (q < stop && n < cap) { int eob, k = step(q, &eob); if (!k || eob) break; q += k; pos[n++] = q; }
   return n;
 }
+// walk from g: symbols until reaching a checkpoint of the spec walk (merge) or
+// passing stop; returns symbols walked, *ex = exit (first boundary >= stop)
+static int sync_walk(uint64_t g, uint64_t stop, const uint64_t* sp, int ns, int mf, uint64_t sx, uint64_t* ex) {
+  uint64_t q = g; int n = 0;
+  for (;;) {
+    for (int m = mf; m <= 8 * mf; m *= 2) if (m <= ns && sp[m - 1] == q) { *ex = sx; return n; }
+    if (q >= stop) { *ex = q; return n; }
+    int eob, k = step(q, &eob);
+    if (!k || eob) { *ex = q; return n; }
+    q += k; ++n;
+  }
+}
+static uint64_t SPP[1024][4096];
 static void sim_sync(uint64_t b0, uint64_t bend, const uint8_t* tb) {
   uint64_t R = bend - b0, S = (R + NSL - 1) / NSL;
   int mf = S < 400 ? 2 : 4;
-  static uint64_t sp[4096], tw[4096];
-  int per = NSL / 256;  // walks per lane
-  static int slen[1024], syl[1024], chg[1024];
+  static int ns[1024], lenspec[1024], cost[1024];
+  static uint64_t a_[1024], st[1024], sx[1024], ex[1024], prevx[1024];
+  int nsl = 0;
   for (int sl = 0; sl < NSL; ++sl) {
-    uint64_t a = b0 + sl * S, stop = a + S;
-    slen[sl] = 0; syl[sl] = 0; chg[sl] = 0;
-    if (a >= bend) continue;
-    if (stop > bend) stop = bend;
-    int ns = walkn(a, stop, sp, 4096);
-    slen[sl] = ns;
-    uint64_t t = a;
-    while (t < bend && !((tb[(t - b0) >> 3] >> ((t - b0) & 7)) & 1)) ++t;
-    int nt = walkn(t, stop, tw, 4096);
-    int c = nt; int merged = 0;
-    for (int n = 0; n <= nt; ++n) {
-      uint64_t z = n == 0 ? t : tw[n - 1];
-      int hit = 0;
-      for (int m = mf; m <= 8 * mf; m *= 2) if (m <= ns && sp[m - 1] == z) hit = 1;
-      if (hit) { c = n; merged = 1; break; }
+    a_[sl] = b0 + sl * S; st[sl] = a_[sl] + S;
+    if (a_[sl] >= bend) break;
+    if (st[sl] > bend) st[sl] = bend;
+    ns[sl] = walkn(a_[sl], st[sl], SPP[sl], 4096);
+    sx[sl] = ns[sl] ? SPP[sl][ns[sl] - 1] : a_[sl];
+    // the spec walk's exit: the first boundary >= stop (walkn stops there)
+    ex[sl] = sx[sl];
+    lenspec[sl] = ns[sl];
+    nsl = sl + 1;
+  }
+  int per = NSL / 256;
+  // spec cost per wave
+  for (int w = 0; w < 4; ++w) {
+    int m = 0;
+    for (int l = w * 64; l < w * 64 + 64; ++l) for (int k = 0; k < per; ++k) { int sl = l + 256 * k; if (sl < nsl && lenspec[sl] > m) m = lenspec[sl]; }
+    sp_cost[cur_round] += m; nwaves[cur_round] += 1;
+  }
+  // sync iterations: slice i (> 0) re-walks from ex[i-1] when it differs from where its walk started
+  static uint64_t start[1024];
+  for (int sl = 0; sl < nsl; ++sl) start[sl] = a_[sl];
+  int it = 0;
+  for (;;) {
+    int any = 0;
+    for (int sl = 0; sl < nsl; ++sl) prevx[sl] = ex[sl];
+    for (int sl = 0; sl < nsl; ++sl) cost[sl] = 0;
+    for (int sl = 1; sl < nsl; ++sl) {
+      uint64_t px = prevx[sl - 1];
+      if (px == start[sl]) continue;
+      any = 1;
+      start[sl] = px;
+      uint64_t e;
+      cost[sl] = sync_walk(px, st[sl], SPP[sl], ns[sl], mf, sx[sl], &e);
+      ex[sl] = e;
     }
-    syl[sl] = c; chg[sl] = !merged;
-    sym_tot[cur_round] += nt;
+    if (!any || ++it > 40) break;
+    for (int w = 0; w < 4; ++w) {
+      int m = 0;
+      for (int l = w * 64; l < w * 64 + 64; ++l) for (int k = 0; k < per; ++k) { int sl = l + 256 * k; if (sl < nsl && cost[sl] > m) m = cost[sl]; }
+      sy_cost[cur_round] += m;
+    }
+    iters[cur_round] += 1;
   }
-  for (int w = 0; w < 4; ++w) {
-    int ms = 0, my = 0;
-    for (int l = w * 64; l < w * 64 + 64; ++l)
-      for (int k = 0; k < per; ++k) { int sl = l + 256 * k; if (slen[sl] > ms) ms = slen[sl]; if (syl[sl] > my) my = syl[sl]; }
-    sp_cost[cur_round] += ms; sy_cost[cur_round] += my; nwaves[cur_round] += 1;
-  }
-  // second sync iteration: slices whose predecessor did not merge re-walk from the corrected exit;
-  // approximate its cost by the wave max of syl over those slices
-  for (int w = 0; w < 4; ++w) {
-    int my = 0;
-    for (int l = w * 64; l < w * 64 + 64; ++l)
-      for (int k = 0; k < per; ++k) { int sl = l + 256 * k; if (sl > 0 && chg[sl - 1] && syl[sl] > my) my = syl[sl]; }
-    iters2[cur_round] += my;
-  }
+  nblk[cur_round] += 1;
+  for (int sl = 0; sl < nsl; ++sl) sym_tot[cur_round] += lenspec[sl];
 }
 int main(int argc, char** argv) {
   if (argc < 2) return 2;
@@ -268,9 +293,10 @@ int main(int argc, char** argv) {
     printf("warm-up %3d bits: lane mismatch %.4f  waves with a mismatch %.4f  warm-up symbols/lane %.1f\n", DELTAS[k],
            (double)mism[k] / lanes, (double)wmism[k] / waves, (double)warm_syms[k] / lanes);
   for (int r = 0; r < 2; ++r)
-    printf("round %d, %d slices: per wave spec %.1f  sync(it1) %.1f  sync(it2) %.1f  emit %.1f  symbols/slice %.1f\n", r, NSL,
-           sp_cost[r] / nwaves[r], sy_cost[r] / nwaves[r], iters2[r] / nwaves[r], sp_cost[r] / nwaves[r],
-           sym_tot[r] / (nwaves[r] / 4 * NSL));
+    printf("DEFLATE block %s, %d slices: per wave spec %.1f  sync (all iterations) %.1f  emit %.1f  total %.1f; "
+           "sync iterations per block %.2f, symbols/slice %.1f\n", r ? "1st" : "2nd", NSL, sp_cost[r] / nwaves[r],
+           sy_cost[r] / nwaves[r], sp_cost[r] / nwaves[r], (2 * sp_cost[r] + sy_cost[r]) / nwaves[r],
+           iters[r] / nblk[r], sym_tot[r] / (nblk[r] * NSL));
   return 0;
 }
 // (appended) -- see main2: sync-walk cost model with checkpoint sets
