@@ -223,7 +223,7 @@ int SpanCursor::decode_window(BamFile& f, Carry from, bool cont, uint64_t m, Win
   w->ended = st.ended;
   w->status = st.status;
   w->error = st.error;
-  w->blocks = std::make_shared<const std::vector<BlockInfo>>(p.blocks());
+  w->blocks = std::make_shared<const std::vector<BlockInfo>>(p.blocks().begin(), p.blocks().end());
   w->pack_m = 0;
   if (s.n) {
     const ColLayout L(s.n, true);
@@ -553,7 +553,7 @@ int SpanCursor::next_batch_all(BamFile& f, uint64_t vstart, uint64_t vend, Batch
     ++windows;
     const SpanDev& s = all_step_.span;
     if (s.n) {
-      all_seg_.emplace_back(h.n, std::make_shared<const std::vector<BlockInfo>>(f.pipe().blocks()));
+      all_seg_.emplace_back(h.n, std::make_shared<const std::vector<BlockInfo>>(f.pipe().blocks().begin(), f.pipe().blocks().end()));
       rc = fetch_span(f.pipe(), s, 0, s.n, &h, err);
       if (rc != kOk) return rc;
     }

@@ -429,9 +429,8 @@ int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_sta
   HIPCHK(launch_block_ustart(dblocks_.p + nprev, n, isz_.p, ust_.p, nullptr, &sb, ubase, s));
   HIPCHK(scan_tmp_.reserve(sb + 16));
   HIPCHK(launch_block_ustart(dblocks_.p + nprev, n, isz_.p, ust_.p, scan_tmp_.p, &sb, ubase, s));
-  hblocks_.resize(nprev + n);
-  if (n)
-    HIPCHK(rb(hblocks_.data() + nprev, dblocks_.p + nprev, n * sizeof(BlockInfo), s));
+  HIPCHK(hblocks_.resize(nprev + n));  // (page-locked: k_readback writes it in place)
+  if (n) HIPCHK(launch_readback(hblocks_.data() + nprev, dblocks_.p + nprev, n * sizeof(BlockInfo), s));
   HIPCHK(rb_sync(s));
   *nnew = n;
   return kOk;
@@ -457,10 +456,15 @@ int Pipeline::finish_blocks() {
         dead.push_back(hblocks_[k].ustart);
   }
   HIPCHK(dead_.reserve(dead.size() + 1));
-  if (!dead.empty())
-    HIPCHK(hipMemcpyAsync(dead_.p, dead.data(), dead.size() * 8, hipMemcpyHostToDevice, stream_));
+  // from page-locked memory by a copy kernel: no host wait before the
+  // inflate is planned (hdead_ is rewritten only by the next locate, after
+  // its own read-backs have synchronized stream_)
+  HIPCHK(hdead_.resize(dead.size()));
+  if (!dead.empty()) {
+    memcpy(hdead_.data(), dead.data(), dead.size() * 8);
+    HIPCHK(launch_readback(dead_.p, hdead_.data(), dead.size() * 8, stream_));
+  }
   ndead_ = (uint32_t)dead.size();
-  HIPCHK(rb_sync(stream_));
   return kOk;
 }
 
@@ -550,7 +554,7 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
     lo = tail;
   }
   window_end_ = base_ + len;
-  int rc = finish_blocks();  // waits for the queued inflates (stream_)
+  int rc = finish_blocks();  // (the inflates: ordered before stream_'s next work)
   if (rc != kOk) return rc;
   HIPCHK(flags_.reserve(4));
   const uint32_t none = 0xffffffffu;
@@ -577,6 +581,7 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
 
 int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
   HIPCHK(hipSetDevice(device_));
+  inflate_queued_ = false;
   const uint32_t nblk = (uint32_t)hblocks_.size();
   b1 = std::min(b1, nblk);
   if (b0 >= b1) return kOk;
@@ -695,13 +700,9 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
     times.inflate = times.huff = times.lz77 = times.tables = 0;
     return kOk;
   }
+  inflate_queued_ = true;
   if (!check) return kOk;  // the caller checks hout_ once all blocks are queued
-  HIPCHK(flags_.reserve(4));
-  const uint32_t none = 0xffffffffu;
-  HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags_.p + 3), (int)none, 1, stream_));
-  HIPCHK(launch_first_error_hout(hout_.p, b0, b1 - b0, flags_.p + 3, stream_));
-  uint32_t first = none;
-  HIPCHK(rb(&first, flags_.p + 3, 4, stream_));
+  HIPCHK(queue_inflate_check(b0, b1));
   if (timing) HIPCHK(hipEventRecord(ev_[3], stream_));
   HIPCHK(rb_sync(stream_));
   if (timing) {
@@ -710,16 +711,28 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
     times.huff = huff_ms;
     times.lz77 = lz_ms;
   }
-  if (first != none) {
-    HuffOut ho;
-    HIPCHK(rb(&ho, hout_.p + b0 + first, sizeof ho, stream_));
-    HIPCHK(rb_sync(stream_));
-    for (uint32_t k = b0; k < b1; ++k) inflated_[k] = 0;
-    const BlockInfo& bad = hblocks_[b0 + first];
-    const char* what = ho.status == kErrFormat ? "Did not inflate expected amount" : "invalid DEFLATE data";
-    return fail(ho.status, std::string(what) + " in BGZF block at offset " + std::to_string(bad.coff));
-  }
-  return kOk;
+  return inflate_verdict(b0, b1);
+}
+
+hipError_t Pipeline::queue_inflate_check(uint32_t b0, uint32_t b1) {
+  hipError_t e = flags_.reserve(4);
+  if (e == hipSuccess) e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags_.p + 3), -1, 1, stream_);
+  if (e == hipSuccess) e = launch_first_error_hout(hout_.p, b0, b1 - b0, flags_.p + 3, stream_);
+  infl_first_ = 0xffffffffu;
+  if (e == hipSuccess) e = rb(&infl_first_, flags_.p + 3, 4, stream_);
+  return e;
+}
+
+int Pipeline::inflate_verdict(uint32_t b0, uint32_t b1) {
+  const uint32_t first = infl_first_;
+  if (first == 0xffffffffu) return kOk;
+  HuffOut ho;
+  HIPCHK(rb(&ho, hout_.p + b0 + first, sizeof ho, stream_));
+  HIPCHK(rb_sync(stream_));
+  for (uint32_t k = b0; k < b1; ++k) inflated_[k] = 0;
+  const BlockInfo& bad = hblocks_[b0 + first];
+  const char* what = ho.status == kErrFormat ? "Did not inflate expected amount" : "invalid DEFLATE data";
+  return fail(ho.status, std::string(what) + " in BGZF block at offset " + std::to_string(bad.coff));
 }
 
 uint32_t Pipeline::block_containing(uint64_t pos) const {
@@ -830,7 +843,16 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
   for (int it = 0;; ++it) {
     if (it >= kMaxChainIters) return fail(kErrState, "record chain did not converge");
     after_stop_pending_ = false;  // (only the last iteration's stop counts)
-    int rc = inflate(k0, inf_end);
+    // production runs check the inflate's DEFLATE status with the link
+    // check's read-back (one host round trip fewer; the chain kernels take
+    // any bytes, and their results are not used before the verdict)
+    const bool defer = !timing;
+    int rc = inflate(k0, inf_end, false, !defer);
+    bool check_pending = false;
+    if (rc == kOk && defer && inflate_queued_) {
+      HIPCHK(queue_inflate_check(k0, inf_end));
+      check_pending = true;
+    }
     if (timing) {
       infl_ms += times.inflate;
       huff_ms += times.huff;
@@ -900,12 +922,57 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
       ++shown;
       }
     };
+    uint64_t sm[2] = {0, 0};
+    unsigned long long need = 0;
+    // the lists' record counts scanned into base_arr_ (the output offsets of
+    // k_rec_check_out; their total bounds the span's records) and the list
+    // overflow flag come back with the chain's end in one host round trip
+    HIPCHK(fuse_.reserve(4));
+    uint64_t bound = 0, last_base = 0;
+    uint32_t ovf = 0, last_cnt = 0;
+    auto list_bound = [&]() -> hipError_t {
+      hipError_t e = launch_list_counts(a, stream_);
+      size_t tb = 0;
+      if (e == hipSuccess) e = scan_u32_to_u64(nullptr, &tb, cnt_.p, base_arr_.p, nb, stream_);
+      if (e == hipSuccess) e = scan_tmp_.reserve(tb + 16);
+      a.scan_tmp = scan_tmp_.p;  // (a grown buffer serves the next link check too)
+      if (e == hipSuccess) e = scan_u32_to_u64(scan_tmp_.p, &tb, cnt_.p, base_arr_.p, nb, stream_);
+      if (e == hipSuccess) e = rb(&last_base, base_arr_.p + nb - 1, 8, stream_);
+      if (e == hipSuccess) e = rb(&last_cnt, cnt_.p + nb - 1, 4, stream_);
+      if (e == hipSuccess) e = rb(&ovf, counters_.p + 2, 4, stream_);
+      return e;
+    };
+    // the chain's end: the link max-scan's last entry (read before
+    // list_bound's scan overwrites base_arr_) and the last block's exit
+    uint64_t t[2] = {0, 0};
+    auto chain_end = [&]() -> hipError_t {
+      hipError_t e = rb(&t[0], base_arr_.p + nb - 1, 8, stream_);
+      if (e == hipSuccess) e = rb(&t[1], x2_.p + nb - 1, 8, stream_);
+      return e;
+    };
+    bool spec_bound = false;  // chain end + list bound read with the first link check
     for (int fix = 0;; ++fix) {
       HIPCHK(hipMemsetAsync(counters_.p, 0, 8, stream_));
       HIPCHK(launch_chain(a, mode, kStageLinkCheck, stream_));
       uint32_t ctr[2] = {0, 0};
       HIPCHK(rb(ctr, counters_.p, 8, stream_));
+      // first round: queue the chain end and the list bound as if the link
+      // holds (it does in every production pass: link_rewalks 0); a re-walk
+      // or the serial link recomputes them
+      const bool spec = fix == 0 && !timing;
+      if (spec) {
+        HIPCHK(chain_end());
+        HIPCHK(list_bound());
+      }
       HIPCHK(rb_sync(stream_));
+      if (check_pending) {
+        check_pending = false;
+        if (int vr = inflate_verdict(k0, inf_end)) return vr;
+      }
+      if (spec && ctr[0] == 0 && ctr[1] == 0) {
+        spec_bound = true;
+        break;
+      }
       if (ctr[0] || (ctr[1] && fix == kMaxLinkFix)) {
         if (getenv("HBAM_CURSOR_TRACE"))
           fprintf(stderr, "[chain] serial link: blocks [%u, %u) e_inf %llu e_true %llu p0 %llu rewalk round %d, "
@@ -923,25 +990,6 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
       ++link_rewalks_;
       HIPCHK(launch_chain(a, mode, kStageRewalk, stream_));
     }
-    uint64_t sm[2] = {0, 0};
-    unsigned long long need = 0;
-    // the lists' record counts scanned into base_arr_ (the output offsets of
-    // k_rec_check_out; their total bounds the span's records) and the list
-    // overflow flag come back with the chain's end in one host round trip
-    HIPCHK(fuse_.reserve(4));
-    uint64_t bound = 0, last_base = 0;
-    uint32_t ovf = 0, last_cnt = 0;
-    auto list_bound = [&]() -> hipError_t {
-      hipError_t e = launch_list_counts(a, stream_);
-      size_t tb = 0;
-      if (e == hipSuccess) e = scan_u32_to_u64(nullptr, &tb, cnt_.p, base_arr_.p, nb, stream_);
-      if (e == hipSuccess) e = scan_tmp_.reserve(tb + 16);
-      if (e == hipSuccess) e = scan_u32_to_u64(scan_tmp_.p, &tb, cnt_.p, base_arr_.p, nb, stream_);
-      if (e == hipSuccess) e = rb(&last_base, base_arr_.p + nb - 1, 8, stream_);
-      if (e == hipSuccess) e = rb(&last_cnt, cnt_.p + nb - 1, 4, stream_);
-      if (e == hipSuccess) e = rb(&ovf, counters_.p + 2, 4, stream_);
-      return e;
-    };
     if (serial) {  // exact serial link (writes entry[] + summary), then lists off entry[]
       ++link_fallbacks_;
       HIPCHK(launch_chain(a, mode, kStageSerialLink, stream_));
@@ -950,11 +998,11 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
       HIPCHK(list_bound());
       HIPCHK(rb_sync(stream_));
     } else {  // final chain position = max of every walk exit; no stop
-      uint64_t t[2] = {0, 0};
-      HIPCHK(rb(&t[0], base_arr_.p + nb - 1, 8, stream_));  // (the link max-scan, before list_bound's scan)
-      HIPCHK(rb(&t[1], x2_.p + nb - 1, 8, stream_));
-      HIPCHK(list_bound());
-      HIPCHK(rb_sync(stream_));
+      if (!spec_bound) {
+        HIPCHK(chain_end());
+        HIPCHK(list_bound());
+        HIPCHK(rb_sync(stream_));
+      }
       sm[0] = nb == 1 ? t[1] : std::max(t[0], t[1]);
       sm[1] = 0;
     }

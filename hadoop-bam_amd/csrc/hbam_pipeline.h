@@ -17,6 +17,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstring>
 #include <string>
 #include <thread>
 #include <vector>
@@ -91,6 +92,53 @@ struct DevBuf {
     }
     return e;
   }
+};
+
+// A page-locked host array of a trivially copyable T that kernels read or
+// write in place (k_readback): the block table (54 K entries, 1.7 MB for C2)
+// lands where the host reads it -- no zero fill on resize and no copy out of
+// the read-back bounce buffer, ~0.11 ms of idle GPU per locate
+// (profiles/r06/gaps.txt).
+template <typename T>
+class HostTable {
+ public:
+  HostTable() = default;
+  HostTable(const HostTable&) = delete;
+  HostTable& operator=(const HostTable&) = delete;
+  ~HostTable() {
+    if (p_) pinned_free(p_, bytes_);
+  }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  T* data() { return p_; }
+  const T* data() const { return p_; }
+  T& operator[](size_t i) { return p_[i]; }
+  const T& operator[](size_t i) const { return p_[i]; }
+  const T* begin() const { return p_; }
+  const T* end() const { return p_ + n_; }
+  const T& back() const { return p_[n_ - 1]; }
+  void clear() { n_ = 0; }
+  // keeps the first min(n, size()) elements, the others uninitialised; the
+  // caller has waited for every kernel that reads or writes the array
+  hipError_t resize(size_t n) {
+    if (n > bytes_ / sizeof(T)) {
+      void* q = nullptr;
+      size_t got = 0;
+      const size_t c = std::max(n, n_ + n_ / 2);
+      const hipError_t e = pinned_alloc(&q, c * sizeof(T), &got);
+      if (e != hipSuccess) return e;
+      if (n_) memcpy(q, p_, n_ * sizeof(T));
+      if (p_) pinned_free(p_, bytes_);
+      p_ = static_cast<T*>(q);
+      bytes_ = got;
+    }
+    n_ = n;
+    return hipSuccess;
+  }
+
+ private:
+  T* p_ = nullptr;
+  size_t n_ = 0, bytes_ = 0;
 };
 
 // Result of one span decode, resident on the device.
@@ -186,7 +234,7 @@ class Pipeline {
   // block (split-guess windows); the block chain starts at the first header
   // candidate whose BSIZE chain runs to the window end.
   int locate(bool free_start = false);
-  const std::vector<BlockInfo>& blocks() const { return hblocks_; }
+  const HostTable<BlockInfo>& blocks() const { return hblocks_; }
   uint64_t total_u() const { return total_u_; }
   const BlockInfo* d_blocks() const { return dblocks_.p; }
   // file offset just past the last located block (where the next window starts)
@@ -267,6 +315,12 @@ class Pipeline {
   int locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_start, uint32_t nprev, uint64_t ubase,
                    hipStream_t s, uint32_t* nnew, uint64_t* tail);
   int finish_blocks();  // total_u_, dead positions, pads, per-block state after locate
+  // the first failing block of [b0, b1)'s inflate, read back into
+  // infl_first_ at the next rb_sync; inflate_verdict: its error, if any
+  hipError_t queue_inflate_check(uint32_t b0, uint32_t b1);
+  int inflate_verdict(uint32_t b0, uint32_t b1);
+  uint32_t infl_first_ = 0xffffffffu;
+  bool inflate_queued_ = false;  // the last inflate() queued any chunk
   // SoA store for n records (voff = rec_voff_) + the deferred long-key list
   int alloc_columns(uint64_t n, uint64_t stream_bytes, Columns* c);
   int hip_check(hipError_t e, const char* what);
@@ -303,7 +357,8 @@ class Pipeline {
   uint64_t window_end_ = 0;
 
   DevBuf<BlockInfo> dblocks_;
-  std::vector<BlockInfo> hblocks_;
+  HostTable<BlockInfo> hblocks_;  // read back in place (k_readback)
+  HostTable<uint64_t> hdead_;      // dead positions, copied to dead_ by k_readback
   uint64_t total_u_ = 0;
   uint32_t ndead_ = 0;
   // empty blocks among hblocks_ (counted by the verify kernel), or unknown
