@@ -173,8 +173,8 @@ int decode_device(BamFile& f, uint64_t vstart, uint64_t vend, int32_t flags, hba
       st->ms_decode += p.times.decode;
     }
     if (s.n) {
-      if (first) (void)hipMemcpy(&st->first_voff, s.rec_voff, 8, hipMemcpyDeviceToHost);
-      (void)hipMemcpy(&st->last_voff, s.rec_voff + s.n - 1, 8, hipMemcpyDeviceToHost);
+      if (first) st->first_voff = s.first_voff;
+      st->last_voff = s.last_voff;
       first = false;
       if (digest) {
         uint64_t dg[4];

@@ -3109,8 +3109,21 @@ __device__ __forceinline__ void decode_record(const uint8_t* __restrict__ u, uin
 // the k2 twin) is independent across 16 B blocks, so the 64 lanes do it for
 // 64 consecutive blocks from one coalesced 1 KB load; only the h1/h2 chain is
 // serial, and it runs on wave-uniform values (scalar ALU) fed by readlane.
+// A speculative launch (queued before the host has read k_rec_check_out's
+// verdict) passes a gate: it runs only if no block stopped the span
+// (*bad == ~0) and no record needs bytes past the inflated range; otherwise
+// rec_pos past the stop may be stale and the host launches it again.
+struct SpecGate {
+  const unsigned long long* bad = nullptr;  // nullptr: no gate
+  const unsigned long long* need = nullptr;
+  uint64_t e_inf = 0;
+};
+__device__ __forceinline__ bool gate_closed(const SpecGate& g) {
+  return g.bad && (*g.bad != ~0ull || *g.need > g.e_inf);
+}
 __global__ __launch_bounds__(64) void k_long_hash(const uint8_t* __restrict__ u, const uint64_t* __restrict__ rec_pos,
-                                                  Columns col) {
+                                                  Columns col, SpecGate gate) {
+  if (gate_closed(gate)) return;
   const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
   const uint32_t lane = lane_id();
   const uint32_t nrec = min(*col.long_n, col.long_cap);
@@ -3733,8 +3746,9 @@ __global__ void k_sbi_emit(const uint64_t* __restrict__ voff, uint64_t n, uint32
 // the chain successor of the last record of a span: where the next window
 // (or the next batch of a split) resumes
 __global__ void k_next_pos(const uint8_t* __restrict__ u, const uint64_t* __restrict__ rec_pos, uint64_t n,
-                           uint64_t p0, int mode, uint64_t* __restrict__ out) {
+                           uint64_t p0, int mode, uint64_t* __restrict__ out, SpecGate gate) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (gate_closed(gate)) return;
   if (n == 0) {
     *out = p0;
     return;
@@ -4252,8 +4266,13 @@ hipError_t launch_sbi_emit(const uint64_t* voff, uint64_t n, uint32_t g, uint64_
   return hipGetLastError();
 }
 hipError_t launch_next_pos(const uint8_t* u, const uint64_t* rec_pos, uint64_t n, uint64_t p0, int mode,
-                           uint64_t* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_next_pos, dim3(1), dim3(64), 0, s, u, rec_pos, n, p0, mode, out);
+                           uint64_t* out, hipStream_t s, const unsigned long long* gate_bad,
+                           const unsigned long long* gate_need, uint64_t gate_e_inf) {
+  SpecGate g;
+  g.bad = gate_bad;
+  g.need = gate_need;
+  g.e_inf = gate_e_inf;
+  hipLaunchKernelGGL(k_next_pos, dim3(1), dim3(64), 0, s, u, rec_pos, n, p0, mode, out, g);
   return hipGetLastError();
 }
 hipError_t launch_readback(void* dst, const void* src, uint64_t n, hipStream_t s) {
@@ -4305,10 +4324,16 @@ hipError_t launch_wr_encode(const uint8_t* u, uint64_t p0, uint64_t nbytes, cons
                      dst);
   return hipGetLastError();
 }
-hipError_t launch_long_hash(const uint8_t* u, const uint64_t* rec_pos, const Columns& col, hipStream_t s) {
+hipError_t launch_long_hash(const uint8_t* u, const uint64_t* rec_pos, const Columns& col, hipStream_t s,
+                            const unsigned long long* gate_bad, const unsigned long long* gate_need,
+                            uint64_t gate_e_inf) {
   if (!col.long_rec || col.long_cap == 0) return hipSuccess;
   const uint32_t grid = std::min<uint32_t>(col.long_cap, 256u * 16u);
-  hipLaunchKernelGGL(k_long_hash, dim3(grid), dim3(64), 0, s, u, rec_pos, col);
+  SpecGate g;
+  g.bad = gate_bad;
+  g.need = gate_need;
+  g.e_inf = gate_e_inf;
+  hipLaunchKernelGGL(k_long_hash, dim3(grid), dim3(64), 0, s, u, rec_pos, col, g);
   return hipGetLastError();
 }
 hipError_t launch_wr_decode(const uint8_t* buf, uint64_t len, const uint64_t* offs, uint64_t n, const Columns& col,

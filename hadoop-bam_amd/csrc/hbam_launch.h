@@ -104,8 +104,11 @@ hipError_t launch_truncate_counts(uint32_t* cnt, uint32_t nb, const uint32_t* cu
 // (ordinals k*g - 1): ent[j] for the j-th such ordinal of the span
 hipError_t launch_sbi_emit(const uint64_t* voff, uint64_t n, uint32_t g, uint64_t o0, uint64_t* ent, hipStream_t s);
 // *out = the chain successor of the last of n records (p0 when n == 0)
+// gate_* (optional): a speculative launch, skipped on the device unless
+// *gate_bad == ~0 and *gate_need <= gate_e_inf (k_rec_check_out's verdict)
 hipError_t launch_next_pos(const uint8_t* u, const uint64_t* rec_pos, uint64_t n, uint64_t p0, int mode,
-                           uint64_t* out, hipStream_t s);
+                           uint64_t* out, hipStream_t s, const unsigned long long* gate_bad = nullptr,
+                           const unsigned long long* gate_need = nullptr, uint64_t gate_e_inf = 0);
 // drop-in batches: records [0, n) of a decoded span -> an export slot
 // (ColLayout with rec_pos; positions rebased by base, dst_pos[n] = nbytes);
 // m > 0: also batch-major column blocks of m records at `packed`
@@ -127,7 +130,9 @@ hipError_t launch_gather_u64(uint64_t* dst, const uint64_t* const* src, int n, h
 // order-sensitive key / voff digests (see k_digest)
 hipError_t launch_digest(const int64_t* keys, const uint64_t* voffs, uint64_t n, uint64_t* out, hipStream_t s);
 // keys deferred by decode_record (rest > kLongHash bytes): one wave per record
-hipError_t launch_long_hash(const uint8_t* u, const uint64_t* rec_pos, const Columns& col, hipStream_t s);
+hipError_t launch_long_hash(const uint8_t* u, const uint64_t* rec_pos, const Columns& col, hipStream_t s,
+                            const unsigned long long* gate_bad = nullptr, const unsigned long long* gate_need = nullptr,
+                            uint64_t gate_e_inf = 0);
 // SAMRecordWritable.write of a span's records: u[p0, p0+nbytes) -> dst
 // (16 B-aligned, room for nbytes rounded up to 16) + bin patches (refID < 0)
 hipError_t launch_wr_encode(const uint8_t* u, uint64_t p0, uint64_t nbytes, const uint64_t* rec_pos,

@@ -368,6 +368,20 @@ int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_sta
   bool serial = count > cap || (count == 0 && len > 0);
   if (free_start && count == 0) return kOk;  // no header in the window: no blocks
   uint32_t n = serial ? 0 : count;
+  // the block table of n located blocks: ustart by a scan, read back in place
+  // into page-locked hblocks_ (the read lands at the next rb_sync)
+  auto queue_table = [&](uint32_t nt) -> int {
+    HIPCHK(dblocks_.grow(nprev + nt + 1));
+    HIPCHK(isz_.reserve(nt + 1));
+    HIPCHK(ust_.reserve(nt + 1));
+    size_t sb = 0;
+    HIPCHK(launch_block_ustart(dblocks_.p + nprev, nt, isz_.p, ust_.p, nullptr, &sb, ubase, s));
+    HIPCHK(scan_tmp_.reserve(sb + 16));
+    HIPCHK(launch_block_ustart(dblocks_.p + nprev, nt, isz_.p, ust_.p, scan_tmp_.p, &sb, ubase, s));
+    HIPCHK(hblocks_.resize(nprev + nt));
+    if (nt) HIPCHK(launch_readback(hblocks_.data() + nprev, dblocks_.p + nprev, nt * sizeof(BlockInfo), s));
+    return kOk;
+  };
   std::vector<uint64_t> starts;  // free start: candidates to try, in order
   if (!serial && n > 0) {
     HIPCHK(dblocks_.grow(nprev + n + 1));
@@ -387,6 +401,11 @@ int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_sta
     uint64_t last = 0;
     HIPCHK(rb(fl, flags_.p + 1, 16, s));
     HIPCHK(rb(&last, sorted_.p + n - 1, 8, s));
+    // the table queued behind the verdict as if the chain holds (a false
+    // header candidate breaks it: the serial walk below then rebuilds the
+    // table); a block cut by hi is the last entry, and the scan's entries
+    // before it do not depend on it
+    if (int rc = queue_table(n)) return rc;
     HIPCHK(rb_sync(s));
     if (!fl[0] && empty_blocks_ != kEmptyUnknown) empty_blocks_ += fl[3];
     if (fl[0]) serial = true;
@@ -394,6 +413,11 @@ int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_sta
     else if (fl[2]) {  // the last candidate's block is cut by hi: next range
       n -= 1;
       *tail = last;
+    }
+    if (!serial) {
+      HIPCHK(hblocks_.resize(nprev + n));  // (drops the cut block's entry)
+      *nnew = n;
+      return kOk;
     }
   }
   if (serial) {
@@ -422,15 +446,7 @@ int Pipeline::locate_range(uint64_t lo, uint64_t hi, bool partial, bool free_sta
       return fail(kErrFormat, "malformed BGZF block");
     }
   }
-  HIPCHK(dblocks_.grow(nprev + n + 1));
-  HIPCHK(isz_.reserve(n + 1));
-  HIPCHK(ust_.reserve(n + 1));
-  size_t sb = 0;
-  HIPCHK(launch_block_ustart(dblocks_.p + nprev, n, isz_.p, ust_.p, nullptr, &sb, ubase, s));
-  HIPCHK(scan_tmp_.reserve(sb + 16));
-  HIPCHK(launch_block_ustart(dblocks_.p + nprev, n, isz_.p, ust_.p, scan_tmp_.p, &sb, ubase, s));
-  HIPCHK(hblocks_.resize(nprev + n));  // (page-locked: k_readback writes it in place)
-  if (n) HIPCHK(launch_readback(hblocks_.data() + nprev, dblocks_.p + nprev, n * sizeof(BlockInfo), s));
+  if (int rc = queue_table(n)) return rc;
   HIPCHK(rb_sync(s));
   *nnew = n;
   return kOk;
@@ -840,6 +856,10 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
   bool fused = false;
   uint64_t fused_total = 0;
   uint32_t fused_first = 0xffffffffu;
+  // the span's tail (deferred long keys + the next record's start) queued
+  // with k_rec_check_out, gated on its verdict, read back with it
+  bool spec_tail = false;
+  uint64_t spec_next = 0, spec_voff[2] = {0, 0};
   for (int it = 0;; ++it) {
     if (it >= kMaxChainIters) return fail(kErrState, "record chain did not converge");
     after_stop_pending_ = false;  // (only the last iteration's stop counts)
@@ -1029,12 +1049,25 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
       a.rec_voff = rec_voff_.p;
       if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
       HIPCHK(launch_rec_check_out(a, mode, dec, c, bound + 1, stream_));
+      const bool spec = !timing;
+      if (spec) {
+        const unsigned long long* gb = reinterpret_cast<const unsigned long long*>(fuse_.p);
+        if (dec) HIPCHK(launch_long_hash(du_.p, rec_pos_.p, c, stream_, gb, need_.p, a.e_inf));
+        HIPCHK(scalars_.reserve(8));
+        HIPCHK(launch_next_pos(du_.p, rec_pos_.p, bound, p0, mode, scalars_.p, stream_, gb, need_.p, a.e_inf));
+        HIPCHK(rb(&spec_next, scalars_.p, 8, stream_));
+        if (bound) {  // (stale unless the gate opens: then unused)
+          HIPCHK(rb(&spec_voff[0], rec_voff_.p, 8, stream_));
+          HIPCHK(rb(&spec_voff[1], rec_voff_.p + bound - 1, 8, stream_));
+        }
+      }
       uint64_t bad = 0;
       uint32_t fl[2] = {0, 0};
       HIPCHK(rb(&need, need_.p, 8, stream_));
       HIPCHK(rb(&bad, fuse_.p, 8, stream_));
       HIPCHK(rb(fl, fuse_.p + 2, 4, stream_));
       HIPCHK(rb_sync(stream_));
+      spec_tail = spec && bad == ~0ull && need <= a.e_inf;
       fused_first = fl[0];
       if (bad == ~0ull) {
         fused_total = bound;  // every block kept its whole list
@@ -1134,13 +1167,23 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
     if (timing) HIPCHK(hipEventRecord(ev_[1], stream_));
     if (dec) HIPCHK(launch_rec_decode(du_.p, rec_pos_.p, total, c, stream_));
   }
-  if (dec) HIPCHK(launch_long_hash(du_.p, rec_pos_.p, c, stream_));
-  // the next record's start: the chain successor of the last record
-  HIPCHK(scalars_.reserve(8));
-  HIPCHK(launch_next_pos(du_.p, rec_pos_.p, total, p0, mode, scalars_.p, stream_));
-  HIPCHK(rb(&out->next_pos, scalars_.p, 8, stream_));
-  if (timing) HIPCHK(hipEventRecord(ev_[2], stream_));
-  HIPCHK(rb_sync(stream_));
+  if (fused && spec_tail) {  // (then total == bound: no block stopped the span)
+    out->next_pos = spec_next;  // (done and read with k_rec_check_out's verdict)
+    out->first_voff = spec_voff[0];
+    out->last_voff = spec_voff[1];
+  } else {
+    if (total) {
+      HIPCHK(rb(&out->first_voff, rec_voff_.p, 8, stream_));
+      HIPCHK(rb(&out->last_voff, rec_voff_.p + total - 1, 8, stream_));
+    }
+    if (dec) HIPCHK(launch_long_hash(du_.p, rec_pos_.p, c, stream_));
+    // the next record's start: the chain successor of the last record
+    HIPCHK(scalars_.reserve(8));
+    HIPCHK(launch_next_pos(du_.p, rec_pos_.p, total, p0, mode, scalars_.p, stream_));
+    HIPCHK(rb(&out->next_pos, scalars_.p, 8, stream_));
+    if (timing) HIPCHK(hipEventRecord(ev_[2], stream_));
+    HIPCHK(rb_sync(stream_));
+  }
   if (after_stop_pending_ && after_stop_flag_) ++records_after_stop_;
   after_stop_pending_ = false;
   after_stop_flag_ = 0;

@@ -150,6 +150,7 @@ struct SpanDev {
   std::string error;
   uint64_t* rec_pos = nullptr;    // device
   uint64_t* rec_voff = nullptr;   // device
+  uint64_t first_voff = 0, last_voff = 0;  // rec_voff[0], rec_voff[n - 1] (host; read back with the span)
   Columns col{};                  // device (reader mode + decode)
   const uint8_t* data = nullptr;  // device stream rec_pos / rest_off index (nullptr = the inflated stream)
 };
