@@ -80,3 +80,58 @@ def test_indexer_list_overflow_takes_the_separate_launches(g, eof_mid):
         c0 = f.pipeline_counters()
         assert f.splitting_index(g) == want
         assert f.pipeline_counters()["record_fallbacks"] > c0["record_fallbacks"]
+
+
+def _with_false_start(n=3000, at=(1000,), seed=3):
+    """A C2-like BAM whose records `at` each carry, as their last tag (B:c),
+    the bytes of another whole record, and a BGZF block that starts exactly
+    there: the block's first plausible record start is that embedded copy,
+    whose chain runs on into the true next record."""
+    d, _ = synth.make_bam(n, seed=seed)
+    s0 = orc.Stream(d)
+    u = bytes(s0.data)
+    h = s0.header_end
+    starts, q = [], h
+    while q < len(u):
+        starts.append(q)
+        q += 4 + struct.unpack_from("<i", u, q)[0]
+    out, cuts, prev = bytearray(u[:h]), [], h
+    for r in sorted(at):
+        a, b = starts[r], starts[r + 1]
+        donor = u[starts[n - 1 - r]:starts[n - r]] if n - r < len(starts) else u[starts[n - 1 - r]:]
+        out += u[prev:a]
+        body = bytearray(u[a + 4:b]) + b"XXBc" + struct.pack("<i", len(donor))
+        cuts.append(len(out) + 4 + len(body))  # the embedded copy's first byte
+        body += donor
+        out += struct.pack("<i", len(body)) + body
+        prev = b
+    out += u[prev:]
+    lens, p = [], 0
+    for c in cuts + [len(out)]:
+        while c - p > 65280:
+            lens.append(65280)
+            p += 65280
+        if c > p:
+            lens.append(c - p)
+            p = c
+    return orc.bgzf_compress(bytes(out), lens, level=5, eof=True)
+
+
+@pytest.mark.parametrize("at", [(1000,), (700, 1400, 2100)])
+def test_false_start_at_a_block_start_is_rewalked(at):
+    """(c) the link check's re-walk round: the speculative list bound queued
+    with the first link check is discarded and recomputed after it."""
+    data = _with_false_start(at=at)
+    s = orc.Stream(data)
+    rc, want = s.decode_all()
+    assert rc == 0 and len(want["key"]) == 3000
+    with hbam.BamFile(data, window_bytes=1 << 30) as f:
+        c0 = f.pipeline_counters()
+        got = f.decode_all()
+        assert_same_records(got, want)
+        c1 = f.pipeline_counters()
+        assert c1["link_rewalks"] + c1["link_fallbacks"] > c0["link_rewalks"] + c0["link_fallbacks"]
+        st = f.decode_span_device(f.header()["first_record_voff"], ALL)
+        assert st["records"] == 3000 and st["status"] == 0
+        assert st["first_voff"] == want["voff"][0] and st["last_voff"] == want["voff"][-1]
+        assert f.splitting_index(5) == s.splitting_index(5)
