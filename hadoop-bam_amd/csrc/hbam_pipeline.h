@@ -124,7 +124,11 @@ class HostTable {
     if (n > bytes_ / sizeof(T)) {
       void* q = nullptr;
       size_t got = 0;
-      const size_t c = std::max(n, n_ + n_ / 2);
+      // at least 1 MiB: smaller page-locked blocks are not cached
+      // (hbam_mem.cpp kMinCached), and hipHostFree waits for the device --
+      // a drop-in context would pay it per window (ramped windows grow the
+      // table several times per split)
+      const size_t c = std::max(std::max(n, n_ + n_ / 2), (size_t(1) << 20) / sizeof(T));
       const hipError_t e = pinned_alloc(&q, c * sizeof(T), &got);
       if (e != hipSuccess) return e;
       if (n_) memcpy(q, p_, n_ * sizeof(T));
