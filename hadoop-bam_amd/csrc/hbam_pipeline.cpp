@@ -563,7 +563,7 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
     // inflate in launches of >= kStreamInflateBlocks blocks: a piece's few
     // thousand blocks alone would leave most CUs idle in each round's tail
     if (nb > queued && (nb - queued >= kStreamInflateBlocks || last)) {
-      rc = inflate(queued, nb, true, false);
+      rc = inflate(queued, nb, true, false, false);  // (phase B beside the next piece's phase A)
       if (rc != kOk) return rc;
       queued = nb;
     }
@@ -595,7 +595,7 @@ int Pipeline::run_streamed(const uint8_t* data, uint64_t len, uint64_t piece, ui
   return kOk;
 }
 
-int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
+int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check, bool join) {
   HIPCHK(hipSetDevice(device_));
   inflate_queued_ = false;
   const uint32_t nblk = (uint32_t)hblocks_.size();
@@ -671,12 +671,15 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
     }
     // rounds: each decode stops a block before its next DEFLATE header, which
     // the next round's table build parses (the last round decodes inline)
+    // (the first chunk's round-0 tables run on stream_ itself: nothing runs
+    // beside them, and a cross-stream wait costs ~15 us at the pass's start)
+    const bool t_own = !serial && j > 0;
     for (uint32_t r = 0; r < kInflateRounds; ++r) {
       HIPCHK(mark());
       HIPCHK(launch_huff_tables(fbase, dblocks_.p, cb, ce - cb, tables_[par].p, tinfo_[par].p, hout_.p, r,
-                                r == 0 ? sT : stream_));
+                                r == 0 && t_own ? sT : stream_));
       HIPCHK(mark());
-      if (r == 0 && !serial) {
+      if (r == 0 && t_own) {
         HIPCHK(hipEventRecord(tab_ev_[par], stream_t_));
         HIPCHK(hipStreamWaitEvent(stream_, tab_ev_[par], 0));
       }
@@ -686,20 +689,24 @@ int Pipeline::inflate(uint32_t b0, uint32_t b1, bool force, bool check) {
                                           stream_));
       HIPCHK(mark());
     }
-    if (!serial) {
-      HIPCHK(hipEventRecord(hdone_ev_[par], stream_));
+    // the last chunk's phase B on stream_ itself: nothing of this call is
+    // left to overlap it, and the chain after it then needs no cross-stream wait
+    const bool b_own = !serial && (j + 1 < nc || !join);
+    hipStream_t sBj = b_own ? sB : stream_;
+    if (!serial) HIPCHK(hipEventRecord(hdone_ev_[par], stream_));
+    if (b_own) {
       HIPCHK(hipEventRecord(sync_ev_[par], stream_));
       HIPCHK(hipStreamWaitEvent(stream_b_, sync_ev_[par], 0));
     }
     HIPCHK(mark());
-    HIPCHK(launch_inflate_lz77(dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, du_.p, sB));
+    HIPCHK(launch_inflate_lz77(dblocks_.p, cb, ce - cb, cu, tokens_[par].p, hout_.p, du_.p, sBj));
     HIPCHK(mark());
-    if (!serial) HIPCHK(hipEventRecord(sync_ev_[2 + par], stream_b_));
+    if (!serial) HIPCHK(hipEventRecord(sync_ev_[2 + par], sBj));
     std::fill(inflated_.begin() + cb, inflated_.begin() + ce, (uint8_t)1);
     ++inflate_launches_;
   }
   if (any && !serial) {  // everything after this call on stream_ sees phase B done
-    HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + ((nc - 1) & 1)], 0));
+    if (!join) HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + ((nc - 1) & 1)], 0));  // (with join it ran on stream_)
     if (nc >= 2) HIPCHK(hipStreamWaitEvent(stream_, sync_ev_[2 + ((nc - 2) & 1)], 0));
   }
   float tab_ms = 0, huff_ms = 0, lz_ms = 0;

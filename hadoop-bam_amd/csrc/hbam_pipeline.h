@@ -247,7 +247,9 @@ class Pipeline {
 
   // Inflate blocks [b0, b1) into the contiguous inflated stream.  check =
   // false leaves the work queued (no DEFLATE error check, no host wait).
-  int inflate(uint32_t b0, uint32_t b1, bool force = false, bool check = true);
+  // join: the last chunk's phase B runs on stream() itself (the caller's next
+  // work needs it); else on the phase-B stream, beside what is queued next.
+  int inflate(uint32_t b0, uint32_t b1, bool force = false, bool check = true, bool join = true);
 
   // End-to-end pass from host memory: the file (same length as the loaded
   // one) is copied to HBM in pieces on a copy stream while the BGZF blocks of
