@@ -3614,6 +3614,8 @@ __device__ __forceinline__ void check_listed_h(const ChainEnv& E, uint64_t q, ui
 //            the inflated range.
 constexpr int kBadShift = 40;
 
+// (4 / 6 / 8 waves per SIMD: 1.116 / 1.065 / 1.052 ms per C2 pass,
+// profiles/r06_late/variants_check_out_waves.log)
 template <int MODE, bool DECODE>
 __global__ __launch_bounds__(64, 6) void k_rec_check_out(ChainEnv E, const uint64_t* __restrict__ entry,
                                                          const uint32_t* __restrict__ wcnt,
