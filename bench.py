@@ -1155,9 +1155,16 @@ def main():
                     "stages_ms": r["stages_ms_rank0"], "windows_rank0": r["windows_rank0"],
                     "roofline": r["roofline"], "cpu_baseline": r["cpu_baseline"]}
         if D.world > 1 and not args.no_extra:
+            # the C3 contexts are closed: their cached device blocks go back to
+            # HIP first (with --one-device the ranks share one GPU's HBM)
+            import gc
+            import hbam
+            gc.collect()
+            hbam.release_cached_memory()
             try:  # the weak-scaling side leg: N x C2, one C2 per rank
                 w = run_c2(D, args, steps=max(3, args.steps // 2), warmup=1, extras=False)
             except Exception as e:
+                log(f"[rank {D.rank}] weak N x C2 leg failed: {e!r}")
                 w = {"error": repr(e)}
             if D.rank == 0:
                 line["extra"] = {"weak_nxc2": w}

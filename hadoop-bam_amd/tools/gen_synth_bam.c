@@ -92,7 +92,9 @@ static void locus(const model *m, uint64_t i, int *ref, int32_t *pos) {
   uint64_t g = (i * m->span) / (m->n_mapped ? m->n_mapped : 1) + (step > 1 ? hash2(0x10c05ULL, i) % step : 0);
   int c = 0;
   while (c < 24 && g >= (uint64_t)kContigLen[c]) { g -= (uint64_t)kContigLen[c]; ++c; }
-  const uint64_t room = m->p->mode == 1 ? 60000 : 200;
+  /* short reads: the first mate's mate starts 200 bp on, and a mate start
+   * must lie inside the contig (STRICT: 1-based start <= length), so 201 */
+  const uint64_t room = m->p->mode == 1 ? 60000 : 201;
   if (g + room > (uint64_t)kContigLen[c]) g = kContigLen[c] > (int32_t)room ? (uint64_t)kContigLen[c] - room : 0;
   *ref = c;
   *pos = (int32_t)g;

@@ -176,3 +176,18 @@ def test_scan_field_and_rest_digests():
         assert r["rest_bytes"] == len(rests) and r["rest_crc"] == zlib.crc32(rests)
     v = want["tlen"]
     assert orc.digest_np(v)[1] == orc.digest([int(x) & ((1 << 64) - 1) for x in v.astype(np.int64)])
+
+
+def test_synthetic_reads_at_a_contig_end_are_valid():
+    """The generator's model at 80 M records (bench.py's weak N x C2 leg at
+    N = 8) walks past chr1's end: the reads placed there, and their mates'
+    starts, stay inside the contig (STRICT: a mate start past the reference
+    length is a SAMFormatException)."""
+    from hbam import synth
+    n, end = 80_000_000, 249_250_621 // 5  # model span: 5 bp per mapped read
+    h, _ = synth.make_bam_segment(n, 0, 0, with_header=True, eof_block=False)
+    seg, _ = synth.make_bam_segment(n, end - 1000, end + 1000, with_header=False, eof_block=True)
+    s = orc.Stream(np.concatenate([h, seg]).tobytes())
+    rc, got = s.decode_span(h.nbytes << 16, (1 << 64) - 1)
+    assert rc == 0 and len(got["key"]) == 2000
+    assert (got["ref_id"] == 0).any() and (got["ref_id"] == 1).any()  # the walk crosses chr1's end
