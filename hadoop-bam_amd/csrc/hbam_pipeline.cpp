@@ -978,6 +978,7 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
       return e;
     };
     bool spec_bound = false;  // chain end + list bound read with the first link check
+    bool early_zeroed = false;  // k_rec_check_out's counters zeroed with them
     for (int fix = 0;; ++fix) {
       HIPCHK(hipMemsetAsync(counters_.p, 0, 8, stream_));
       HIPCHK(launch_chain(a, mode, kStageLinkCheck, stream_));
@@ -990,6 +991,12 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
       if (spec) {
         HIPCHK(chain_end());
         HIPCHK(list_bound());
+        // k_rec_check_out's counters too (they do not depend on the bound):
+        // after the host wait only its launch remains
+        HIPCHK(long_n_.reserve(1));
+        HIPCHK(hipMemsetAsync(long_n_.p, 0, 4, stream_));
+        HIPCHK(hipMemsetAsync(fuse_.p, 0xff, 12, stream_));  // early-stop key, first failing block: none
+        early_zeroed = true;
       }
       HIPCHK(rb_sync(stream_));
       if (check_pending) {
@@ -1046,10 +1053,10 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
       HIPCHK(rec_pos_.reserve(bound + 1));
       HIPCHK(rec_voff_.reserve(bound + 1));
       if (dec) {
-        int rc = alloc_columns(bound, total_u_, &c);
+        int rc = alloc_columns(bound, total_u_, &c, !early_zeroed);
         if (rc != kOk) return rc;
       }
-      HIPCHK(hipMemsetAsync(fuse_.p, 0xff, 12, stream_));  // early-stop key, first failing block: none
+      if (!early_zeroed) HIPCHK(hipMemsetAsync(fuse_.p, 0xff, 12, stream_));  // early-stop key, first failing block: none
       a.fuse_bad = reinterpret_cast<uint64_t*>(fuse_.p);
       a.fuse_flags = fuse_.p + 2;
       a.rec_pos = rec_pos_.p;
@@ -1208,7 +1215,7 @@ int Pipeline::decode_span_pos(uint64_t p0, uint64_t vend, ChainMode mode, bool d
   return kOk;
 }
 
-int Pipeline::alloc_columns(uint64_t total, uint64_t stream_bytes, Columns* cp) {
+int Pipeline::alloc_columns(uint64_t total, uint64_t stream_bytes, Columns* cp, bool zero_long_n) {
   // SoA backing store: 8-byte columns first, then 4, 2, 1 (alignment)
   const uint64_t n = std::max<uint64_t>(total, 1);
   const uint64_t per = 8 * 2 + 4 * 7 + 2 * 3 + 1 * 2;
@@ -1243,7 +1250,7 @@ int Pipeline::alloc_columns(uint64_t total, uint64_t stream_bytes, Columns* cp) 
   const uint64_t cap = std::min<uint64_t>(stream_bytes / kLongHash + 64, 0xffffffffull);
   HIPCHK(long_rec_.reserve(cap));
   HIPCHK(long_n_.reserve(1));
-  HIPCHK(hipMemsetAsync(long_n_.p, 0, 4, stream_));
+  if (zero_long_n) HIPCHK(hipMemsetAsync(long_n_.p, 0, 4, stream_));
   c.long_rec = long_rec_.p;
   c.long_n = long_n_.p;
   c.long_cap = (uint32_t)cap;

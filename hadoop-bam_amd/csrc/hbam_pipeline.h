@@ -329,7 +329,7 @@ class Pipeline {
   uint32_t infl_first_ = 0xffffffffu;
   bool inflate_queued_ = false;  // the last inflate() queued any chunk
   // SoA store for n records (voff = rec_voff_) + the deferred long-key list
-  int alloc_columns(uint64_t n, uint64_t stream_bytes, Columns* c);
+  int alloc_columns(uint64_t n, uint64_t stream_bytes, Columns* c, bool zero_long_n = true);
   int hip_check(hipError_t e, const char* what);
 
   template <typename... B>
