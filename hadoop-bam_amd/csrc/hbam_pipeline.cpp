@@ -17,9 +17,13 @@ namespace hbam {
 namespace {
 constexpr uint32_t kStreamInflateBlocks = 8192;  // run_streamed: blocks per inflate call
 #ifndef HBAM_INFLATE_CHUNK
-#define HBAM_INFLATE_CHUNK 32768
+#define HBAM_INFLATE_CHUNK 65536
 #endif
-constexpr uint32_t kInflateChunkBlocks = HBAM_INFLATE_CHUNK;  // blocks per phase-A/B launch pair (16 K: -0.7 %, 8 K: -4 % on C2)
+// blocks per phase-A/B launch pair: C2's 52 K blocks in one chunk beat two
+// overlapped ones (phase B cannot share a CU with phase A, and each chunk pays
+// its launch tails): 16.07-16.16 vs 16.13-16.25 ms per pass in three A/B runs
+// (profiles/r06_late/variants_chunk_*.log); 20 K: 16.31, 16 K: -0.7 %, 8 K: -4 %
+constexpr uint32_t kInflateChunkBlocks = HBAM_INFLATE_CHUNK;
 constexpr int kMaxChainIters = 64;
 constexpr int kMaxLinkFix = 4;        // re-walk rounds before the serial link
 constexpr int kMaxFreeStarts = 64;    // header candidates tried by a free-start locate
